@@ -1,0 +1,180 @@
+/*
+ * llmi.h — the drop-in C ABI of the MI355X-native GGUF decode path (libllmi.so).
+ *
+ * The reference (zepfu/llama-gguf-inference) has no FFI of its own: it launches the
+ * external llama.cpp `llama-server` (scripts/start.sh:235, argv at :473-494) and
+ * proxies HTTP to it (scripts/gateway.py:699-804).  Inside that binary the decode
+ * loop is driven through llama.cpp's C API (llama.h, upstream, not vendored).  This
+ * header restates that llama.h surface — same names, argument meaning, return codes
+ * and ownership rules — for the functions on the decode path, so a
+ * llama-server-compatible HTTP shim (llmi/server.py) or any ctypes/cgo caller can
+ * bind it the way it would bind libllama.  Structs are llmi's own (llama.h's
+ * carry many more fields), so this is API-shape compatible, not ABI compatible.
+ *
+ * Each entry point names the upstream function it replaces and the reference call
+ * site that reaches it.  llmi_* entries are build extras.
+ *
+ * Threading: a context is NOT thread-safe (one host thread per context).  A model is
+ * read-only and shared by contexts on its device.  No C++ exception crosses the ABI;
+ * failures return NULL / a non-zero code and set the thread-local llmi_last_error().
+ */
+#ifndef LLMI_H
+#define LLMI_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#pragma GCC visibility push(default)
+
+typedef int32_t llama_token;
+typedef int32_t llama_pos;
+typedef int32_t llama_seq_id;
+
+struct llama_model;
+struct llama_context;
+struct llama_vocab;
+
+/* upstream llama_model_params (subset).  n_gpu_layers: llmi is GPU-only; 0 means the
+ * reference's CPU llama-server path (Dockerfile.cpu:84-89, NGL=0) and is rejected —
+ * there is no CPU fallback in the product.  Any value > 0 offloads every layer. */
+struct llama_model_params {
+    int32_t n_gpu_layers;
+    int32_t main_gpu;      /* HIP device index */
+    bool vocab_only;       /* parse metadata + vocab, upload no weights */
+    bool use_mmap;         /* always true in llmi; kept for signature parity */
+    bool no_upload;        /* llmi: build the device arena layout but leave it unfilled
+                              (a replica that will receive the arena by RCCL broadcast) */
+};
+
+/* upstream llama_context_params (subset) */
+struct llama_context_params {
+    uint32_t n_ctx;        /* 0 = model's context_length capped at 4096 */
+    uint32_t n_batch;      /* max tokens per llama_decode call (logical batch) */
+    uint32_t n_ubatch;
+    uint32_t n_seq_max;    /* llmi: 1 sequence per context (one replica = one stream) */
+    int32_t n_threads;     /* ignored (GPU) */
+    bool use_graphs;       /* llmi: replay the decode step as a HIP graph (default true) */
+};
+
+/* upstream llama_batch, field for field */
+struct llama_batch {
+    int32_t n_tokens;
+    llama_token* token;
+    float* embd;           /* unsupported in llmi: must be NULL */
+    llama_pos* pos;        /* NULL: consecutive positions after the context's last token */
+    int32_t* n_seq_id;
+    llama_seq_id** seq_id;
+    int8_t* logits;        /* NULL: logits for the last token only */
+};
+
+/* ---------- lifecycle (upstream llama.h; reached via llama-server startup,
+ *            scripts/start.sh:473-521) ---------- */
+void llama_backend_init(void);
+void llama_backend_free(void);
+struct llama_model_params llama_model_default_params(void);
+struct llama_context_params llama_context_default_params(void);
+/* upstream llama_model_load_from_file (`-m $MODEL`, scripts/start.sh:474). NULL on error. */
+struct llama_model* llama_model_load_from_file(const char* path_model, struct llama_model_params params);
+void llama_model_free(struct llama_model* model);
+/* upstream llama_init_from_model (`-c $CTX`, scripts/start.sh:477). NULL on error. */
+struct llama_context* llama_init_from_model(struct llama_model* model, struct llama_context_params params);
+void llama_free(struct llama_context* ctx);
+
+/* ---------- batches ---------- */
+struct llama_batch llama_batch_get_one(llama_token* tokens, int32_t n_tokens);
+struct llama_batch llama_batch_init(int32_t n_tokens, int32_t embd, int32_t n_seq_max);
+void llama_batch_free(struct llama_batch batch);
+
+/* ---------- decode: THE HOT PATH ----------
+ * upstream llama_decode, called by llama-server's slot loop for every prompt batch
+ * and every generated token of /v1/chat/completions (docs/API_REFERENCE.md:341-605,
+ * proxied by scripts/gateway.py:699-804).
+ * Returns 0 ok; 1 no KV slot (pos >= n_ctx; recoverable); 2 aborted;
+ * -1 invalid batch; < -1 fatal.  Synchronises the device before returning. */
+int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch);
+/* legacy upstream llama_eval: tokens at positions n_past..n_past+n_tokens-1; 0 = ok */
+int llama_eval(struct llama_context* ctx, llama_token* tokens, int32_t n_tokens, int32_t n_past);
+
+/* logits: context-owned host memory, valid until the next decode/free; never freed by
+ * the caller.  i = index in the last batch of a token whose logits were requested,
+ * or -1 for the last one.  NULL (and llmi_last_error) if i had no logits. */
+float* llama_get_logits(struct llama_context* ctx);
+float* llama_get_logits_ith(struct llama_context* ctx, int32_t i);
+
+/* ---------- model / context introspection ---------- */
+const struct llama_vocab* llama_model_get_vocab(const struct llama_model* model);
+int32_t llama_vocab_n_tokens(const struct llama_vocab* vocab);
+llama_token llama_vocab_bos(const struct llama_vocab* vocab);
+llama_token llama_vocab_eos(const struct llama_vocab* vocab);
+/* raw GGUF token text of `token` (no byte-fallback decoding yet: SURVEY.md §8f row 2) */
+const char* llama_vocab_get_text(const struct llama_vocab* vocab, llama_token token);
+int32_t llama_model_n_embd(const struct llama_model* model);
+int32_t llama_model_n_layer(const struct llama_model* model);
+int32_t llama_model_n_head(const struct llama_model* model);
+int32_t llama_model_n_head_kv(const struct llama_model* model);
+int32_t llama_model_n_ctx_train(const struct llama_model* model);
+uint64_t llama_model_size(const struct llama_model* model);  /* tensor bytes */
+int32_t llama_model_desc(const struct llama_model* model, char* buf, size_t buf_size);
+uint32_t llama_n_ctx(const struct llama_context* ctx);
+/* upstream llama_memory_clear / llama_kv_self_clear: reset the KV cache of ctx */
+void llama_kv_self_clear(struct llama_context* ctx);
+
+/* ---------- llmi extras ---------- */
+const char* llmi_last_error(void);
+int32_t llmi_device_count(void);
+/* device-side argmax of the logits of batch entry i (-1 = last); first max wins, as
+ * upstream llama_sampler_greedy.  Avoids the n_vocab*4 B logits copy. */
+llama_token llmi_greedy_ith(struct llama_context* ctx, int32_t i);
+/* Greedy decode of n_gen tokens starting from `first` at position pos0, entirely on
+ * the device (token feedback through the on-device argmax; no host round trip per
+ * token).  out[k] = token sampled after step k.  Returns n_gen or < 0 on error. */
+int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_gen, llama_token* out);
+/* Roofline accounting of the last llama_decode / llmi_generate_greedy call:
+ * algorithmic HBM bytes it streamed and its device time in microseconds. */
+void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec);
+/* Algorithmic bytes of one decode step at KV length n_kv (weights + one embedding row
+ * + norms + KV read/write), the numerator of achieved GB/s. */
+double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv);
+/* Device weight arena (for RCCL broadcast by a caller that owns the communicator). */
+int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64_t* bytes);
+/* In-process replica fan-out: copies model's arena to devices[0..n) with an RCCL
+ * broadcast over xGMI and returns one model handle per device (out[i]). 0 on success. */
+int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_t n, struct llama_model** out);
+
+/* Synthetic GGUF writer: preset = "llama3-8b-q4km", "tinyllama-q8_0",
+ * "mistral7b-q6k", "mistral7b-q5km", "llama3-70b-q4km", or "tiny-mixed" (2 layers, E=256,
+ * all four quant types).  Overrides (0 = preset value): n_layer, n_ctx_train, n_vocab.
+ * Returns bytes written or < 0. */
+int64_t llmi_synth_write_gguf(const char* path, const char* preset, uint64_t seed,
+                              int32_t n_layer, int32_t n_vocab, int32_t n_threads);
+
+/* ---------- kernel-level entry points (tests and microbenchmarks) ----------
+ * All pointers are DEVICE pointers on the current HIP device; the call is enqueued
+ * on the NULL stream and synchronised.  Types are ggml type ids (Q4_K=12, Q5_K=13,
+ * Q6_K=14, Q8_0=8).  `w_dev` holds the weight in llmi's device layout produced by
+ * llmi_repack (identity for Q4_K/Q5_K/F32).  Return 0 on success. */
+int64_t llmi_device_layout_bytes(int32_t type, int64_t rows, int64_t cols);
+int32_t llmi_repack(int32_t type, const void* raw_dev, void* w_dev, int64_t rows, int64_t cols);
+/* y = W . quantize(norm_w ? rmsnorm(x)*norm_w : x); mode 0 store, 1 accumulate (y += .) */
+int32_t llmi_matvec(int32_t type, const void* w_dev, int64_t rows, int64_t cols, const float* x_dev,
+                    const float* norm_w_dev, float eps, float* y_dev, int32_t mode);
+/* the activation quantization the matvec prologue performs, written out in ggml block
+ * form (block_q8_K for K-quant weight types, block_q8_0 for Q8_0) for bit-exact checks */
+int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x_dev, const float* norm_w_dev,
+                          float eps, void* out_dev);
+/* timed microbenchmark: `reps` matvecs rotating over n_mats distinct weight copies
+ * (to defeat the 256 MB Infinity Cache); returns average microseconds per matvec */
+double llmi_bench_matvec(int32_t type, const void* w_dev, int32_t n_mats, int64_t rows, int64_t cols,
+                         const float* x_dev, float* y_dev, int32_t reps);
+
+#pragma GCC visibility pop
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLMI_H */

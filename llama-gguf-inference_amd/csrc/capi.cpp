@@ -1,0 +1,552 @@
+// capi.cpp — extern "C" drop-in surface (include/llmi.h).  Each function restates
+// the upstream llama.h entry point of the same name; no C++ exception
+// crosses this boundary, errors go to the thread-local llmi_last_error().
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/llmi.h"
+#include "engine.h"
+
+using namespace llmi;
+
+struct llama_model {
+    Model m;
+};
+struct llama_vocab {
+    const Model* m;
+};
+struct llama_context {
+    Context c;
+    llama_model* owner;
+    uint8_t* outs = nullptr;        // device copies of flagged logits rows [cap][n_vocab]
+    int outs_cap = 0;
+    std::vector<char> host_valid;   // per output row: logits_host filled
+    unsigned long long* keys_pinned = nullptr;  // per output row argmax key (pinned host)
+    int keys_cap = 0;
+};
+
+namespace {
+thread_local std::string g_err;
+void set_err(const std::string& e) { g_err = e; }
+#define API_TRY try {
+#define API_CATCH(ret)                                   \
+    }                                                    \
+    catch (const std::bad_alloc&) {                      \
+        set_err("out of host memory");                   \
+        return ret;                                      \
+    }                                                    \
+    catch (...) {                                        \
+        set_err("internal error");                       \
+        return ret;                                      \
+    }
+
+llama_vocab* vocab_handle(const llama_model* m) {
+    static thread_local std::vector<std::unique_ptr<llama_vocab>> pool;
+    for (auto& v : pool)
+        if (v->m == &m->m) return v.get();
+    pool.push_back(std::make_unique<llama_vocab>(llama_vocab{&m->m}));
+    return pool.back().get();
+}
+
+bool ensure_outs(llama_context* ctx, int n) {
+    const int V = ctx->c.m->hp.n_vocab;
+    if (n <= ctx->outs_cap) return true;
+    if (ctx->outs) (void)hipFree(ctx->outs);
+    ctx->outs = nullptr;
+    ctx->outs_cap = 0;
+    if (hipMalloc(&ctx->outs, (size_t)n * V * 4) != hipSuccess) { set_err("hipMalloc logits outputs"); return false; }
+    ctx->outs_cap = n;
+    if (n > ctx->keys_cap) {
+        if (ctx->keys_pinned) (void)hipHostFree(ctx->keys_pinned);
+        ctx->keys_pinned = nullptr;
+        if (hipHostMalloc((void**)&ctx->keys_pinned, (size_t)n * 8, hipHostMallocDefault) != hipSuccess) {
+            set_err("hipHostMalloc");
+            return false;
+        }
+        ctx->keys_cap = n;
+    }
+    return true;
+}
+}  // namespace
+
+extern "C" {
+
+const char* llmi_last_error(void) { return g_err.c_str(); }
+
+void llama_backend_init(void) { (void)hipInit(0); }
+void llama_backend_free(void) {}
+
+struct llama_model_params llama_model_default_params(void) {
+    struct llama_model_params p;
+    p.n_gpu_layers = 999;
+    p.main_gpu = 0;
+    p.vocab_only = false;
+    p.use_mmap = true;
+    p.no_upload = false;
+    return p;
+}
+
+struct llama_context_params llama_context_default_params(void) {
+    struct llama_context_params p;
+    p.n_ctx = 4096;
+    p.n_batch = 2048;
+    p.n_ubatch = 512;
+    p.n_seq_max = 1;
+    p.n_threads = 0;
+    p.use_graphs = true;
+    return p;
+}
+
+int32_t llmi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+struct llama_model* llama_model_load_from_file(const char* path, struct llama_model_params params) {
+    API_TRY
+    if (!path) { set_err("null path"); return nullptr; }
+    if (params.n_gpu_layers == 0 && !params.vocab_only) {
+        set_err("n_gpu_layers=0 requests the CPU path; llmi is GPU-only (the NGL=0 path is the reference's "
+                "llama.cpp CPU server, Dockerfile.cpu:84-89)");
+        return nullptr;
+    }
+    if (!params.vocab_only) {
+        const int n = llmi_device_count();
+        if (n <= 0) { set_err("no HIP device visible"); return nullptr; }
+        if (params.main_gpu < 0 || params.main_gpu >= n) { set_err("main_gpu out of range"); return nullptr; }
+    }
+    auto* m = new llama_model();
+    std::string err;
+    if (!model_load(path, params.main_gpu, params.vocab_only, params.no_upload, m->m, err)) {
+        set_err(err);
+        delete m;
+        return nullptr;
+    }
+    return m;
+    API_CATCH(nullptr)
+}
+
+void llama_model_free(struct llama_model* model) { delete model; }
+
+struct llama_context* llama_init_from_model(struct llama_model* model, struct llama_context_params params) {
+    API_TRY
+    if (!model || !model->m.arena) { set_err("model has no device weights"); return nullptr; }
+    auto* ctx = new llama_context();
+    ctx->owner = model;
+    std::string err;
+    if (!context_init(&model->m, (int)params.n_ctx, params.use_graphs, ctx->c, err)) {
+        set_err(err);
+        delete ctx;
+        return nullptr;
+    }
+    return ctx;
+    API_CATCH(nullptr)
+}
+
+void llama_free(struct llama_context* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->c.m->device);
+    if (ctx->outs) (void)hipFree(ctx->outs);
+    if (ctx->keys_pinned) (void)hipHostFree(ctx->keys_pinned);
+    delete ctx;
+}
+
+struct llama_batch llama_batch_get_one(llama_token* tokens, int32_t n_tokens) {
+    struct llama_batch b;
+    std::memset(&b, 0, sizeof b);
+    b.n_tokens = n_tokens;
+    b.token = tokens;
+    return b;
+}
+
+struct llama_batch llama_batch_init(int32_t n_tokens, int32_t embd, int32_t n_seq_max) {
+    struct llama_batch b;
+    std::memset(&b, 0, sizeof b);
+    if (n_tokens <= 0) return b;
+    if (embd) b.embd = (float*)calloc((size_t)n_tokens * embd, sizeof(float));
+    else b.token = (llama_token*)calloc((size_t)n_tokens, sizeof(llama_token));
+    b.pos = (llama_pos*)calloc((size_t)n_tokens, sizeof(llama_pos));
+    b.n_seq_id = (int32_t*)calloc((size_t)n_tokens, sizeof(int32_t));
+    b.seq_id = (llama_seq_id**)calloc((size_t)n_tokens + 1, sizeof(llama_seq_id*));
+    for (int i = 0; i < n_tokens; ++i) b.seq_id[i] = (llama_seq_id*)calloc((size_t)std::max(1, n_seq_max), sizeof(llama_seq_id));
+    b.logits = (int8_t*)calloc((size_t)n_tokens, 1);
+    return b;
+}
+
+void llama_batch_free(struct llama_batch b) {
+    free(b.token);
+    free(b.embd);
+    free(b.pos);
+    free(b.n_seq_id);
+    if (b.seq_id) {
+        for (int i = 0; b.seq_id[i]; ++i) free(b.seq_id[i]);
+        free(b.seq_id);
+    }
+    free(b.logits);
+}
+
+int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
+    API_TRY
+    if (!ctx) { set_err("null context"); return -1; }
+    Context& c = ctx->c;
+    const HParams& hp = c.m->hp;
+    if (batch.n_tokens <= 0 || !batch.token) { set_err("llama_decode: empty batch or no tokens"); return -1; }
+    if (batch.embd) { set_err("llama_decode: embedding input is not supported"); return -1; }
+    const int n = batch.n_tokens;
+    std::vector<int> rows((size_t)n, -1);
+    int n_out = 0;
+    for (int i = 0; i < n; ++i)
+        if (batch.logits ? batch.logits[i] != 0 : i == n - 1) rows[(size_t)i] = n_out++;
+    for (int i = 0; i < n; ++i) {
+        const int tok = batch.token[i];
+        if (tok < 0 || tok >= hp.n_vocab) { set_err("llama_decode: token id out of range"); return -1; }
+        const int pos = batch.pos ? batch.pos[i] : c.n_past + i;
+        if (pos < 0) { set_err("llama_decode: negative position"); return -1; }
+        if (pos >= c.n_ctx) { set_err("llama_decode: no KV slot (position >= n_ctx)"); return 1; }
+    }
+    if (hipSetDevice(c.m->device) != hipSuccess) { set_err("hipSetDevice"); return -2; }
+    if (n_out > 0 && !ensure_outs(ctx, n_out)) return -2;
+    c.out_rows = rows;
+    c.n_outputs = n_out;
+    ctx->host_valid.assign((size_t)n_out, 0);
+    c.logits_host.resize((size_t)std::max(1, n_out) * hp.n_vocab);
+    std::string err;
+    double bytes = 0;
+    hipEventRecord(c.ev0, c.stream);
+    int last_pos = c.n_past - 1;
+    for (int i = 0; i < n; ++i) {
+        const int pos = batch.pos ? batch.pos[i] : c.n_past + i;
+        if (launch_state_set(c.st, batch.token[i], pos, c.stream) != hipSuccess || !step_run(c, pos, err)) {
+            set_err("llama_decode: " + (err.empty() ? std::string("launch failed") : err));
+            return -3;
+        }
+        bytes += bytes_per_token(*c.m, pos + 1);
+        const int r = rows[(size_t)i];
+        if (r >= 0) {
+            (void)hipMemcpyAsync(ctx->outs + (size_t)r * hp.n_vocab * 4, c.logits, (size_t)hp.n_vocab * 4,
+                                 hipMemcpyDeviceToDevice, c.stream);
+            (void)hipMemcpyAsync(ctx->keys_pinned + r, &c.st->argmax_key, 8, hipMemcpyDeviceToHost, c.stream);
+        }
+        last_pos = std::max(last_pos, pos);
+    }
+    hipEventRecord(c.ev1, c.stream);
+    hipError_t e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) { set_err("llama_decode: " + hip_err(e)); return -4; }
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, c.ev0, c.ev1);
+    c.last_us = ms * 1e3;
+    c.last_bytes = bytes;
+    c.n_past = last_pos + 1;
+    return 0;
+    API_CATCH(-5)
+}
+
+int llama_eval(struct llama_context* ctx, llama_token* tokens, int32_t n_tokens, int32_t n_past) {
+    if (!ctx || !tokens || n_tokens <= 0) { set_err("llama_eval: bad arguments"); return 1; }
+    std::vector<llama_pos> pos((size_t)n_tokens);
+    for (int i = 0; i < n_tokens; ++i) pos[(size_t)i] = n_past + i;
+    struct llama_batch b = llama_batch_get_one(tokens, n_tokens);
+    b.pos = pos.data();
+    return llama_decode(ctx, b) == 0 ? 0 : 1;
+}
+
+static int out_row(llama_context* ctx, int32_t i) {
+    Context& c = ctx->c;
+    if (c.n_outputs <= 0) return -1;
+    if (i < 0) return c.n_outputs - 1;
+    if (i >= (int)c.out_rows.size()) return -1;
+    return c.out_rows[(size_t)i];
+}
+
+float* llama_get_logits_ith(struct llama_context* ctx, int32_t i) {
+    API_TRY
+    if (!ctx) return nullptr;
+    const int r = out_row(ctx, i);
+    if (r < 0) { set_err("llama_get_logits_ith: no logits for this batch index"); return nullptr; }
+    Context& c = ctx->c;
+    const size_t V = (size_t)c.m->hp.n_vocab;
+    if (!ctx->host_valid[(size_t)r]) {
+        (void)hipSetDevice(c.m->device);
+        if (hipMemcpy(c.logits_host.data() + (size_t)r * V, ctx->outs + (size_t)r * V * 4, V * 4,
+                      hipMemcpyDeviceToHost) != hipSuccess) {
+            set_err("logits copy failed");
+            return nullptr;
+        }
+        ctx->host_valid[(size_t)r] = 1;
+    }
+    return c.logits_host.data() + (size_t)r * V;
+    API_CATCH(nullptr)
+}
+
+float* llama_get_logits(struct llama_context* ctx) {
+    if (!ctx || ctx->c.n_outputs <= 0) { set_err("llama_get_logits: no outputs"); return nullptr; }
+    for (int r = 0; r < ctx->c.n_outputs; ++r) {
+        // materialise every output row
+        int idx = -1;
+        for (size_t k = 0; k < ctx->c.out_rows.size(); ++k)
+            if (ctx->c.out_rows[k] == r) idx = (int)k;
+        if (idx >= 0 && !llama_get_logits_ith(ctx, idx)) return nullptr;
+    }
+    return ctx->c.logits_host.data();
+}
+
+llama_token llmi_greedy_ith(struct llama_context* ctx, int32_t i) {
+    if (!ctx) return -1;
+    const int r = out_row(ctx, i);
+    if (r < 0) { set_err("llmi_greedy_ith: no logits for this batch index"); return -1; }
+    const unsigned long long k = ctx->keys_pinned[r];
+    return (llama_token)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+}
+
+int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_gen, llama_token* out) {
+    API_TRY
+    if (!ctx || !out || n_gen <= 0) { set_err("llmi_generate_greedy: bad arguments"); return -1; }
+    Context& c = ctx->c;
+    const HParams& hp = c.m->hp;
+    if (first < 0 || first >= hp.n_vocab) { set_err("llmi_generate_greedy: token out of range"); return -1; }
+    if (pos0 < 0 || pos0 + n_gen > c.n_ctx) { set_err("llmi_generate_greedy: exceeds n_ctx"); return 1; }
+    (void)hipSetDevice(c.m->device);
+    std::string err;
+    double bytes = 0;
+    if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
+    hipEventRecord(c.ev0, c.stream);
+    for (int k = 0; k < n_gen; ++k) {
+        if (!step_run(c, pos0 + k, err)) { set_err("llmi_generate_greedy: " + err); return -3; }
+        bytes += bytes_per_token(*c.m, pos0 + k + 1);
+    }
+    hipEventRecord(c.ev1, c.stream);
+    std::vector<int32_t> h((size_t)n_gen);
+    unsigned long long key = 0;
+    if (n_gen > 1)
+        (void)hipMemcpyAsync(h.data(), c.hist + pos0 + 1, (size_t)(n_gen - 1) * 4, hipMemcpyDeviceToHost, c.stream);
+    (void)hipMemcpyAsync(&key, &c.st->argmax_key, 8, hipMemcpyDeviceToHost, c.stream);
+    hipError_t e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) { set_err("llmi_generate_greedy: " + hip_err(e)); return -4; }
+    for (int k = 0; k + 1 < n_gen; ++k) out[k] = h[(size_t)k];
+    out[n_gen - 1] = (llama_token)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, c.ev0, c.ev1);
+    c.last_us = ms * 1e3;
+    c.last_bytes = bytes;
+    c.n_past = pos0 + n_gen;
+    c.n_outputs = 0;
+    return n_gen;
+    API_CATCH(-5)
+}
+
+void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec) {
+    if (!ctx) return;
+    if (bytes) *bytes = ctx->c.last_bytes;
+    if (usec) *usec = ctx->c.last_us;
+}
+
+double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv) {
+    return model ? bytes_per_token(model->m, n_kv) : 0.0;
+}
+
+int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64_t* bytes) {
+    if (!model) return -1;
+    if (dev_ptr) *dev_ptr = model->m.arena;
+    if (bytes) *bytes = model->m.arena_bytes;
+    return 0;
+}
+
+int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_t n, struct llama_model** out) {
+    API_TRY
+    if (!model || !devices || n <= 0 || !out) { set_err("llmi_replicate: bad arguments"); return -1; }
+    std::vector<llama_model*> reps((size_t)n, nullptr);
+    std::string err;
+    for (int i = 0; i < n; ++i) {
+        reps[(size_t)i] = new llama_model();
+        if (!model_clone_layout(model->m, devices[i], reps[(size_t)i]->m, err)) {
+            set_err("llmi_replicate: " + err);
+            for (auto* r : reps) delete r;
+            return -2;
+        }
+    }
+    // one communicator over {source device, replicas...}; rank 0 broadcasts the arena
+    std::vector<int> devs;
+    devs.push_back(model->m.device);
+    for (int i = 0; i < n; ++i) devs.push_back(devices[i]);
+    std::vector<ncclComm_t> comms(devs.size());
+    if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
+        set_err("ncclCommInitAll failed");
+        for (auto* r : reps) delete r;
+        return -3;
+    }
+    const size_t bytes = model->m.arena_bytes;
+    ncclResult_t nr = ncclGroupStart();
+    for (size_t r = 0; r < devs.size() && nr == ncclSuccess; ++r) {
+        (void)hipSetDevice(devs[r]);
+        void* buf = r == 0 ? (void*)model->m.arena : (void*)reps[r - 1]->m.arena;
+        nr = ncclBroadcast(buf, buf, bytes, ncclUint8, 0, comms[r], nullptr);
+    }
+    if (nr == ncclSuccess) nr = ncclGroupEnd();
+    else (void)ncclGroupEnd();
+    for (size_t r = 0; r < devs.size(); ++r) {
+        (void)hipSetDevice(devs[r]);
+        (void)hipDeviceSynchronize();
+        ncclCommDestroy(comms[r]);
+    }
+    if (nr != ncclSuccess) {
+        set_err("ncclBroadcast failed");
+        for (auto* r : reps) delete r;
+        return -4;
+    }
+    for (int i = 0; i < n; ++i) out[i] = reps[(size_t)i];
+    return 0;
+    API_CATCH(-5)
+}
+
+const struct llama_vocab* llama_model_get_vocab(const struct llama_model* model) {
+    return model ? vocab_handle(model) : nullptr;
+}
+int32_t llama_vocab_n_tokens(const struct llama_vocab* v) { return v ? v->m->hp.n_vocab : 0; }
+llama_token llama_vocab_bos(const struct llama_vocab* v) { return v ? v->m->bos : -1; }
+llama_token llama_vocab_eos(const struct llama_vocab* v) { return v ? v->m->eos : -1; }
+const char* llama_vocab_get_text(const struct llama_vocab* v, llama_token t) {
+    if (!v || t < 0 || t >= (int)v->m->vocab.size()) return nullptr;
+    return v->m->vocab[(size_t)t].c_str();
+}
+int32_t llama_model_n_embd(const struct llama_model* m) { return m ? m->m.hp.n_embd : 0; }
+int32_t llama_model_n_layer(const struct llama_model* m) { return m ? m->m.hp.n_layer : 0; }
+int32_t llama_model_n_head(const struct llama_model* m) { return m ? m->m.hp.n_head : 0; }
+int32_t llama_model_n_head_kv(const struct llama_model* m) { return m ? m->m.hp.n_head_kv : 0; }
+int32_t llama_model_n_ctx_train(const struct llama_model* m) { return m ? m->m.hp.n_ctx_train : 0; }
+uint64_t llama_model_size(const struct llama_model* m) { return m ? (uint64_t)model_tensor_bytes(m->m) : 0; }
+int32_t llama_model_desc(const struct llama_model* m, char* buf, size_t n) {
+    if (!m) return -1;
+    return snprintf(buf, n, "%s", m->m.desc.c_str());
+}
+uint32_t llama_n_ctx(const struct llama_context* ctx) { return ctx ? (uint32_t)ctx->c.n_ctx : 0; }
+void llama_kv_self_clear(struct llama_context* ctx) {
+    if (ctx) context_clear(ctx->c);
+}
+
+int64_t llmi_synth_write_gguf(const char* path, const char* preset, uint64_t seed, int32_t n_layer, int32_t n_vocab,
+                              int32_t n_threads) {
+    API_TRY
+    if (!path || !preset) { set_err("null argument"); return -1; }
+    std::string err;
+    int64_t r = synth_write_gguf(path, preset, seed, n_layer, n_vocab, n_threads, err);
+    if (r < 0) set_err(err);
+    return r;
+    API_CATCH(-1)
+}
+
+// ---------------- kernel-level entry points (tests / microbenchmarks) ----------------
+static Seg seg_at(int32_t type, const void* w, int64_t rows, int64_t cols) {
+    DevMat dm;
+    dm.type = type;
+    dm.rows = rows;
+    dm.cols = cols;
+    plan_planes(dm, 0);
+    Seg s;
+    s.a = (const uint8_t*)w + dm.off_a;
+    s.s = (const uint8_t*)w + dm.off_s;
+    s.d = (const uint8_t*)w + dm.off_d;
+    s.type = type;
+    s.rows = (int)rows;
+    s.row0 = 0;
+    return s;
+}
+
+int64_t llmi_device_layout_bytes(int32_t type, int64_t rows, int64_t cols) {
+    if (!type_supported(type) || cols % block_elems(type)) return -1;
+    DevMat dm;
+    dm.type = type; dm.rows = rows; dm.cols = cols;
+    return (int64_t)plan_planes(dm, 0);
+}
+
+int32_t llmi_repack(int32_t type, const void* raw, void* w, int64_t rows, int64_t cols) {
+    if (!type_supported(type) || cols % block_elems(type)) { set_err("bad type/shape"); return -1; }
+    DevMat dm;
+    dm.type = type; dm.rows = rows; dm.cols = cols;
+    plan_planes(dm, 0);
+    hipError_t e;
+    if (type == T_Q6_K || type == T_Q8_0) {
+        e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_s, (uint8_t*)w + dm.off_d,
+                          rows * (cols / block_elems(type)), nullptr);
+    } else {
+        e = hipMemcpy(w, raw, dm.bytes, hipMemcpyDeviceToDevice);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+    return 0;
+}
+
+int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, const float* x, const float* nw, float eps,
+                    float* y, int32_t mode) {
+    if (!(type == T_Q4_K || type == T_Q5_K || type == T_Q6_K || type == T_Q8_0) || cols % 256 || rows <= 0) {
+        set_err("llmi_matvec: unsupported type/shape");
+        return -1;
+    }
+    MVArgs a;
+    a.seg[0] = seg_at(type, w, rows, cols);
+    a.nseg = 1;
+    a.cols = (int)cols;
+    a.npairs = (int)((rows + 1) / 2);
+    a.x = x; a.nw = nw; a.eps = eps; a.y = y;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev);
+    hipError_t e = launch_matvec(a, mode == 1 ? EPI_ADD : EPI_STORE, std::max(64, prop.multiProcessorCount * 4), nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+    return 0;
+}
+
+int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x, const float* nw, float eps, void* out) {
+    if (cols % 256) { set_err("cols must be a multiple of 256"); return -1; }
+    MVArgs a;
+    a.cols = (int)cols; a.x = x; a.nw = nw; a.eps = eps;
+    hipError_t e = launch_quant_dump(a, act_kind(type), out, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+    return 0;
+}
+
+double llmi_bench_matvec(int32_t type, const void* w, int32_t n_mats, int64_t rows, int64_t cols, const float* x, float* y,
+                         int32_t reps) {
+    const int64_t lb = llmi_device_layout_bytes(type, rows, cols);
+    if (lb <= 0 || n_mats <= 0 || reps <= 0) { set_err("bad arguments"); return -1.0; }
+    const size_t stride = align_up((size_t)lb, 4096);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev);
+    const int mb = std::max(64, prop.multiProcessorCount * 4);
+    MVArgs a;
+    a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
+    for (int k = 0; k < n_mats; ++k) {  // warm-up (code, TLB)
+        a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows, cols);
+        if (launch_matvec(a, EPI_STORE, mb, nullptr) != hipSuccess) { set_err("launch failed"); return -1.0; }
+    }
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, nullptr);
+    for (int r = 0; r < reps; ++r) {
+        a.seg[0] = seg_at(type, (const uint8_t*)w + stride * (r % n_mats), rows, cols);
+        (void)launch_matvec(a, EPI_STORE, mb, nullptr);
+    }
+    hipEventRecord(e1, nullptr);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return (double)ms * 1e3 / reps;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// common.h — shared host/device definitions of the llmi decode path.
+//
+// Device weight layouts (DESIGN.md §Data layout in HBM).  Every quantized matrix is
+// stored row-major by 256- (K-quants) or 32- (Q8_0) element blocks; the algorithmic
+// byte count of every layout equals the GGUF byte count exactly:
+//   Q4_K  native 144-B blocks (16-B aligned: 144 = 9*16)             [planes: A]
+//   Q5_K  native 176-B blocks (176 = 11*16)                            [A]
+//   Q6_K  "Q6R": the 210-B block is not 16-B aligned, so it is repacked at load into
+//         A = 192 B/block: 4 chunks x {32 B low nibbles, 16 B 2-bit highs} in the
+//             64-weight chunk order every K-quant kernel lane uses,
+//         S = 16 B/block int8 scales, D = 2 B/block fp16 d              [A, S, D]
+//   Q8_0  "Q80R": Q = 32 B/block int8, D = 2 B/block fp16 d               [A, D]
+//   F32/F16 plain.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/llmi_synth.h"
+
+namespace llmi {
+
+enum : int {
+    T_F32 = LLMI_T_F32, T_F16 = LLMI_T_F16, T_Q8_0 = LLMI_T_Q8_0,
+    T_Q4_K = LLMI_T_Q4_K, T_Q5_K = LLMI_T_Q5_K, T_Q6_K = LLMI_T_Q6_K
+};
+
+inline int block_elems(int t) {
+    switch (t) {
+        case T_F32: case T_F16: return 1;
+        case T_Q8_0: return 32;
+        case T_Q4_K: case T_Q5_K: case T_Q6_K: return 256;
+        default: return 0;
+    }
+}
+inline int block_bytes(int t) {
+    switch (t) {
+        case T_F32: return 4; case T_F16: return 2; case T_Q8_0: return 34;
+        case T_Q4_K: return 144; case T_Q5_K: return 176; case T_Q6_K: return 210;
+        default: return 0;
+    }
+}
+inline bool is_kquant(int t) { return t == T_Q4_K || t == T_Q5_K || t == T_Q6_K; }
+inline bool type_supported(int t) { return block_bytes(t) != 0; }
+inline const char* type_name(int t) {
+    switch (t) {
+        case T_F32: return "f32"; case T_F16: return "f16"; case T_Q8_0: return "q8_0";
+        case T_Q4_K: return "q4_K"; case T_Q5_K: return "q5_K"; case T_Q6_K: return "q6_K";
+        default: return "?";
+    }
+}
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+// bytes of a tensor in GGUF (== algorithmic bytes of its device layout)
+inline size_t tensor_bytes(int t, int64_t rows, int64_t cols) {
+    return (size_t)rows * (size_t)(cols / block_elems(t)) * (size_t)block_bytes(t);
+}
+
+// Placement of one matrix inside the device arena.
+struct DevMat {
+    int type = -1;
+    int64_t rows = 0, cols = 0;
+    size_t off_a = 0, off_s = 0, off_d = 0;  // plane offsets (arena-relative)
+    size_t bytes = 0;                          // algorithmic bytes
+};
+
+// plane layout of a matrix starting at arena offset `base`; returns end offset
+inline size_t plan_planes(DevMat& m, size_t base) {
+    const size_t nblk = (size_t)m.rows * (size_t)(m.cols / block_elems(m.type));
+    m.bytes = tensor_bytes(m.type, m.rows, m.cols);
+    m.off_a = align_up(base, 256);
+    if (m.type == T_Q6_K) {
+        m.off_s = align_up(m.off_a + nblk * 192, 256);
+        m.off_d = align_up(m.off_s + nblk * 16, 256);
+        return m.off_d + nblk * 2;
+    }
+    if (m.type == T_Q8_0) {
+        m.off_d = align_up(m.off_a + nblk * 32, 256);
+        m.off_s = m.off_d;
+        return m.off_d + nblk * 2;
+    }
+    m.off_s = m.off_d = m.off_a;
+    return m.off_a + m.bytes;
+}
+
+// On-device decode state (one per context).  The first kernel of a step selects the
+// token (host-fed, or the previous step's on-device argmax) and advances pos.
+struct StepState {
+    int32_t token_in;        // >= 0: host-provided token; -1: take argmax of previous step
+    int32_t pos_next;        // position of the next step
+    int32_t pos;             // position of the current step (written by the embed kernel)
+    int32_t token;           // token of the current step
+    unsigned long long argmax_key;  // (ordered logit << 32) | (0xffffffff - row)
+};
+
+}  // namespace llmi

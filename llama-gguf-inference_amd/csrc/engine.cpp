@@ -1,0 +1,397 @@
+// engine.cpp — GGUF model -> HBM arena, decode context, per-step kernel schedule.
+//
+// Replaces the parts of upstream libllama that sit on the decode path:
+// llama_model_loader (a4), the llm_build_llama graph for one token (a5-a15) and the
+// f16 KV cache (a16).  One decode step is 2 + 6*n_layer kernel launches, captured once
+// per 256-position KV bucket into a HIP graph and replayed; the next token is fed back
+// on the device (argmax key -> k_embed), so greedy generation needs no host round trip.
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace llmi {
+
+std::string hip_err(hipError_t e) { return std::string(hipGetErrorString(e)); }
+
+#define HIPC(expr)                                                         \
+    do {                                                                   \
+        hipError_t e_ = (expr);                                            \
+        if (e_ != hipSuccess) {                                            \
+            err = std::string(#expr) + ": " + hip_err(e_);                 \
+            return false;                                                  \
+        }                                                                  \
+    } while (0)
+
+Model::~Model() {
+    if (arena && owns_arena) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        (void)hipFree(arena);
+        (void)hipSetDevice(cur);
+    }
+}
+
+Context::~Context() {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (m) (void)hipSetDevice(m->device);
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
+    void* bufs[] = {x, q, att, h, logits, scores, rope, kc, vc, st, hist};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+    (void)hipSetDevice(cur);
+}
+
+namespace {
+
+bool map_mat(const GgufFile& f, const std::string& name, DevMat& m, std::string& err, bool required = true) {
+    const GgufTensor* t = f.tensor(name);
+    if (!t) {
+        if (required) err = "missing tensor " + name;
+        return false;
+    }
+    m.type = t->type;
+    m.cols = t->ne[0];
+    m.rows = t->ne[1] * t->ne[2] * t->ne[3];
+    return true;
+}
+
+}  // namespace
+
+size_t model_tensor_bytes(const Model& m) {
+    size_t b = m.tok_embd.bytes + m.out_norm.bytes + (m.output.off_a == m.tok_embd.off_a ? 0 : m.output.bytes);
+    for (const Layer& L : m.layers)
+        b += L.attn_norm.bytes + L.wq.bytes + L.wk.bytes + L.wv.bytes + L.wo.bytes + L.ffn_norm.bytes + L.wg.bytes +
+             L.wu.bytes + L.wd.bytes;
+    return b;
+}
+
+double bytes_per_token(const Model& m, int n_kv) {
+    const HParams& hp = m.hp;
+    double b = (double)m.output.bytes + (double)m.out_norm.bytes + (double)m.tok_embd.bytes / hp.n_vocab;
+    for (const Layer& L : m.layers)
+        b += (double)(L.attn_norm.bytes + L.wq.bytes + L.wk.bytes + L.wv.bytes + L.wo.bytes + L.ffn_norm.bytes +
+                      L.wg.bytes + L.wu.bytes + L.wd.bytes);
+    const double kv_row = 2.0 * hp.n_head_kv * hp.head_dim * 2.0;  // K+V f16 per layer per position
+    b += hp.n_layer * kv_row * (double)n_kv;                       // KV read
+    b += hp.n_layer * kv_row;                                      // KV write of the new token
+    return b;
+}
+
+bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& M, std::string& err) {
+    M.path = path;
+    M.device = device;
+    M.file = std::make_shared<GgufFile>();
+    GgufFile& f = *M.file;
+    if (!f.open(path, err)) return false;
+    const std::string arch = f.str("general.architecture", "");
+    if (arch != "llama") { err = "unsupported architecture '" + arch + "' (llmi decodes the llama family)"; return false; }
+    HParams& hp = M.hp;
+    hp.n_embd = (int)f.num("llama.embedding_length", 0);
+    hp.n_layer = (int)f.num("llama.block_count", 0);
+    hp.n_head = (int)f.num("llama.attention.head_count", 0);
+    hp.n_head_kv = (int)f.num("llama.attention.head_count_kv", hp.n_head);
+    hp.n_ff = (int)f.num("llama.feed_forward_length", 0);
+    hp.n_ctx_train = (int)f.num("llama.context_length", 4096);
+    hp.eps = (float)f.num("llama.attention.layer_norm_rms_epsilon", 1e-5);
+    hp.rope_base = (float)f.num("llama.rope.freq_base", 10000.0);
+    hp.file_type = (int)f.num("general.file_type", 0);
+    if (hp.n_embd <= 0 || hp.n_layer <= 0 || hp.n_head <= 0 || hp.n_head_kv <= 0) {
+        err = "missing llama.* hyperparameters";
+        return false;
+    }
+    hp.head_dim = hp.n_embd / hp.n_head;
+    hp.n_rot = (int)f.num("llama.rope.dimension_count", hp.head_dim);
+    if (const GgufKV* tk = f.kv("tokenizer.ggml.tokens")) M.vocab = tk->arr_str;
+    M.bos = (int)f.num("tokenizer.ggml.bos_token_id", -1);
+    M.eos = (int)f.num("tokenizer.ggml.eos_token_id", -1);
+    if (!map_mat(f, "token_embd.weight", M.tok_embd, err)) return false;
+    if (!map_mat(f, "output_norm.weight", M.out_norm, err)) return false;
+    bool tied = !map_mat(f, "output.weight", M.output, err, false);
+    hp.n_vocab = (int)M.tok_embd.rows;
+    if (M.vocab.empty()) {
+        M.vocab.resize((size_t)hp.n_vocab);
+    }
+    M.layers.resize((size_t)hp.n_layer);
+    for (int l = 0; l < hp.n_layer; ++l) {
+        Layer& L = M.layers[(size_t)l];
+        const std::string p = "blk." + std::to_string(l) + ".";
+        if (!map_mat(f, p + "attn_norm.weight", L.attn_norm, err) || !map_mat(f, p + "attn_q.weight", L.wq, err) ||
+            !map_mat(f, p + "attn_k.weight", L.wk, err) || !map_mat(f, p + "attn_v.weight", L.wv, err) ||
+            !map_mat(f, p + "attn_output.weight", L.wo, err) || !map_mat(f, p + "ffn_norm.weight", L.ffn_norm, err) ||
+            !map_mat(f, p + "ffn_gate.weight", L.wg, err) || !map_mat(f, p + "ffn_up.weight", L.wu, err) ||
+            !map_mat(f, p + "ffn_down.weight", L.wd, err))
+            return false;
+    }
+    if (hp.n_ff <= 0) hp.n_ff = (int)M.layers[0].wg.rows;
+    // shape checks: everything the kernels assume
+    const int E = hp.n_embd, D = hp.head_dim, nq = hp.n_head * D, nk = hp.n_head_kv * D;
+    if (D != 64 && D != 128) { err = "head_dim " + std::to_string(D) + " unsupported (64 or 128)"; return false; }
+    const int gqa = hp.n_head / hp.n_head_kv;
+    if (hp.n_head % hp.n_head_kv || (gqa != 1 && gqa != 2 && gqa != 4 && gqa != 8)) {
+        err = "GQA ratio unsupported";
+        return false;
+    }
+    if (hp.n_rot > D || hp.n_rot % 2) { err = "bad rope.dimension_count"; return false; }
+    if (E % 256 || hp.n_ff % 256) { err = "n_embd and n_ff must be multiples of 256"; return false; }
+    auto chk = [&](const DevMat& m, int64_t rows, int64_t cols, const char* nm, bool quant) {
+        if (m.rows != rows || m.cols != cols) { err = std::string(nm) + ": unexpected shape"; return false; }
+        if (quant && !(m.type == T_Q4_K || m.type == T_Q5_K || m.type == T_Q6_K || m.type == T_Q8_0)) {
+            err = std::string(nm) + ": weight type " + type_name(m.type) + " not supported on the decode path";
+            return false;
+        }
+        if (!quant && m.type != T_F32) { err = std::string(nm) + ": norm weight must be f32"; return false; }
+        return true;
+    };
+    if (!chk(M.out_norm, 1, E, "output_norm", false)) return false;
+    if (M.tok_embd.cols != E) { err = "token_embd: unexpected shape"; return false; }
+    if (!tied && !chk(M.output, hp.n_vocab, E, "output", true)) return false;
+    for (const Layer& L : M.layers) {
+        if (!chk(L.attn_norm, 1, E, "attn_norm", false) || !chk(L.ffn_norm, 1, E, "ffn_norm", false) ||
+            !chk(L.wq, nq, E, "attn_q", true) || !chk(L.wk, nk, E, "attn_k", true) || !chk(L.wv, nk, E, "attn_v", true) ||
+            !chk(L.wo, E, nq, "attn_output", true) || !chk(L.wg, hp.n_ff, E, "ffn_gate", true) ||
+            !chk(L.wu, hp.n_ff, E, "ffn_up", true) || !chk(L.wd, E, hp.n_ff, "ffn_down", true))
+            return false;
+        if (act_kind(L.wg.type) != act_kind(L.wu.type)) { err = "ffn_gate/ffn_up mix Q8_0 with K-quants"; return false; }
+    }
+    if (const GgufTensor* rf = f.tensor("rope_freqs.weight")) {
+        if (rf->type != T_F32 || rf->ne[0] * 2 < hp.n_rot) { err = "bad rope_freqs.weight"; return false; }
+        M.rope_freq_host.assign((const float*)rf->data, (const float*)rf->data + rf->ne[0]);
+        M.has_rope_freqs = true;
+    }
+    // ---- arena plan ----
+    size_t off = 0;
+    auto plan = [&](DevMat& m) { off = plan_planes(m, off); };
+    plan(M.tok_embd);
+    plan(M.out_norm);
+    if (tied) M.output = M.tok_embd;
+    else plan(M.output);
+    for (Layer& L : M.layers) {
+        plan(L.attn_norm); plan(L.wq); plan(L.wk); plan(L.wv); plan(L.wo);
+        plan(L.ffn_norm); plan(L.wg); plan(L.wu); plan(L.wd);
+    }
+    M.arena_bytes = align_up(off, 4096);
+    char desc[256];
+    snprintf(desc, sizeof desc, "llama %dL E%d H%d/%d FF%d V%d ftype %d (%.2f GB)", hp.n_layer, E, hp.n_head,
+             hp.n_head_kv, hp.n_ff, hp.n_vocab, hp.file_type, (double)model_tensor_bytes(M) / 1e9);
+    M.desc = desc;
+    if (vocab_only) return true;
+    HIPC(hipSetDevice(device));
+    HIPC(hipMalloc(&M.arena, M.arena_bytes));
+    M.owns_arena = true;
+    if (no_upload) return true;
+    // ---- upload: H2D + on-device repack of the unaligned block types ----
+    struct Item { const GgufTensor* t; DevMat* m; };
+    std::vector<Item> items;
+    auto add = [&](const std::string& name, DevMat* m) { items.push_back({f.tensor(name), m}); };
+    add("token_embd.weight", &M.tok_embd);
+    add("output_norm.weight", &M.out_norm);
+    if (!tied) add("output.weight", &M.output);
+    for (int l = 0; l < hp.n_layer; ++l) {
+        Layer& L = M.layers[(size_t)l];
+        const std::string p = "blk." + std::to_string(l) + ".";
+        add(p + "attn_norm.weight", &L.attn_norm); add(p + "attn_q.weight", &L.wq); add(p + "attn_k.weight", &L.wk);
+        add(p + "attn_v.weight", &L.wv); add(p + "attn_output.weight", &L.wo); add(p + "ffn_norm.weight", &L.ffn_norm);
+        add(p + "ffn_gate.weight", &L.wg); add(p + "ffn_up.weight", &L.wu); add(p + "ffn_down.weight", &L.wd);
+    }
+    size_t stage_bytes = 0;
+    for (const Item& it : items)
+        if (it.m->type == T_Q6_K || it.m->type == T_Q8_0) stage_bytes = std::max(stage_bytes, it.t->nbytes);
+    uint8_t* stage = nullptr;
+    if (stage_bytes) HIPC(hipMalloc(&stage, stage_bytes));
+    bool ok = true;
+    for (const Item& it : items) {
+        hipError_t e;
+        if (it.m->type == T_Q6_K || it.m->type == T_Q8_0) {
+            e = hipMemcpy(stage, it.t->data, it.t->nbytes, hipMemcpyHostToDevice);
+            if (e == hipSuccess) {
+                const int64_t nblk = it.m->rows * (it.m->cols / block_elems(it.m->type));
+                e = launch_repack(it.m->type, stage, M.arena + it.m->off_a, M.arena + it.m->off_s, M.arena + it.m->off_d,
+                                  nblk, nullptr);
+                if (e == hipSuccess) e = hipDeviceSynchronize();
+            }
+        } else {
+            e = hipMemcpy(M.arena + it.m->off_a, it.t->data, it.t->nbytes, hipMemcpyHostToDevice);
+        }
+        if (e != hipSuccess) { err = "upload of " + it.t->name + ": " + hip_err(e); ok = false; break; }
+    }
+    if (stage) (void)hipFree(stage);
+    return ok;
+}
+
+bool model_clone_layout(const Model& src, int device, Model& dst, std::string& err) {
+    dst.device = device;
+    dst.path = src.path;
+    dst.desc = src.desc;
+    dst.file = src.file;
+    dst.hp = src.hp;
+    dst.tok_embd = src.tok_embd; dst.out_norm = src.out_norm; dst.output = src.output;
+    dst.layers = src.layers;
+    dst.vocab = src.vocab; dst.bos = src.bos; dst.eos = src.eos;
+    dst.rope_freq_host = src.rope_freq_host; dst.has_rope_freqs = src.has_rope_freqs;
+    dst.arena_bytes = src.arena_bytes;
+    HIPC(hipSetDevice(device));
+    HIPC(hipMalloc(&dst.arena, dst.arena_bytes));
+    dst.owns_arena = true;
+    return true;
+}
+
+bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string& err) {
+    const HParams& hp = m->hp;
+    c.m = m;
+    c.n_ctx = n_ctx > 0 ? n_ctx : std::min(hp.n_ctx_train > 0 ? hp.n_ctx_train : 4096, 4096);
+    c.use_graphs = use_graphs;
+    HIPC(hipSetDevice(m->device));
+    hipDeviceProp_t prop;
+    HIPC(hipGetDeviceProperties(&prop, m->device));
+    c.max_blocks = std::max(64, prop.multiProcessorCount * 4);
+    HIPC(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    HIPC(hipEventCreate(&c.ev0));
+    HIPC(hipEventCreate(&c.ev1));
+    const size_t E = (size_t)hp.n_embd, QD = (size_t)hp.n_head * hp.head_dim;
+    const size_t kv_elems = (size_t)hp.n_layer * hp.n_head_kv * (size_t)c.n_ctx * hp.head_dim;
+    HIPC(hipMalloc(&c.x, E * 4));
+    HIPC(hipMalloc(&c.q, QD * 4));
+    HIPC(hipMalloc(&c.att, QD * 4));
+    HIPC(hipMalloc(&c.h, (size_t)hp.n_ff * 4));
+    HIPC(hipMalloc(&c.logits, (size_t)hp.n_vocab * 4));
+    HIPC(hipMalloc(&c.scores, (size_t)hp.n_head * c.n_ctx * 4));
+    HIPC(hipMalloc(&c.kc, kv_elems * 2));
+    HIPC(hipMalloc(&c.vc, kv_elems * 2));
+    HIPC(hipMalloc(&c.st, sizeof(StepState)));
+    HIPC(hipMalloc(&c.hist, (size_t)c.n_ctx * 4));
+    // RoPE table [pos][n_rot/2][cos,sin]: ggml_rope_cache_init's iterative theta, computed
+    // on the host with libm cosf/sinf exactly as the CPU path does
+    const int half = hp.n_rot / 2;
+    std::vector<float> tab((size_t)c.n_ctx * half * 2);
+    const float theta_scale = powf(hp.rope_base, -2.0f / (float)hp.n_rot);
+    for (int p = 0; p < c.n_ctx; ++p) {
+        float theta = (float)p;
+        for (int i = 0; i < half; ++i) {
+            const float ff = m->has_rope_freqs ? m->rope_freq_host[(size_t)i] : 1.0f;
+            const float th = 1.0f * (theta / ff);
+            tab[((size_t)p * half + i) * 2 + 0] = cosf(th) * 1.0f;
+            tab[((size_t)p * half + i) * 2 + 1] = sinf(th) * 1.0f;
+            theta *= theta_scale;
+        }
+    }
+    HIPC(hipMalloc(&c.rope, tab.size() * 4));
+    HIPC(hipMemcpy(c.rope, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    context_clear(c);
+    HIPC(hipStreamSynchronize(c.stream));
+    return true;
+}
+
+void context_clear(Context& c) {
+    const HParams& hp = c.m->hp;
+    const size_t kv_elems = (size_t)hp.n_layer * hp.n_head_kv * (size_t)c.n_ctx * hp.head_dim;
+    (void)hipSetDevice(c.m->device);
+    (void)hipMemsetAsync(c.kc, 0, kv_elems * 2, c.stream);
+    (void)hipMemsetAsync(c.vc, 0, kv_elems * 2, c.stream);
+    (void)hipMemsetAsync(c.hist, 0, (size_t)c.n_ctx * 4, c.stream);
+    StepState s0{-1, 0, 0, 0, 0ull};
+    (void)hipMemcpyAsync(c.st, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
+    (void)hipStreamSynchronize(c.stream);
+    c.n_past = 0;
+}
+
+namespace {
+
+Seg seg_of(const Model& m, const DevMat& d, int row0) {
+    Seg s;
+    s.a = m.arena + d.off_a;
+    s.s = m.arena + d.off_s;
+    s.d = m.arena + d.off_d;
+    s.type = d.type;
+    s.rows = (int)d.rows;
+    s.row0 = row0;
+    return s;
+}
+
+}  // namespace
+
+bool step_enqueue(Context& c, int kv_bound, std::string& err) {
+    const Model& m = *c.m;
+    const HParams& hp = m.hp;
+    const int E = hp.n_embd, D = hp.head_dim, nq = hp.n_head * D, nk = hp.n_head_kv * D;
+    const size_t kv_layer = (size_t)hp.n_head_kv * c.n_ctx * D;
+    EmbArgs ea;
+    ea.w = seg_of(m, m.tok_embd, 0);
+    ea.cols = E; ea.vocab = hp.n_vocab; ea.x = c.x; ea.st = c.st; ea.hist = c.hist; ea.n_ctx = c.n_ctx;
+    HIPC(launch_embed(ea, c.stream));
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const Layer& L = m.layers[(size_t)l];
+        // --- QKV + RoPE + KV write (grouped by activation kind) ---
+        MVArgs a;
+        a.cols = E; a.x = c.x; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps; a.y = c.q;
+        a.kc = c.kc + l * kv_layer; a.vc = c.vc + l * kv_layer; a.rope = c.rope; a.st = c.st;
+        a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = nq; a.nk = nk;
+        const Seg qkv[3] = {seg_of(m, L.wq, 0), seg_of(m, L.wk, nq), seg_of(m, L.wv, nq + nk)};
+        int i = 0;
+        while (i < 3) {
+            int j = i;
+            a.nseg = 0;
+            int rows = 0;
+            while (j < 3 && act_kind(qkv[j].type) == act_kind(qkv[i].type)) { a.seg[a.nseg++] = qkv[j]; rows += qkv[j].rows; ++j; }
+            a.npairs = rows / 2;
+            HIPC(launch_matvec(a, EPI_QKV, c.max_blocks, c.stream));
+            i = j;
+        }
+        // --- attention ---
+        AttnArgs at;
+        at.q = c.q; at.kc = a.kc; at.vc = a.vc; at.scores = c.scores; at.out = c.att; at.st = c.st;
+        at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
+        HIPC(launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
+        // --- output projection + residual ---
+        MVArgs o;
+        o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
+        HIPC(launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
+        // --- gate/up + SwiGLU ---
+        MVArgs gu;
+        gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2;
+        gu.cols = E; gu.x = c.x; gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps;
+        gu.y = c.h; gu.npairs = hp.n_ff;
+        HIPC(launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
+        // --- down + residual ---
+        MVArgs dn;
+        dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
+        HIPC(launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
+    }
+    MVArgs lo;
+    lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
+    lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
+    lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = &c.st->argmax_key;
+    HIPC(launch_matvec(lo, EPI_LOGITS, c.max_blocks, c.stream));
+    return true;
+}
+
+bool step_run(Context& c, int pos, std::string& err) {
+    const int bucket = pos / 256;
+    const int kv_bound = std::min(c.n_ctx, (bucket + 1) * 256);
+    if (!c.use_graphs) return step_enqueue(c, kv_bound, err);
+    auto it = c.graphs.find(bucket);
+    if (it == c.graphs.end()) {
+        hipGraph_t g = nullptr;
+        HIPC(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+        std::string e2;
+        const bool ok = step_enqueue(c, kv_bound, e2);
+        hipError_t ec = hipStreamEndCapture(c.stream, &g);
+        if (!ok) { err = "capture: " + e2; if (g) (void)hipGraphDestroy(g); return false; }
+        if (ec != hipSuccess) { err = "hipStreamEndCapture: " + hip_err(ec); return false; }
+        hipGraphExec_t ex = nullptr;
+        hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ei != hipSuccess) { err = "hipGraphInstantiate: " + hip_err(ei); return false; }
+        it = c.graphs.emplace(bucket, ex).first;
+    }
+    HIPC(hipGraphLaunch(it->second, c.stream));
+    return true;
+}
+
+}  // namespace llmi

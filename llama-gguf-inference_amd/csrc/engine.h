@@ -1,0 +1,85 @@
+// engine.h — model (device weight arena) and context (KV cache, scratch, step graphs).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "gguf.h"
+#include "kernels.h"
+
+namespace llmi {
+
+struct HParams {
+    int n_embd = 0, n_layer = 0, n_head = 0, n_head_kv = 0, head_dim = 0, n_ff = 0, n_vocab = 0;
+    int n_rot = 0, n_ctx_train = 0, file_type = 0;
+    float eps = 1e-5f, rope_base = 10000.f;
+};
+
+struct Layer {
+    DevMat attn_norm, wq, wk, wv, wo, ffn_norm, wg, wu, wd;
+};
+
+struct Model {
+    int device = 0;
+    std::string path, desc;
+    std::shared_ptr<GgufFile> file;
+    HParams hp;
+    DevMat tok_embd, out_norm, output, rope_freqs;
+    bool has_rope_freqs = false;
+    std::vector<Layer> layers;
+    uint8_t* arena = nullptr;
+    size_t arena_bytes = 0;
+    bool owns_arena = true;
+    std::vector<std::string> vocab;
+    int bos = -1, eos = -1;
+    std::vector<float> rope_freq_host;  // rope_freqs.weight, if present
+    ~Model();
+};
+
+struct Context {
+    Model* m = nullptr;
+    int n_ctx = 0;
+    bool use_graphs = true;
+    hipStream_t stream = nullptr;
+    int max_blocks = 1024;
+    // device
+    float *x = nullptr, *q = nullptr, *att = nullptr, *h = nullptr, *logits = nullptr, *scores = nullptr;
+    float* rope = nullptr;
+    uint16_t *kc = nullptr, *vc = nullptr;
+    StepState* st = nullptr;
+    int32_t* hist = nullptr;
+    // host
+    std::vector<float> logits_host;         // [n_outputs][n_vocab]
+    std::vector<int> out_rows;              // batch index -> row in logits_host, -1 none
+    std::vector<unsigned long long> out_keys;  // per output: argmax key
+    int n_outputs = 0;
+    int n_past = 0;
+    std::map<int, hipGraphExec_t> graphs;   // by KV bucket
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_bytes = 0, last_us = 0;
+    ~Context();
+};
+
+// all return false and set err on failure
+bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& m, std::string& err);
+bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string& err);
+// enqueue one decode step for a state already set (token_in/pos_next); kv_bound >= pos+1
+bool step_enqueue(Context& c, int kv_bound, std::string& err);
+// run one step via the cached graph of its KV bucket (or eagerly)
+bool step_run(Context& c, int pos, std::string& err);
+double bytes_per_token(const Model& m, int n_kv);
+void context_clear(Context& c);
+size_t model_tensor_bytes(const Model& m);
+// arena layout of a model for another device (replica); no upload
+bool model_clone_layout(const Model& src, int device, Model& dst, std::string& err);
+
+std::string hip_err(hipError_t e);
+int64_t synth_write_gguf(const std::string& path, const std::string& preset, uint64_t seed, int n_layer, int n_vocab,
+                         int n_threads, std::string& err);
+
+}  // namespace llmi

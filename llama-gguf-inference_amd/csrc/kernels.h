@@ -1,0 +1,78 @@
+// kernels.h — launch interface of the gfx950 decode kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+namespace llmi {
+
+constexpr int kMVThreads = 256;  // 4 waves of 64; each wave owns one row pair at a time
+
+enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
+
+// One weight matrix of a fused matvec launch.
+struct Seg {
+    const uint8_t* a = nullptr;  // plane A (blocks / Q6R chunks / Q80R quants)
+    const uint8_t* s = nullptr;  // Q6R scales
+    const uint8_t* d = nullptr;  // Q6R / Q80R fp16 d
+    int type = -1;
+    int rows = 0;
+    int row0 = 0;                // first row of this segment in the launch's output space
+};
+
+struct MVArgs {
+    Seg seg[3];
+    int nseg = 0;
+    int cols = 0;
+    int npairs = 0;              // row pairs (SWIGLU: gate/up pairs)
+    const float* x = nullptr;    // f32[cols] input
+    const float* nw = nullptr;   // RMSNorm weight (nullptr: quantize x as is)
+    float eps = 0.f;
+    float* y = nullptr;          // STORE/ADD/LOGITS: f32[rows]; SWIGLU: h; QKV: q
+    // QKV epilogue: RoPE + f16 KV-cache write
+    uint16_t* kc = nullptr;      // layer K cache [HK][n_ctx][D]
+    uint16_t* vc = nullptr;      // layer V cache, transposed [HK][D][n_ctx]
+    const float* rope = nullptr; // [n_ctx][n_rot/2][cos,sin]
+    const StepState* st = nullptr;
+    int head_dim = 0, n_rot = 0, n_ctx = 0, nq = 0, nk = 0;
+    unsigned long long* argmax = nullptr;  // LOGITS
+};
+
+struct AttnArgs {
+    const float* q = nullptr;      // f32[H*D] (roped)
+    const uint16_t* kc = nullptr;  // layer base
+    const uint16_t* vc = nullptr;
+    float* scores = nullptr;       // f32[H][n_ctx]
+    float* out = nullptr;          // f32[H*D]
+    const StepState* st = nullptr;
+    int n_ctx = 0;
+    float scale = 0.f;
+};
+
+struct EmbArgs {
+    Seg w;                          // token_embd in device layout
+    int cols = 0;
+    int vocab = 0;
+    float* x = nullptr;
+    StepState* st = nullptr;
+    int32_t* hist = nullptr;        // token history [n_ctx]
+    int n_ctx = 0;
+};
+
+// activation kind of a weight type: 0 = block_q8_K (K-quants), 1 = block_q8_0
+inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
+size_t mv_lds_bytes(int act, int cols);
+
+// All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).
+hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t stream);
+hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
+hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
+hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* s, uint8_t* d, int64_t nblk, hipStream_t stream);
+// writes the prologue's quantized activation in ggml block form (test hook)
+hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);
+hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream_t stream);
+
+}  // namespace llmi

@@ -1,0 +1,802 @@
+// kernels.hip — gfx950 (CDNA4, wave64) kernels of the GGUF K-quant decode step.
+//
+// The hot path of SURVEY.md §8(a): per token, every linear layer is a quantized
+// matrix-vector product that streams the whole weight matrix from HBM once (rows
+// a6-a9, ~100% of the bytes), wrapped by the small fused ops a5 (activation
+// quantization), a10-a15.  Design:
+//
+//   k_matvec  one launch per fused weight group (QKV, O, gate+up, down, output head).
+//     prologue  every workgroup re-derives the quantized activation in LDS from the
+//               f32 input (L2-resident, 16-57 KB): optional RMSNorm (double sum, as
+//               ggml_compute_forward_rms_norm) then quantize_row_q8_K_ref /
+//               quantize_row_q8_0_ref bit-exactly.  This replaces a separate norm +
+//               quantize launch (~1.2-1.9 us dependent-kernel boundary on MI355X).
+//     body      a wave owns a PAIR of rows; lane i owns 64-weight chunk i (+64k) of
+//               both rows: 16-B nontemporal loads of the quantized weights, integer
+//               v_dot4c_i32_i8 against the LDS activation (read conflict-free through
+//               an 80-B-per-chunk padded layout), exact int32 per-chunk sums combined
+//               in fp32 exactly as ggml_vec_dot_*_q8_K (d_w*d_a*isum - dmin_w*d_a*imin),
+//               then a 64-lane butterfly reduction.
+//     epilogue  store / residual add / RoPE + f16 KV write / SwiGLU / logits + argmax.
+//   k_attn_scores, k_attn_pv   decode attention over the f16 KV cache with ggml's
+//               non-flash numerics (q rounded to f16, softmax with double sum,
+//               probabilities rounded to f16) — exact f16 products summed in double.
+//   k_embed    token selection (host token or previous argmax) + get_rows dequant.
+//   k_repack_* one-time load-time layout transforms (common.h).
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+namespace llmi {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr bool kNontemporalWeights = true;  // weights are read once per token (MI355X_MICROARCH nt-weights)
+
+__device__ __forceinline__ float h2f(uint32_t h) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+}
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+__device__ __forceinline__ u32x4 ldw(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x4*)p);
+    else return *(const u32x4*)p;
+}
+__device__ __forceinline__ uint32_t ldw32(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const uint32_t*)p);
+    else return *(const uint32_t*)p;
+}
+__device__ __forceinline__ int dot4(uint32_t a, int b, int c) {
+    return __builtin_amdgcn_sdot4((int)a, b, c, false);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ----------------------------------------------------------------------------------
+// LDS carve for the quantized activation
+//   qs: (cols/64) chunks x 80 B (64 B of int8 + 16 B pad: lane i reads chunk i at
+//       80*i + 16*k, which maps 16 consecutive lanes of a ds_read_b128 group to 16
+//       distinct 16-B bank slots -> conflict-free)
+//   d : per-block activation scale (f32; Q8_K per 256, Q8_0 per 32, f16-rounded)
+//   bs: Q8_K bsums (int16 per 16 elements)
+// ----------------------------------------------------------------------------------
+struct Lds {
+    uint8_t* qs;
+    float* d;
+    int16_t* bs;
+    double* red;
+};
+__host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t lds_d_off(int cols) { return a16((size_t)(cols / 64) * 80); }
+__host__ __device__ inline size_t lds_bs_off(int act, int cols) {
+    return a16(lds_d_off(cols) + (size_t)(act ? cols / 32 : cols / 256) * 4);
+}
+__host__ __device__ inline size_t lds_red_off(int act, int cols) {
+    return a16(lds_bs_off(act, cols) + (size_t)(act ? 0 : cols / 16) * 2);
+}
+size_t mv_lds_bytes(int act, int cols) { return lds_red_off(act, cols) + 8 * sizeof(double); }
+
+__device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
+    Lds l;
+    l.qs = smem;
+    l.d = (float*)(smem + lds_d_off(cols));
+    l.bs = (int16_t*)(smem + lds_bs_off(act, cols));
+    l.red = (double*)(smem + lds_red_off(act, cols));
+    return l;
+}
+
+__device__ double block_sum_d(double v, double* red) {
+    v = wave_sum_d(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ----------------------------------------------------------------------------------
+// Prologue: [RMSNorm] + activation quantization into LDS.
+// Thread t handles 16-element sub-blocks sb = t + 256k; the 16 lanes of one DPP row
+// hold the 16 sub-blocks of one 256-element Q8_K block, two adjacent lanes one Q8_0
+// block.  Bit-exact with ggml:
+//   rms_norm: sum += (double)(x*x); mean = (float)(sum/n); scale = 1/sqrtf(mean+eps);
+//             y = (x*scale)*w                          (ggml_compute_forward_rms_norm + mul)
+//   q8_K:     first max |y| (signed) -> iscale = -127/max; q = min(127, nearest_int(iscale*y));
+//             bsums per 16; d = 1/iscale; all-zero block -> d = 0, q = 0 (quantize_row_q8_K_ref)
+//   q8_0:     d = amax/127 (stored f16), q = roundf(y * (d ? 1/d : 0))   (quantize_row_q8_0_ref)
+// ----------------------------------------------------------------------------------
+template <int ACT, bool NORM>
+__device__ void mv_prologue(const MVArgs& A, const Lds& L) {
+    const int tid = threadIdx.x, cols = A.cols;
+    float scale = 1.0f;
+    if constexpr (NORM) {
+        double s = 0.0;
+        for (int i = tid * 4; i < cols; i += kMVThreads * 4) {
+            const float4 v = *(const float4*)(A.x + i);
+            s += (double)(v.x * v.x);
+            s += (double)(v.y * v.y);
+            s += (double)(v.z * v.z);
+            s += (double)(v.w * v.w);
+        }
+        s = block_sum_d(s, L.red);
+        const float mean = (float)(s / (double)cols);
+        scale = 1.0f / sqrtf(mean + A.eps);
+    }
+    const int nsub = cols / 16;
+    for (int sb = tid; sb < nsub; sb += kMVThreads) {
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
+            v[4 * k + 0] = xv.x; v[4 * k + 1] = xv.y; v[4 * k + 2] = xv.z; v[4 * k + 3] = xv.w;
+        }
+        if constexpr (NORM) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                v[4 * k + 0] = (v[4 * k + 0] * scale) * wv.x;
+                v[4 * k + 1] = (v[4 * k + 1] * scale) * wv.y;
+                v[4 * k + 2] = (v[4 * k + 2] * scale) * wv.z;
+                v[4 * k + 3] = (v[4 * k + 3] * scale) * wv.w;
+            }
+        }
+        int q[16];
+        if constexpr (ACT == 0) {
+            float am = 0.f, mv = 0.f;
+            int gi = sb * 16;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float ax = fabsf(v[j]);
+                if (ax > am) { am = ax; mv = v[j]; gi = sb * 16 + j; }
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {  // 16-lane (one Q8_K block) arg-max, first index wins
+                const float am2 = __shfl_xor(am, o), mv2 = __shfl_xor(mv, o);
+                const int gi2 = __shfl_xor(gi, o);
+                if (am2 > am || (am2 == am && gi2 < gi)) { am = am2; mv = mv2; gi = gi2; }
+            }
+            float dval = 0.f;
+            int bsum = 0;
+            if (am == 0.f) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) q[j] = 0;
+            } else {
+                const float iscale = -127.f / mv;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int t = llmi_nearest_int(iscale * v[j]);
+                    q[j] = t < 127 ? t : 127;
+                    bsum += q[j];
+                }
+                dval = 1.0f / iscale;
+            }
+            L.bs[sb] = (int16_t)bsum;
+            if ((tid & 15) == 0) L.d[sb >> 4] = dval;
+        } else {
+            float am = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+            am = fmaxf(am, __shfl_xor(am, 1));
+            const float d = am / 127;
+            const float id = d != 0.f ? 1.0f / d : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
+            if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
+        }
+        u32x4 pk;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
+                    ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
+        *(u32x4*)(L.qs + (sb >> 2) * 80 + (sb & 3) * 16) = pk;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// Per-type 64-weight chunk: load (global) and integer dot against the LDS activation
+// ----------------------------------------------------------------------------------
+struct Act {
+    i32x4 a0, a1, a2, a3;  // activation bytes 0-15, 16-31, 32-47, 48-63 of the chunk
+};
+__device__ __forceinline__ Act load_act(const Lds& L, int ci) {
+    const i32x4* p = (const i32x4*)(L.qs + ci * 80);
+    return {p[0], p[1], p[2], p[3]};
+}
+__device__ __forceinline__ int act_word(const Act& a, int w) {
+    const i32x4& v = w < 4 ? a.a0 : w < 8 ? a.a1 : w < 12 ? a.a2 : a.a3;
+    return v[w & 3];
+}
+
+struct Raw {
+    u32x4 v0, v1, v2, v3, v4;
+    uint32_t e0, e1;
+};
+
+constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u, M1 = 0x01010101u;
+
+// upstream get_scale_min_k4 on the 12 scale bytes held as three words
+__device__ __forceinline__ void scale_min(int j, uint32_t s0, uint32_t s1, uint32_t s2, int& sc, int& m) {
+    const int k = (j & 3) * 8;
+    const uint32_t b0 = (s0 >> k) & 0xffu, b1 = (s1 >> k) & 0xffu, b2 = (s2 >> k) & 0xffu;
+    if (j < 4) {
+        sc = (int)(b0 & 63u); m = (int)(b1 & 63u);
+    } else {
+        sc = (int)((b2 & 0xFu) | ((b0 >> 6) << 4));
+        m = (int)((b2 >> 4) | ((b1 >> 6) << 4));
+    }
+}
+
+template <int T>
+__device__ __forceinline__ Raw load_chunk(const Seg& s, int row, int ci, int nb) {
+    Raw r;
+    const int c = ci & 3;
+    if constexpr (T == T_Q4_K) {
+        const uint8_t* blk = s.a + ((size_t)row * nb + (ci >> 2)) * 144;
+        r.v0 = ldw(blk);
+        r.v1 = ldw(blk + 16 + 32 * c);
+        r.v2 = ldw(blk + 32 + 32 * c);
+    } else if constexpr (T == T_Q5_K) {
+        const uint8_t* blk = s.a + ((size_t)row * nb + (ci >> 2)) * 176;
+        r.v0 = ldw(blk);
+        r.v1 = ldw(blk + 16);
+        r.v2 = ldw(blk + 32);
+        r.v3 = ldw(blk + 48 + 32 * c);
+        r.v4 = ldw(blk + 64 + 32 * c);
+    } else if constexpr (T == T_Q6_K) {
+        const size_t rb = (size_t)row * nb + (ci >> 2);
+        const uint8_t* ch = s.a + rb * 192 + 48 * c;
+        r.v0 = ldw(ch);
+        r.v1 = ldw(ch + 16);
+        r.v2 = ldw(ch + 32);
+        r.e0 = ldw32(s.s + rb * 16 + 4 * c);
+        r.e1 = *(const uint16_t*)(s.d + rb * 2);
+    } else {  // Q8_0: two 32-weight blocks
+        const size_t b0 = (size_t)row * nb + 2 * (size_t)ci;
+        const uint8_t* q = s.a + b0 * 32;
+        r.v0 = ldw(q);
+        r.v1 = ldw(q + 16);
+        r.v2 = ldw(q + 32);
+        r.v3 = ldw(q + 48);
+        r.e0 = ldw32(s.d + b0 * 2);
+    }
+    return r;
+}
+
+// ggml_vec_dot_q4_K_q8_K restricted to one 64-weight chunk (sub-blocks 2c, 2c+1)
+template <int T>
+__device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, const Lds& L, int ci) {
+    const int c = ci & 3;
+    if constexpr (T == T_Q4_K || T == T_Q5_K) {
+        int sc0, m0, sc1, m1;
+        scale_min(2 * c, r.v0.y, r.v0.z, r.v0.w, sc0, m0);
+        scale_min(2 * c + 1, r.v0.y, r.v0.z, r.v0.w, sc1, m1);
+        const u32x4 qa = (T == T_Q4_K) ? r.v1 : r.v3;
+        const u32x4 qb = (T == T_Q4_K) ? r.v2 : r.v4;
+        int lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t qw = k < 4 ? qa[k] : qb[k - 4];
+            uint32_t l4 = qw & M4, h4 = (qw >> 4) & M4;
+            if constexpr (T == T_Q5_K) {
+                const uint32_t hw = k < 4 ? r.v1[k] : r.v2[k - 4];
+                l4 |= ((hw >> (2 * c)) & M1) << 4;
+                h4 |= ((hw >> (2 * c + 1)) & M1) << 4;
+            }
+            lo = dot4(l4, act_word(a, k), lo);
+            hi = dot4(h4, act_word(a, 8 + k), hi);
+        }
+        const int isum = sc0 * lo + sc1 * hi;
+        const uint2 bw = *(const uint2*)(L.bs + ci * 4);
+        const int b0 = (int16_t)(bw.x & 0xffff), b1 = (int16_t)(bw.x >> 16);
+        const int b2 = (int16_t)(bw.y & 0xffff), b3 = (int16_t)(bw.y >> 16);
+        const int imin = m0 * (b0 + b1) + m1 * (b2 + b3);
+        const float dA = L.d[ci >> 2];
+        const float d = h2f(r.v0.x), dmin = h2f(r.v0.x >> 16);
+        return (d * dA) * (float)isum - (dmin * dA) * (float)imin;
+    } else if constexpr (T == T_Q6_K) {
+        const uint32_t Q[8] = {r.v0.x, r.v0.y, r.v0.z, r.v0.w, r.v1.x, r.v1.y, r.v1.z, r.v1.w};
+        const uint32_t H[4] = {r.v2.x, r.v2.y, r.v2.z, r.v2.w};
+        int dm[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int sh = 2 * (k >> 2);
+            const uint32_t ulo = (Q[k] & M4) | (((H[k & 3] >> sh) & M2) << 4);
+            const uint32_t uhi = ((Q[k] >> 4) & M4) | (((H[k & 3] >> (4 + sh)) & M2) << 4);
+            dm[k >> 2] = dot4(ulo, act_word(a, k), dm[k >> 2]);
+            dm[2 + (k >> 2)] = dot4(uhi, act_word(a, 8 + k), dm[2 + (k >> 2)]);
+        }
+        const uint2 bw = *(const uint2*)(L.bs + ci * 4);
+        const int bsv[4] = {(int16_t)(bw.x & 0xffff), (int16_t)(bw.x >> 16), (int16_t)(bw.y & 0xffff),
+                            (int16_t)(bw.y >> 16)};
+        int isum = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) isum += (int)(int8_t)(r.e0 >> (8 * m)) * (dm[m] - 32 * bsv[m]);
+        const float dA = L.d[ci >> 2];
+        return (h2f(r.e1) * dA) * (float)isum;
+    } else {
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s0 = dot4(r.v0[k], a.a0[k], s0);
+            s0 = dot4(r.v1[k], a.a1[k], s0);
+            s1 = dot4(r.v2[k], a.a2[k], s1);
+            s1 = dot4(r.v3[k], a.a3[k], s1);
+        }
+        const float dA0 = L.d[2 * ci], dA1 = L.d[2 * ci + 1];
+        return (float)s0 * (h2f(r.e0) * dA0) + (float)s1 * (h2f(r.e0 >> 16) * dA1);
+    }
+}
+
+// Both rows of a pair share the activation chunk reads.
+template <int T>
+__device__ __forceinline__ void pair_rows(const Seg& sa, int ra, const Seg& sb, int rb, bool vb, int cols,
+                                          const Lds& L, float& acc_a, float& acc_b) {
+    const int cpr = cols >> 6;
+    const int nb = (T == T_Q8_0) ? (cols >> 5) : (cols >> 8);
+    const int lane = threadIdx.x & 63;
+    for (int ci = lane; ci < cpr; ci += 64) {
+        const Raw wa = load_chunk<T>(sa, ra, ci, nb);
+        Raw wb;
+        if (vb) wb = load_chunk<T>(sb, rb, ci, nb);
+        const Act act = load_act(L, ci);
+        acc_a += dot_chunk<T>(wa, act, L, ci);
+        if (vb) acc_b += dot_chunk<T>(wb, act, L, ci);
+    }
+}
+
+__device__ __forceinline__ void row_any(int type, const Seg& s, int r, int cols, const Lds& L, float& acc) {
+    float dummy = 0.f;
+    switch (type) {
+        case T_Q4_K: pair_rows<T_Q4_K>(s, r, s, r, false, cols, L, acc, dummy); break;
+        case T_Q5_K: pair_rows<T_Q5_K>(s, r, s, r, false, cols, L, acc, dummy); break;
+        case T_Q6_K: pair_rows<T_Q6_K>(s, r, s, r, false, cols, L, acc, dummy); break;
+        default: break;
+    }
+}
+
+__device__ __forceinline__ Seg pick(const MVArgs& A, int si) {
+    Seg s;
+    s.a = si == 0 ? A.seg[0].a : si == 1 ? A.seg[1].a : A.seg[2].a;
+    s.s = si == 0 ? A.seg[0].s : si == 1 ? A.seg[1].s : A.seg[2].s;
+    s.d = si == 0 ? A.seg[0].d : si == 1 ? A.seg[1].d : A.seg[2].d;
+    s.type = si == 0 ? A.seg[0].type : si == 1 ? A.seg[1].type : A.seg[2].type;
+    s.rows = si == 0 ? A.seg[0].rows : si == 1 ? A.seg[1].rows : A.seg[2].rows;
+    s.row0 = si == 0 ? A.seg[0].row0 : si == 1 ? A.seg[1].row0 : A.seg[2].row0;
+    return s;
+}
+
+// ordered key of (logit, row): larger logit wins, ties -> smaller row (first max wins,
+// as upstream llama_sampler_greedy's strict '>' scan)
+__device__ __forceinline__ unsigned long long argmax_key(float v, int row) {
+    if (v == 0.f) v = 0.f;  // -0 == +0
+    uint32_t u = __float_as_uint(v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
+}
+
+template <int ACT, bool NORM, int EPI>
+__global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Lds L = carve(smem, ACT, A.cols);
+    mv_prologue<ACT, NORM>(A, L);
+    __syncthreads();
+    const int wave = uniform((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    int pos = 0;
+    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
+    unsigned long long best = 0;
+    for (int p = blockIdx.x * 4 + wave; p < A.npairs; p += gridDim.x * 4) {
+        Seg sa, sb;
+        int ra, rb;
+        bool vb;
+        if constexpr (EPI == EPI_SWIGLU) {
+            sa = pick(A, 0); sb = pick(A, 1);
+            ra = rb = p; vb = true;
+        } else {
+            const int g = A.seg[0].row0 + 2 * p;
+            int si = 0;
+            if (A.nseg > 1 && g >= A.seg[1].row0) si = 1;
+            if (A.nseg > 2 && g >= A.seg[2].row0) si = 2;
+            sa = pick(A, si); sb = sa;
+            ra = g - sa.row0; rb = ra + 1; vb = rb < sa.rows;
+        }
+        float acc_a = 0.f, acc_b = 0.f;
+        if constexpr (ACT == 1) {
+            pair_rows<T_Q8_0>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b);
+        } else if (sa.type == sb.type) {
+            switch (sa.type) {
+                case T_Q4_K: pair_rows<T_Q4_K>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b); break;
+                case T_Q5_K: pair_rows<T_Q5_K>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b); break;
+                case T_Q6_K: pair_rows<T_Q6_K>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b); break;
+                default: break;
+            }
+        } else {  // gate/up of different K-quant types
+            row_any(sa.type, sa, ra, A.cols, L, acc_a);
+            if (vb) row_any(sb.type, sb, rb, A.cols, L, acc_b);
+        }
+        acc_a = wave_sum(acc_a);
+        acc_b = wave_sum(acc_b);
+        if (lane == 0) {
+            if constexpr (EPI == EPI_STORE) {
+                A.y[sa.row0 + ra] = acc_a;
+                if (vb) A.y[sa.row0 + rb] = acc_b;
+            } else if constexpr (EPI == EPI_ADD) {
+                A.y[sa.row0 + ra] += acc_a;
+                if (vb) A.y[sa.row0 + rb] += acc_b;
+            } else if constexpr (EPI == EPI_LOGITS) {
+                A.y[ra] = acc_a;
+                unsigned long long k = argmax_key(acc_a, ra);
+                best = k > best ? k : best;
+                if (vb) {
+                    A.y[rb] = acc_b;
+                    k = argmax_key(acc_b, rb);
+                    best = k > best ? k : best;
+                }
+            } else if constexpr (EPI == EPI_SWIGLU) {
+                A.y[p] = llmi_silu(acc_a) * acc_b;
+            } else if constexpr (EPI == EPI_QKV) {
+                // sa.row0 tells q (0), k (nq) or v (nq+nk)
+                const int hd = A.head_dim;
+                const int h = ra / hd, d = ra - h * hd;
+                if (sa.row0 < A.nq + A.nk) {
+                    float o0 = acc_a, o1 = acc_b;
+                    if (d < A.n_rot) {  // ggml rope NORM mode on the adjacent pair (d, d+1)
+                        const float2 cs = *(const float2*)(A.rope + ((size_t)pos * (A.n_rot / 2) + d / 2) * 2);
+                        o0 = acc_a * cs.x - acc_b * cs.y;
+                        o1 = acc_a * cs.y + acc_b * cs.x;
+                    }
+                    if (sa.row0 == 0) {
+                        A.y[ra] = o0;
+                        A.y[ra + 1] = o1;
+                    } else {
+                        const uint32_t w = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
+                        *(uint32_t*)(A.kc + ((size_t)h * A.n_ctx + pos) * hd + d) = w;
+                    }
+                } else {
+                    A.vc[((size_t)h * hd + d) * A.n_ctx + pos] = f2h(acc_a);
+                    A.vc[((size_t)h * hd + d + 1) * A.n_ctx + pos] = f2h(acc_b);
+                }
+            }
+        }
+    }
+    if constexpr (EPI == EPI_LOGITS) {
+        if (lane == 0 && best) atomicMax(A.argmax, best);
+    }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Lds L = carve(smem, ACT, A.cols);
+    if (A.nw) mv_prologue<ACT, true>(A, L);
+    else mv_prologue<ACT, false>(A, L);
+    __syncthreads();
+    const int cols = A.cols;
+    for (int e = threadIdx.x; e < cols; e += blockDim.x) {
+        const int8_t qv = (int8_t)L.qs[(e >> 6) * 80 + (e & 63)];
+        if (ACT == 0) out[(size_t)(e >> 8) * 292 + 4 + (e & 255)] = (uint8_t)qv;
+        else out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = (uint8_t)qv;
+    }
+    if (ACT == 0) {
+        for (int b = threadIdx.x; b < cols / 256; b += blockDim.x) *(float*)(out + (size_t)b * 292) = L.d[b];
+        for (int s = threadIdx.x; s < cols / 16; s += blockDim.x)
+            *(int16_t*)(out + (size_t)(s >> 4) * 292 + 260 + 2 * (s & 15)) = L.bs[s];
+    } else {
+        for (int b = threadIdx.x; b < cols / 32; b += blockDim.x) *(uint16_t*)(out + (size_t)b * 34) = f2h(L.d[b]);
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// Attention, ggml non-flash path:
+//   kq[t] = sum_d f16(q_d) * K[t][d]        (ggml_vec_dot_f16, exact products, double sum)
+//   w[t]  = kq[t] * (1/sqrt(D)); M = max w; e = exp(w-M); S = sum (double) e
+//   p[t]  = f16(e * (float)(1/S));  out[d] = sum_t V[t][d] * p[t]    (double sum)
+// scores: grid (HK, ceil(kv_bound/64)); workgroup = one kv head x 64 positions, its
+//         K tile staged through LDS (rows padded by 16 B: conflict-free ds_read_b128).
+// pv:     grid (HK, D/16); workgroup = one kv head x 16 dims for all GQA heads, reading
+//         the transposed V cache [HK][D][n_ctx] with coalesced 128-B rows.
+// ----------------------------------------------------------------------------------
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_attn_scores(AttnArgs a) {
+    const int g = blockIdx.x, chunk = blockIdx.y;
+    const int n_kv = a.st->pos + 1;
+    const int t0 = chunk * 64;
+    if (t0 >= n_kv) return;
+    const int nt = min(64, n_kv - t0);
+    __shared__ float qs[G][D];
+    __shared__ __attribute__((aligned(16))) uint16_t ks[64][D + 8];
+    for (int i = threadIdx.x; i < G * D; i += 256) qs[i / D][i % D] = h2f(f2h(a.q[(size_t)g * G * D + i]));
+    constexpr int PPR = D * 2 / 16;  // 16-B pieces per K row
+    const uint16_t* kb = a.kc + ((size_t)g * a.n_ctx + t0) * D;
+    for (int i = threadIdx.x; i < nt * PPR; i += 256) {
+        const int r = i / PPR, pc = i % PPR;
+        *(u32x4*)&ks[r][pc * 8] = *(const u32x4*)(kb + (size_t)r * D + pc * 8);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane < nt) {
+        for (int hh = wave; hh < G; hh += 4) {
+            double acc = 0.0;
+#pragma unroll 4
+            for (int d = 0; d < D; d += 8) {
+                const u32x4 kv = *(const u32x4*)&ks[lane][d];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc += (double)(h2f(kv[j]) * qs[hh][d + 2 * j]);
+                    acc += (double)(h2f(kv[j] >> 16) * qs[hh][d + 2 * j + 1]);
+                }
+            }
+            a.scores[(size_t)(g * G + hh) * a.n_ctx + t0 + lane] = (float)acc * a.scale;
+        }
+    }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_attn_pv(AttnArgs a) {
+    const int g = blockIdx.x, dc = blockIdx.y;
+    const int n_kv = a.st->pos + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ float sM[G], sInv[G];
+    __shared__ float sp[G][256];
+    __shared__ double red[4];
+    __shared__ float redf[4];
+    for (int hh = 0; hh < G; ++hh) {
+        const float* w = a.scores + (size_t)(g * G + hh) * a.n_ctx;
+        float mx = -INFINITY;
+        for (int t = tid; t < n_kv; t += 256) mx = fmaxf(mx, w[t]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        if (lane == 0) redf[wave] = mx;
+        __syncthreads();
+        mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+        double s = 0.0;
+        for (int t = tid; t < n_kv; t += 256) s += (double)llmi_expf(w[t] - mx);
+        s = wave_sum_d(s);
+        if (lane == 0) red[wave] = s;
+        __syncthreads();
+        if (tid == 0) {
+            sM[hh] = mx;
+            sInv[hh] = (float)(1.0 / ((red[0] + red[1]) + (red[2] + red[3])));
+        }
+        __syncthreads();
+    }
+    const int d0 = dc * 16 + wave * 4;
+    double acc[G][4];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh)
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) acc[hh][dd] = 0.0;
+    const uint16_t* vb = a.vc + ((size_t)g * D + d0) * a.n_ctx;
+    for (int tc = 0; tc < n_kv; tc += 256) {
+        __syncthreads();
+        const int t = tc + tid;
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            float p = 0.f;
+            if (t < n_kv) {
+                const float e = llmi_expf(a.scores[(size_t)(g * G + hh) * a.n_ctx + t] - sM[hh]);
+                p = h2f(f2h(e * sInv[hh]));
+            }
+            sp[hh][tid] = p;
+        }
+        __syncthreads();
+        const int nt = min(256, n_kv - tc);
+        for (int j = lane; j < nt; j += 64) {
+#pragma unroll
+            for (int dd = 0; dd < 4; ++dd) {
+                const float v = h2f(vb[(size_t)dd * a.n_ctx + tc + j]);
+#pragma unroll
+                for (int hh = 0; hh < G; ++hh) acc[hh][dd] += (double)(v * sp[hh][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh)
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+            const double s = wave_sum_d(acc[hh][dd]);
+            if (lane == 0) a.out[(size_t)(g * G + hh) * D + d0 + dd] = (float)s;
+        }
+}
+
+// ----------------------------------------------------------------------------------
+// Step entry: choose the token, advance pos, dequantize its embedding row
+// (upstream ggml_get_rows + dequantize_row_*; bit-exact).
+// ----------------------------------------------------------------------------------
+__device__ float dequant_elem(const Seg& w, int row, int e, int cols) {
+    switch (w.type) {
+        case T_F32: return ((const float*)w.a)[(size_t)row * cols + e];
+        case T_F16: return h2f(((const uint16_t*)w.a)[(size_t)row * cols + e]);
+        case T_Q4_K:
+        case T_Q5_K: {
+            const int bb = w.type == T_Q4_K ? 144 : 176;
+            const uint8_t* blk = w.a + ((size_t)row * (cols / 256) + e / 256) * bb;
+            const int i = e & 255, c = i >> 6, l = i & 63, hi = l >= 32;
+            const uint32_t* s32 = (const uint32_t*)(blk + 4);
+            int sc, m;
+            scale_min(2 * c + hi, s32[0], s32[1], s32[2], sc, m);
+            const float d = h2f(*(const uint16_t*)blk), dmin = h2f(*(const uint16_t*)(blk + 2));
+            const uint8_t* qs = blk + (w.type == T_Q4_K ? 16 : 48) + 32 * c;
+            int q = hi ? (qs[l - 32] >> 4) : (qs[l] & 0xF);
+            if (w.type == T_Q5_K) q += ((blk[16 + (l & 31)] >> (2 * c + hi)) & 1) ? 16 : 0;
+            const float d1 = d * (float)sc, m1 = dmin * (float)m;
+            return d1 * (float)q - m1;
+        }
+        case T_Q6_K: {
+            const size_t rb = (size_t)row * (cols / 256) + e / 256;
+            const int i = e & 255, c = i >> 6, t = i & 63;
+            const uint8_t* ch = w.a + rb * 192 + 48 * c;
+            const int lo4 = t < 32 ? (ch[t] & 0xF) : (ch[t - 32] >> 4);
+            const int hi2 = (ch[32 + (t & 15)] >> (2 * (t >> 4))) & 3;
+            const int q = (lo4 | (hi2 << 4)) - 32;
+            const float d = h2f(*(const uint16_t*)(w.d + rb * 2));
+            const int sc = (int8_t)w.s[rb * 16 + (i >> 4)];
+            return d * (float)sc * (float)q;
+        }
+        case T_Q8_0: {
+            const size_t b = (size_t)row * (cols / 32) + e / 32;
+            return (float)(int8_t)w.a[b * 32 + (e & 31)] * h2f(*(const uint16_t*)(w.d + b * 2));
+        }
+        default: return 0.f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_embed(EmbArgs a) {
+    __shared__ int s_tok;
+    if (threadIdx.x == 0) {
+        StepState* st = a.st;
+        int tok = st->token_in;
+        if (tok < 0) tok = (int)(0xffffffffu - (uint32_t)(st->argmax_key & 0xffffffffull));
+        if (tok < 0 || tok >= a.vocab) tok = 0;
+        const int pos = st->pos_next;
+        st->pos = pos;
+        st->pos_next = pos + 1;
+        st->token = tok;
+        st->token_in = -1;
+        st->argmax_key = 0;
+        if (pos >= 0 && pos < a.n_ctx) a.hist[pos] = tok;
+        s_tok = tok;
+    }
+    __syncthreads();
+    const int tok = s_tok;
+    for (int e = threadIdx.x; e < a.cols; e += 256) a.x[e] = dequant_elem(a.w, tok, e, a.cols);
+}
+
+__global__ void k_state_set(StepState* st, int token_in, int pos_next) {
+    st->token_in = token_in;
+    st->pos_next = pos_next;
+}
+
+// ----------------------------------------------------------------------------------
+// Load-time repack (common.h): Q6_K 210-B blocks -> Q6R planes; Q8_0 -> Q80R planes.
+// ----------------------------------------------------------------------------------
+__global__ void k_repack_q6k(const uint8_t* raw, uint8_t* A, uint8_t* S, uint8_t* Dp, int64_t nblk) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = gid >> 2;
+    const int c = (int)(gid & 3);
+    if (b >= nblk) return;
+    const uint8_t* x = raw + b * 210;
+    const uint8_t* ql = x;
+    const uint8_t* qh = x + 128;
+    auto u6 = [&](int w) -> int {  // 6-bit unsigned value of weight w of the block
+        const int n = w >> 7, r = w & 127, quad = r >> 5, l = r & 31;
+        const uint8_t qlb = ql[64 * n + l + 32 * (quad & 1)];
+        const int lo = (quad >> 1) ? (qlb >> 4) : (qlb & 0xF);
+        const int hi = (qh[32 * n + l] >> (2 * quad)) & 3;
+        return lo | (hi << 4);
+    };
+    uint8_t* o = A + b * 192 + 48 * c;
+    for (int t = 0; t < 32; ++t) o[t] = (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
+    for (int s = 0; s < 16; ++s) {
+        uint8_t v = 0;
+        for (int j = 0; j < 4; ++j) v |= (uint8_t)((u6(64 * c + 16 * j + s) >> 4) << (2 * j));
+        o[32 + s] = v;
+    }
+    for (int i = 0; i < 4; ++i) S[b * 16 + 4 * c + i] = x[192 + 4 * c + i];
+    if (c == 0) { Dp[b * 2] = x[208]; Dp[b * 2 + 1] = x[209]; }
+}
+
+__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nblk) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    const uint8_t* x = raw + b * 34;
+    for (int i = 0; i < 32; ++i) A[b * 32 + i] = x[2 + i];
+    Dp[b * 2] = x[0];
+    Dp[b * 2 + 1] = x[1];
+}
+
+// ----------------------------------------------------------------------------------
+// launchers
+// ----------------------------------------------------------------------------------
+template <int ACT, bool NORM>
+static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
+    switch (epi) {
+        case EPI_STORE: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_STORE>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_ADD: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_ADD>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_QKV: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_QKV>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_SWIGLU: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_SWIGLU>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_LOGITS: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_LOGITS>), grid, dim3(kMVThreads), lds, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s) {
+    if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0) return hipErrorInvalidValue;
+    const int act = act_kind(a.seg[0].type);
+    for (int i = 1; i < a.nseg; ++i)
+        if (act_kind(a.seg[i].type) != act) return hipErrorInvalidValue;
+    const size_t lds = mv_lds_bytes(act, a.cols);
+    int blocks = (a.npairs + 3) / 4;
+    if (blocks > max_blocks) blocks = max_blocks;
+    const dim3 grid(blocks);
+    const bool norm = a.nw != nullptr;
+    if (act == 0) return norm ? mv_dispatch_epi<0, true>(a, epi, grid, lds, s) : mv_dispatch_epi<0, false>(a, epi, grid, lds, s);
+    return norm ? mv_dispatch_epi<1, true>(a, epi, grid, lds, s) : mv_dispatch_epi<1, false>(a, epi, grid, lds, s);
+}
+
+hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t s) {
+    if (a.cols <= 0 || a.cols % 256) return hipErrorInvalidValue;
+    const size_t lds = mv_lds_bytes(act, a.cols);
+    if (act == 0) hipLaunchKernelGGL((k_quant_dump<0>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+    else hipLaunchKernelGGL((k_quant_dump<1>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+    return hipGetLastError();
+}
+
+template <int D>
+static hipError_t attn_dispatch_g(const AttnArgs& a, int g, int hk, int kv_bound, hipStream_t s) {
+    const dim3 gs(hk, (kv_bound + 63) / 64), gp(hk, D / 16);
+    switch (g) {
+#define LLMI_ATT(G)                                                                   \
+    case G:                                                                           \
+        hipLaunchKernelGGL((k_attn_scores<D, G>), gs, dim3(256), 0, s, a);            \
+        hipLaunchKernelGGL((k_attn_pv<D, G>), gp, dim3(256), 0, s, a);                \
+        break;
+        LLMI_ATT(1) LLMI_ATT(2) LLMI_ATT(4) LLMI_ATT(8)
+#undef LLMI_ATT
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
+    if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    const int g = n_head / n_head_kv;
+    if (head_dim == 128) return attn_dispatch_g<128>(a, g, n_head_kv, kv_bound, s);
+    if (head_dim == 64) return attn_dispatch_g<64>(a, g, n_head_kv, kv_bound, s);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_embed(const EmbArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_embed, dim3(1), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream_t s) {
+    hipLaunchKernelGGL(k_state_set, dim3(1), dim3(1), 0, s, st, token_in, pos_next);
+    return hipGetLastError();
+}
+
+hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* sp, uint8_t* d, int64_t nblk, hipStream_t s) {
+    if (nblk <= 0) return hipSuccess;
+    if (type == T_Q6_K) {
+        const int64_t thr = nblk * 4;
+        hipLaunchKernelGGL(k_repack_q6k, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, sp, d, nblk);
+    } else if (type == T_Q8_0) {
+        hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d, nblk);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace llmi

@@ -1,0 +1,198 @@
+"""llmi — MI355X-native GGUF decode path (Python host side over the libllmi.so C ABI).
+
+Mirrors the llama.cpp decode surface the reference's llama-server drives
+(SURVEY.md §8b): a Model is `llama_model_load_from_file`, a Context is
+`llama_init_from_model`, `Context.decode` is `llama_decode` with the same return
+codes, `Context.logits` is `llama_get_logits_ith`.  All compute runs in the HIP
+library; nothing here computes numerics.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import LlmiLibraryError, last_error, lib, llama_context_params, llama_model_params  # noqa: F401
+
+# ggml type ids
+F32, F16, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 8, 12, 13, 14, 15
+PRESETS = (
+    "llama3-8b-q4km", "llama3-70b-q4km", "tinyllama-q8_0", "mistral7b-q6k", "mistral7b-q5km",
+    "tiny-mixed", "tiny-mixed-d128",
+)
+
+
+class LlmiError(RuntimeError):
+    pass
+
+
+def device_count() -> int:
+    return int(lib().llmi_device_count())
+
+
+def write_synthetic_gguf(path: str, preset: str, seed: int = 3, n_layer: int = 0, n_vocab: int = 0,
+                         n_threads: int = 0) -> int:
+    """Write a synthetic GGUF with the exact shapes/type table of `preset`."""
+    n = lib().llmi_synth_write_gguf(path.encode(), preset.encode(), seed, n_layer, n_vocab, n_threads)
+    if n < 0:
+        raise LlmiError(last_error())
+    return int(n)
+
+
+class Model:
+    """llama_model_load_from_file: GGUF -> HBM arena on `main_gpu`."""
+
+    def __init__(self, path: str, n_gpu_layers: int = 999, main_gpu: int = 0, vocab_only: bool = False,
+                 no_upload: bool = False):
+        L = lib()
+        p = L.llama_model_default_params()
+        p.n_gpu_layers = n_gpu_layers
+        p.main_gpu = main_gpu
+        p.vocab_only = vocab_only
+        p.no_upload = no_upload
+        self._h = L.llama_model_load_from_file(path.encode(), p)
+        if not self._h:
+            raise LlmiError(last_error())
+        self.path = path
+        self.device = main_gpu
+        v = L.llama_model_get_vocab(self._h)
+        self._vocab = v
+        self.n_vocab = L.llama_vocab_n_tokens(v)
+        self.bos = L.llama_vocab_bos(v)
+        self.eos = L.llama_vocab_eos(v)
+        self.n_embd = L.llama_model_n_embd(self._h)
+        self.n_layer = L.llama_model_n_layer(self._h)
+        self.n_head = L.llama_model_n_head(self._h)
+        self.n_head_kv = L.llama_model_n_head_kv(self._h)
+        self.n_ctx_train = L.llama_model_n_ctx_train(self._h)
+        self.size = int(L.llama_model_size(self._h))
+        buf = C.create_string_buffer(256)
+        L.llama_model_desc(self._h, buf, 256)
+        self.desc = buf.value.decode()
+
+    @classmethod
+    def _from_handle(cls, h, path: str, device: int) -> "Model":
+        self = cls.__new__(cls)
+        L = lib()
+        self._h = h
+        self.path = path
+        self.device = device
+        v = L.llama_model_get_vocab(h)
+        self._vocab = v
+        self.n_vocab = L.llama_vocab_n_tokens(v)
+        self.bos, self.eos = L.llama_vocab_bos(v), L.llama_vocab_eos(v)
+        self.n_embd, self.n_layer = L.llama_model_n_embd(h), L.llama_model_n_layer(h)
+        self.n_head, self.n_head_kv = L.llama_model_n_head(h), L.llama_model_n_head_kv(h)
+        self.n_ctx_train = L.llama_model_n_ctx_train(h)
+        self.size = int(L.llama_model_size(h))
+        self.desc = ""
+        return self
+
+    def token_text(self, t: int) -> str:
+        s = lib().llama_vocab_get_text(self._vocab, int(t))
+        return s.decode("utf-8", "replace") if s is not None else ""
+
+    def bytes_per_token(self, n_kv: int) -> float:
+        return float(lib().llmi_bytes_per_token(self._h, int(n_kv)))
+
+    def arena(self) -> tuple[int, int]:
+        p, n = C.c_void_p(), C.c_uint64()
+        lib().llmi_model_arena(self._h, C.byref(p), C.byref(n))
+        return int(p.value or 0), int(n.value)
+
+    def replicate(self, devices: Sequence[int]) -> list["Model"]:
+        """In-process RCCL broadcast of the arena to `devices`."""
+        n = len(devices)
+        devs = (C.c_int32 * n)(*devices)
+        out = (C.c_void_p * n)()
+        if lib().llmi_replicate(self._h, devs, n, out) != 0:
+            raise LlmiError(last_error())
+        return [Model._from_handle(out[i], self.path, devices[i]) for i in range(n)]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().llama_model_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """llama_init_from_model: KV cache + scratch + step graphs on the model's device."""
+
+    def __init__(self, model: Model, n_ctx: int = 0, use_graphs: bool = True):
+        L = lib()
+        p = L.llama_context_default_params()
+        p.n_ctx = n_ctx
+        p.use_graphs = use_graphs
+        self._h = L.llama_init_from_model(model._h, p)
+        if not self._h:
+            raise LlmiError(last_error())
+        self.model = model
+        self.n_ctx = int(L.llama_n_ctx(self._h))
+
+    def decode(self, tokens: Sequence[int], pos: Optional[Sequence[int]] = None, logits_all: bool = False) -> int:
+        """llama_decode: returns 0 ok, 1 no KV slot, <0 error (same codes as upstream)."""
+        n = len(tokens)
+        toks = (C.c_int32 * n)(*tokens)
+        b = lib().llama_batch_get_one(toks, n)
+        keep = [toks]
+        if pos is not None:
+            pa = (C.c_int32 * n)(*pos)
+            b.pos = C.cast(pa, C.POINTER(C.c_int32))
+            keep.append(pa)
+        if logits_all:
+            la = (C.c_int8 * n)(*([1] * n))
+            b.logits = C.cast(la, C.POINTER(C.c_int8))
+            keep.append(la)
+        rc = int(lib().llama_decode(self._h, b))
+        del keep
+        return rc
+
+    def eval(self, tokens: Sequence[int], n_past: int) -> int:
+        n = len(tokens)
+        toks = (C.c_int32 * n)(*tokens)
+        return int(lib().llama_eval(self._h, toks, n, n_past))
+
+    def logits(self, i: int = -1) -> np.ndarray:
+        p = lib().llama_get_logits_ith(self._h, i)
+        if not p:
+            raise LlmiError(last_error())
+        return np.ctypeslib.as_array(p, shape=(self.model.n_vocab,)).copy()
+
+    def greedy(self, i: int = -1) -> int:
+        t = int(lib().llmi_greedy_ith(self._h, i))
+        if t < 0:
+            raise LlmiError(last_error())
+        return t
+
+    def generate_greedy(self, first: int, pos0: int, n: int) -> list[int]:
+        out = (C.c_int32 * n)()
+        r = lib().llmi_generate_greedy(self._h, int(first), int(pos0), int(n), out)
+        if r != n:
+            raise LlmiError(f"llmi_generate_greedy returned {r}: {last_error()}")
+        return list(out)
+
+    def stats(self) -> tuple[float, float]:
+        b, u = C.c_double(), C.c_double()
+        lib().llmi_last_step_stats(self._h, C.byref(b), C.byref(u))
+        return b.value, u.value
+
+    def kv_clear(self) -> None:
+        lib().llama_kv_self_clear(self._h)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().llama_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,712 @@
+/*
+ * ggml_oracle.c — TEST INFRASTRUCTURE ONLY (see ggml_oracle.h): CPU restatement of the
+ * reference's NGL=0 llama.cpp decode numerics.  PARITY UNPINNED by the reference
+ * (SURVEY.md §8c): llama.cpp is an un-vendored, unpinned dependency
+ * (Dockerfile.cpu:11 `FROM ghcr.io/ggml-org/llama.cpp:server`), invoked by
+ * scripts/start.sh:235 (`LLAMA_BIN=/app/llama-server`) with `-ngl $NGL` at
+ * scripts/start.sh:473-494; NGL=0 is the CPU path (Dockerfile.cpu:84-89).
+ *
+ * Every routine cites the upstream function it restates [upstream, recalled] and the
+ * SURVEY.md row it covers.  Deviations from upstream, all documented in DESIGN.md:
+ *   - exp() is llmi_expf (include/llmi_math.h) instead of libm/ggml SIMD exp;
+ *   - compiled with -ffp-contract=off (upstream's FMA contraction depends on -march);
+ *   - the Q4_K/Q5_K scale unpack uses get_scale_min_k4 (upstream's vec_dot uses the
+ *     equivalent utmp/kmask bit trick; both yield the same 8 scales and 8 mins).
+ */
+#include "ggml_oracle.h"
+
+#include <fcntl.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/llmi_math.h"
+
+#define QK_K 256
+#define QK8_0 32
+
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } block_q4_K;
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } block_q5_K;
+typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; } __attribute__((packed)) block_q6_K;
+typedef struct { uint16_t d; int8_t qs[32]; } __attribute__((packed)) block_q8_0;
+typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } block_q8_K;
+
+_Static_assert(sizeof(block_q4_K) == 144, "q4_K");
+_Static_assert(sizeof(block_q5_K) == 176, "q5_K");
+_Static_assert(sizeof(block_q6_K) == 210, "q6_K");
+_Static_assert(sizeof(block_q8_0) == 34, "q8_0");
+_Static_assert(sizeof(block_q8_K) == 292, "q8_K");
+
+static __thread char g_err[512];
+const char* or_last_error(void) { return g_err; }
+#define OR_FAIL(...) do { snprintf(g_err, sizeof g_err, __VA_ARGS__); goto fail; } while (0)
+
+float or_fp16_to_fp32(uint16_t h) { return llmi_h2f(h); }
+uint16_t or_fp32_to_fp16(float f) { return llmi_f2h(f); }
+float or_expf(float x) { return llmi_expf(x); }
+
+size_t or_type_size(int t) {
+    switch (t) {
+        case OR_F32: return 4; case OR_F16: return 2; case OR_Q8_0: return 34;
+        case OR_Q4_K: return 144; case OR_Q5_K: return 176; case OR_Q6_K: return 210;
+        case OR_Q8_K: return 292; default: return 0;
+    }
+}
+int or_block_size(int t) {
+    switch (t) {
+        case OR_F32: case OR_F16: return 1; case OR_Q8_0: return 32;
+        case OR_Q4_K: case OR_Q5_K: case OR_Q6_K: case OR_Q8_K: return 256; default: return 0;
+    }
+}
+/* upstream type_traits_cpu[...].vec_dot_type: K-quants -> Q8_K, Q8_0 -> Q8_0, F16 -> F16 */
+int or_vec_dot_type(int t) {
+    switch (t) {
+        case OR_Q4_K: case OR_Q5_K: case OR_Q6_K: return OR_Q8_K;
+        case OR_Q8_0: return OR_Q8_0; case OR_F16: return OR_F16; case OR_F32: return OR_F32;
+        default: return -1;
+    }
+}
+
+/* upstream get_scale_min_k4 (ggml-quants.c) — SURVEY.md Appendix A */
+static inline void get_scale_min_k4(int j, const uint8_t* q, uint8_t* d, uint8_t* m) {
+    if (j < 4) {
+        *d = q[j] & 63; *m = q[j + 4] & 63;
+    } else {
+        *d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        *m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4);
+    }
+}
+
+/* ---------------- dequantize_row_*  ---------------- */
+/* upstream dequantize_row_q4_K */
+static void deq_q4_K(const block_q4_K* x, float* y, int64_t k) {
+    for (int64_t i = 0; i < k / QK_K; i++) {
+        const uint8_t* q = x[i].qs;
+        const float d = llmi_h2f(x[i].d), min = llmi_h2f(x[i].dmin);
+        int is = 0; uint8_t sc, m;
+        for (int j = 0; j < QK_K; j += 64) {
+            get_scale_min_k4(is + 0, x[i].scales, &sc, &m);
+            const float d1 = d * sc, m1 = min * m;
+            get_scale_min_k4(is + 1, x[i].scales, &sc, &m);
+            const float d2 = d * sc, m2 = min * m;
+            for (int l = 0; l < 32; ++l) *y++ = d1 * (q[l] & 0xF) - m1;
+            for (int l = 0; l < 32; ++l) *y++ = d2 * (q[l] >> 4) - m2;
+            q += 32; is += 2;
+        }
+    }
+}
+/* upstream dequantize_row_q5_K */
+static void deq_q5_K(const block_q5_K* x, float* y, int64_t k) {
+    for (int64_t i = 0; i < k / QK_K; i++) {
+        const uint8_t* ql = x[i].qs; const uint8_t* qh = x[i].qh;
+        const float d = llmi_h2f(x[i].d), min = llmi_h2f(x[i].dmin);
+        int is = 0; uint8_t sc, m; uint8_t u1 = 1, u2 = 2;
+        for (int j = 0; j < QK_K; j += 64) {
+            get_scale_min_k4(is + 0, x[i].scales, &sc, &m);
+            const float d1 = d * sc, m1 = min * m;
+            get_scale_min_k4(is + 1, x[i].scales, &sc, &m);
+            const float d2 = d * sc, m2 = min * m;
+            for (int l = 0; l < 32; ++l) *y++ = d1 * ((ql[l] & 0xF) + (qh[l] & u1 ? 16 : 0)) - m1;
+            for (int l = 0; l < 32; ++l) *y++ = d2 * ((ql[l] >> 4) + (qh[l] & u2 ? 16 : 0)) - m2;
+            ql += 32; is += 2; u1 <<= 2; u2 <<= 2;
+        }
+    }
+}
+/* upstream dequantize_row_q6_K */
+static void deq_q6_K(const block_q6_K* x, float* y, int64_t k) {
+    for (int64_t i = 0; i < k / QK_K; i++) {
+        const float d = llmi_h2f(x[i].d);
+        const uint8_t* ql = x[i].ql; const uint8_t* qh = x[i].qh; const int8_t* sc = x[i].scales;
+        for (int n = 0; n < QK_K; n += 128) {
+            for (int l = 0; l < 32; ++l) {
+                int is = l / 16;
+                const int8_t q1 = (int8_t)((ql[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                const int8_t q2 = (int8_t)((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                const int8_t q3 = (int8_t)((ql[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                const int8_t q4 = (int8_t)((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+                y[l + 0] = d * sc[is + 0] * q1;
+                y[l + 32] = d * sc[is + 2] * q2;
+                y[l + 64] = d * sc[is + 4] * q3;
+                y[l + 96] = d * sc[is + 6] * q4;
+            }
+            y += 128; ql += 64; qh += 32; sc += 8;
+        }
+    }
+}
+/* upstream dequantize_row_q8_0 */
+static void deq_q8_0(const block_q8_0* x, float* y, int64_t k) {
+    for (int64_t i = 0; i < k / QK8_0; i++) {
+        const float d = llmi_h2f(x[i].d);
+        for (int j = 0; j < QK8_0; ++j) y[i * QK8_0 + j] = x[i].qs[j] * d;
+    }
+}
+
+int or_dequantize_row(int type, const void* src, float* dst, int64_t n) {
+    switch (type) {
+        case OR_F32: memcpy(dst, src, (size_t)n * 4); return 0;
+        case OR_F16: for (int64_t i = 0; i < n; ++i) dst[i] = llmi_h2f(((const uint16_t*)src)[i]); return 0;
+        case OR_Q4_K: deq_q4_K(src, dst, n); return 0;
+        case OR_Q5_K: deq_q5_K(src, dst, n); return 0;
+        case OR_Q6_K: deq_q6_K(src, dst, n); return 0;
+        case OR_Q8_0: deq_q8_0(src, dst, n); return 0;
+        default: return -1;
+    }
+}
+
+/* ---------------- activation quantization ---------------- */
+/* upstream quantize_row_q8_K_ref: signed max-abs per 256, iscale=-127/max, bsums per 16 */
+void or_quantize_row_q8_K(const float* x, void* vy, int64_t k) {
+    block_q8_K* y = vy;
+    for (int64_t i = 0; i < k / QK_K; i++) {
+        float max = 0, amax = 0;
+        for (int j = 0; j < QK_K; ++j) {
+            float ax = fabsf(x[j]);
+            if (ax > amax) { amax = ax; max = x[j]; }
+        }
+        if (!amax) {
+            y[i].d = 0;
+            memset(y[i].qs, 0, QK_K);
+            memset(y[i].bsums, 0, sizeof y[i].bsums);  /* upstream leaves bsums stale; zero is what they sum to */
+            x += QK_K;
+            continue;
+        }
+        const float iscale = -127.f / max;
+        for (int j = 0; j < QK_K; ++j) {
+            int v = llmi_nearest_int(iscale * x[j]);
+            y[i].qs[j] = (int8_t)(v < 127 ? v : 127);
+        }
+        for (int j = 0; j < QK_K / 16; ++j) {
+            int sum = 0;
+            for (int ii = 0; ii < 16; ++ii) sum += y[i].qs[j * 16 + ii];
+            y[i].bsums[j] = (int16_t)sum;
+        }
+        y[i].d = 1 / iscale;
+        x += QK_K;
+    }
+}
+/* upstream quantize_row_q8_0_ref: d = amax/127 (stored f16), q = roundf(x/d) */
+void or_quantize_row_q8_0(const float* x, void* vy, int64_t k) {
+    block_q8_0* y = vy;
+    for (int64_t i = 0; i < k / QK8_0; i++) {
+        float amax = 0.0f;
+        for (int j = 0; j < QK8_0; j++) {
+            const float v = x[i * QK8_0 + j];
+            amax = fmaxf(amax, fabsf(v));
+        }
+        const float d = amax / ((1 << 7) - 1);
+        const float id = d ? 1.0f / d : 0.0f;
+        y[i].d = llmi_f2h(d);
+        for (int j = 0; j < QK8_0; ++j) y[i].qs[j] = (int8_t)roundf(x[i * QK8_0 + j] * id);
+    }
+}
+
+/* ---------------- vec_dot ---------------- */
+/* upstream ggml_vec_dot_q4_K_q8_K_generic */
+static float vd_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
+    int8_t aux8[QK_K]; int16_t aux16[8]; float sums[8]; int32_t aux32[8];
+    memset(sums, 0, sizeof sums);
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const uint8_t* q4 = x[i].qs; const int8_t* q8 = y[i].qs;
+        memset(aux32, 0, sizeof aux32);
+        int8_t* a = aux8;
+        for (int j = 0; j < QK_K / 64; ++j) {
+            for (int l = 0; l < 32; ++l) a[l] = (int8_t)(q4[l] & 0xF);
+            a += 32;
+            for (int l = 0; l < 32; ++l) a[l] = (int8_t)(q4[l] >> 4);
+            a += 32; q4 += 32;
+        }
+        uint8_t scales[8], mins[8];
+        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &scales[j], &mins[j]);
+        int sumi = 0;
+        for (int j = 0; j < QK_K / 16; ++j) sumi += y[i].bsums[j] * mins[j / 2];
+        a = aux8;
+        int is = 0;
+        for (int j = 0; j < QK_K / 32; ++j) {
+            int32_t scale = scales[is++];
+            for (int r = 0; r < 4; ++r) {
+                for (int l = 0; l < 8; ++l) aux16[l] = (int16_t)(q8[l] * a[l]);
+                for (int l = 0; l < 8; ++l) aux32[l] += scale * aux16[l];
+                q8 += 8; a += 8;
+            }
+        }
+        const float d = llmi_h2f(x[i].d) * y[i].d;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+        const float dmin = llmi_h2f(x[i].dmin) * y[i].d;
+        sumf -= dmin * sumi;
+    }
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
+    return sumf;
+}
+/* upstream ggml_vec_dot_q5_K_q8_K_generic */
+static float vd_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
+    int8_t aux8[QK_K]; int16_t aux16[8]; float sums[8]; int32_t aux32[8];
+    memset(sums, 0, sizeof sums);
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const uint8_t* q4 = x[i].qs; const uint8_t* hm = x[i].qh; const int8_t* q8 = y[i].qs;
+        memset(aux32, 0, sizeof aux32);
+        int8_t* a = aux8;
+        uint8_t m = 1;
+        for (int j = 0; j < QK_K / 64; ++j) {
+            for (int l = 0; l < 32; ++l) a[l] = (int8_t)(q4[l] & 0xF);
+            for (int l = 0; l < 32; ++l) a[l] += (hm[l] & m ? 16 : 0);
+            a += 32; m <<= 1;
+            for (int l = 0; l < 32; ++l) a[l] = (int8_t)(q4[l] >> 4);
+            for (int l = 0; l < 32; ++l) a[l] += (hm[l] & m ? 16 : 0);
+            a += 32; m <<= 1;
+            q4 += 32;
+        }
+        uint8_t scales[8], mins[8];
+        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &scales[j], &mins[j]);
+        int sumi = 0;
+        for (int j = 0; j < QK_K / 16; ++j) sumi += y[i].bsums[j] * mins[j / 2];
+        a = aux8;
+        int is = 0;
+        for (int j = 0; j < QK_K / 32; ++j) {
+            int32_t scale = scales[is++];
+            for (int r = 0; r < 4; ++r) {
+                for (int l = 0; l < 8; ++l) aux16[l] = (int16_t)(q8[l] * a[l]);
+                for (int l = 0; l < 8; ++l) aux32[l] += scale * aux16[l];
+                q8 += 8; a += 8;
+            }
+        }
+        const float d = llmi_h2f(x[i].d) * y[i].d;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+        const float dmin = llmi_h2f(x[i].dmin) * y[i].d;
+        sumf -= dmin * sumi;
+    }
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
+    return sumf;
+}
+/* upstream ggml_vec_dot_q6_K_q8_K_generic */
+static float vd_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
+    int8_t aux8[QK_K]; int16_t aux16[8]; float sums[8]; int32_t aux32[8];
+    memset(sums, 0, sizeof sums);
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const uint8_t* q4 = x[i].ql; const uint8_t* qh = x[i].qh; const int8_t* q8 = y[i].qs;
+        memset(aux32, 0, sizeof aux32);
+        int8_t* a = aux8;
+        for (int j = 0; j < QK_K; j += 128) {
+            for (int l = 0; l < 32; ++l) {
+                a[l + 0] = (int8_t)((q4[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                a[l + 32] = (int8_t)((q4[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                a[l + 64] = (int8_t)((q4[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                a[l + 96] = (int8_t)((q4[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+            }
+            a += 128; q4 += 64; qh += 32;
+        }
+        a = aux8;
+        int is = 0;
+        for (int j = 0; j < QK_K / 16; ++j) {
+            int scale = x[i].scales[is++];
+            for (int r = 0; r < 2; ++r) {
+                for (int l = 0; l < 8; ++l) aux16[l] = (int16_t)(q8[l] * a[l]);
+                for (int l = 0; l < 8; ++l) aux32[l] += scale * aux16[l];
+                q8 += 8; a += 8;
+            }
+        }
+        const float d = llmi_h2f(x[i].d) * y[i].d;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+    }
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
+    return sumf;
+}
+/* upstream ggml_vec_dot_q8_0_q8_0 (generic tail loop) */
+static float vd_q8_0(int n, const block_q8_0* x, const block_q8_0* y) {
+    float sumf = 0;
+    for (int ib = 0; ib < n / QK8_0; ++ib) {
+        int sumi = 0;
+        for (int j = 0; j < QK8_0; j++) sumi += x[ib].qs[j] * y[ib].qs[j];
+        sumf += sumi * (llmi_h2f(x[ib].d) * llmi_h2f(y[ib].d));
+    }
+    return sumf;
+}
+/* upstream ggml_vec_dot_f16 (generic: double accumulation) */
+static float vd_f16(int n, const uint16_t* x, const uint16_t* y) {
+    double sumf = 0.0;
+    for (int i = 0; i < n; ++i) sumf += (double)(llmi_h2f(x[i]) * llmi_h2f(y[i]));
+    return (float)sumf;
+}
+/* upstream ggml_vec_dot_f32 (generic: double accumulation) */
+static float vd_f32(int n, const float* x, const float* y) {
+    double sumf = 0.0;
+    for (int i = 0; i < n; ++i) sumf += (double)(x[i] * y[i]);
+    return (float)sumf;
+}
+
+float or_vec_dot(int wtype, int n, const void* w, const void* a) {
+    switch (wtype) {
+        case OR_Q4_K: return vd_q4_K(n, w, a);
+        case OR_Q5_K: return vd_q5_K(n, w, a);
+        case OR_Q6_K: return vd_q6_K(n, w, a);
+        case OR_Q8_0: return vd_q8_0(n, w, a);
+        case OR_F16: return vd_f16(n, w, a);
+        case OR_F32: return vd_f32(n, w, a);
+        default: return NAN;
+    }
+}
+
+static size_t act_bytes(int wtype, int64_t cols) {
+    int vt = or_vec_dot_type(wtype);
+    return (size_t)(cols / or_block_size(vt)) * or_type_size(vt);
+}
+static void quantize_act(int wtype, const float* x, void* act, int64_t cols) {
+    int vt = or_vec_dot_type(wtype);
+    if (vt == OR_Q8_K) or_quantize_row_q8_K(x, act, cols);
+    else if (vt == OR_Q8_0) or_quantize_row_q8_0(x, act, cols);
+    else if (vt == OR_F16) for (int64_t i = 0; i < cols; ++i) ((uint16_t*)act)[i] = llmi_f2h(x[i]);
+    else memcpy(act, x, (size_t)cols * 4);
+}
+
+/* upstream ggml_compute_forward_mul_mat for one src1 column: src1 is converted to
+ * vec_dot_type once, then vec_dot per src0 row. */
+int or_matvec(int wtype, const void* W, int64_t rows, int64_t cols, const float* x, float* y, int nthreads) {
+    if (or_vec_dot_type(wtype) < 0 || cols % or_block_size(wtype)) return -1;
+    void* act = malloc(act_bytes(wtype, cols));
+    if (!act) return -1;
+    quantize_act(wtype, x, act, cols);
+    const size_t row_bytes = (size_t)(cols / or_block_size(wtype)) * or_type_size(wtype);
+    (void)nthreads;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int64_t r = 0; r < rows; ++r)
+        y[r] = or_vec_dot(wtype, (int)cols, (const uint8_t*)W + (size_t)r * row_bytes, act);
+    free(act);
+    return 0;
+}
+
+/* upstream ggml_compute_forward_rms_norm_f32 (sum of x*x in ggml_float=double,
+ * scale = 1/sqrtf(mean+eps)) followed by ggml_compute_forward_mul (y*w) */
+void or_rms_norm_mul(const float* x, const float* w, float* y, int n, float eps) {
+    double sum = 0.0;
+    for (int i = 0; i < n; ++i) sum += (double)(x[i] * x[i]);
+    const float mean = (float)(sum / n);
+    const float scale = 1.0f / sqrtf(mean + eps);
+    for (int i = 0; i < n; ++i) y[i] = x[i] * scale;
+    for (int i = 0; i < n; ++i) y[i] = y[i] * w[i];
+}
+
+/* =======================================================================
+ * GGUF v3 reader (independent of the product's loader) — SURVEY.md §8a row a4,
+ * format per SURVEY.md Appendix A.
+ * ======================================================================= */
+enum { G_U8, G_I8, G_U16, G_I16, G_U32, G_I32, G_F32, G_BOOL, G_STR, G_ARR, G_U64, G_I64, G_F64 };
+
+typedef struct { char name[96]; int type; int n_dims; int64_t ne[4]; uint64_t offset; const uint8_t* data; } or_tensor;
+
+typedef struct {
+    const uint8_t* p; const uint8_t* end; int ok;
+} rd_t;
+static uint64_t rd_u(rd_t* r, int n) {
+    if (r->p + n > r->end) { r->ok = 0; return 0; }
+    uint64_t v = 0;
+    for (int i = 0; i < n; ++i) v |= (uint64_t)r->p[i] << (8 * i);
+    r->p += n; return v;
+}
+static size_t g_scalar_size(int t) {
+    switch (t) {
+        case G_U8: case G_I8: case G_BOOL: return 1; case G_U16: case G_I16: return 2;
+        case G_U32: case G_I32: case G_F32: return 4; case G_U64: case G_I64: case G_F64: return 8;
+        default: return 0;
+    }
+}
+static void rd_skip_value(rd_t* r, int t) {
+    if (t == G_STR) { uint64_t n = rd_u(r, 8); if (r->p + n > r->end) r->ok = 0; else r->p += n; return; }
+    if (t == G_ARR) {
+        int et = (int)rd_u(r, 4); uint64_t n = rd_u(r, 8);
+        for (uint64_t i = 0; i < n && r->ok; ++i) rd_skip_value(r, et);
+        return;
+    }
+    size_t s = g_scalar_size(t);
+    if (!s || r->p + s > r->end) { r->ok = 0; return; }
+    r->p += s;
+}
+static double rd_num(rd_t* r, int t) {
+    uint64_t v = rd_u(r, (int)g_scalar_size(t));
+    switch (t) {
+        case G_I8: return (int8_t)v; case G_I16: return (int16_t)v; case G_I32: return (int32_t)v;
+        case G_I64: return (double)(int64_t)v;
+        case G_F32: { uint32_t u = (uint32_t)v; return llmi_u2f(u); }
+        case G_F64: { double d; memcpy(&d, &v, 8); return d; }
+        default: return (double)v;
+    }
+}
+
+struct or_model {
+    /* file */
+    int fd; uint8_t* map; size_t map_len;
+    int n_tensors; or_tensor* tensors;
+    /* hparams */
+    int n_embd, n_layer, n_head, n_head_kv, n_ff, n_vocab, n_rot, head_dim, n_ctx, file_type;
+    float eps, rope_base;
+    /* weights */
+    const or_tensor *tok_embd, *out_norm, *output, *rope_freqs;
+    struct { const or_tensor *an, *wq, *wk, *wv, *wo, *fn, *wg, *wu, *wd; } *L;
+    /* state */
+    uint16_t *kc, *vc;       /* [layer][pos][n_head_kv*head_dim] f16 */
+    float *x, *xb, *q, *k, *v, *att, *hb, *hb2, *tmp, *sc;
+    float *tap_embd, *tap_final;
+};
+
+static const or_tensor* find_t(const or_model* m, const char* name) {
+    for (int i = 0; i < m->n_tensors; ++i) if (!strcmp(m->tensors[i].name, name)) return &m->tensors[i];
+    return NULL;
+}
+
+static int key_eq(const uint8_t* s, uint64_t n, const char* k) { return strlen(k) == n && !memcmp(s, k, n); }
+
+or_model* or_model_load(const char* path, int n_ctx) {
+    or_model* m = calloc(1, sizeof *m);
+    if (!m) return NULL;
+    m->fd = -1;
+    m->rope_base = 10000.0f; m->eps = 1e-5f;
+    struct stat st;
+    m->fd = open(path, O_RDONLY);
+    if (m->fd < 0) OR_FAIL("open %s failed", path);
+    if (fstat(m->fd, &st)) OR_FAIL("stat failed");
+    m->map_len = (size_t)st.st_size;
+    m->map = mmap(NULL, m->map_len, PROT_READ, MAP_PRIVATE, m->fd, 0);
+    if (m->map == MAP_FAILED) { m->map = NULL; OR_FAIL("mmap failed"); }
+    rd_t r = {m->map, m->map + m->map_len, 1};
+    if (rd_u(&r, 4) != 0x46554747u) OR_FAIL("bad magic");
+    uint32_t version = (uint32_t)rd_u(&r, 4);
+    if (version != 3) OR_FAIL("unsupported GGUF version %u", version);
+    uint64_t n_tensors = rd_u(&r, 8), n_kv = rd_u(&r, 8);
+    uint64_t alignment = 32;
+    int64_t arch_vocab = -1, toks_n = -1;
+    for (uint64_t i = 0; i < n_kv && r.ok; ++i) {
+        uint64_t kl = rd_u(&r, 8);
+        const uint8_t* key = r.p;
+        if (r.p + kl > r.end) { r.ok = 0; break; }
+        r.p += kl;
+        int t = (int)rd_u(&r, 4);
+        if (t == G_STR || t == G_ARR) {
+            if (t == G_ARR && key_eq(key, kl, "tokenizer.ggml.tokens")) {
+                const uint8_t* save = r.p; rd_u(&r, 4); toks_n = (int64_t)rd_u(&r, 8); r.p = save;
+            }
+            rd_skip_value(&r, t);
+            continue;
+        }
+        double v = rd_num(&r, t);
+#define KV(name, field) else if (key_eq(key, kl, name)) m->field = (typeof(m->field))v
+        if (key_eq(key, kl, "general.alignment")) alignment = (uint64_t)v;
+        KV("llama.embedding_length", n_embd); KV("llama.block_count", n_layer);
+        KV("llama.feed_forward_length", n_ff); KV("llama.attention.head_count", n_head);
+        KV("llama.attention.head_count_kv", n_head_kv); KV("llama.rope.dimension_count", n_rot);
+        KV("llama.attention.layer_norm_rms_epsilon", eps); KV("llama.rope.freq_base", rope_base);
+        KV("general.file_type", file_type);
+        else if (key_eq(key, kl, "llama.vocab_size")) arch_vocab = (int64_t)v;
+#undef KV
+    }
+    if (!r.ok) OR_FAIL("truncated metadata");
+    if (!m->n_embd || !m->n_layer || !m->n_head) OR_FAIL("missing llama.* hyperparameters");
+    if (!m->n_head_kv) m->n_head_kv = m->n_head;
+    m->head_dim = m->n_embd / m->n_head;
+    if (!m->n_rot) m->n_rot = m->head_dim;
+    m->n_tensors = (int)n_tensors;
+    m->tensors = calloc(n_tensors ? n_tensors : 1, sizeof(or_tensor));
+    for (uint64_t i = 0; i < n_tensors && r.ok; ++i) {
+        or_tensor* T = &m->tensors[i];
+        uint64_t nl = rd_u(&r, 8);
+        if (nl >= sizeof T->name || r.p + nl > r.end) OR_FAIL("bad tensor name");
+        memcpy(T->name, r.p, nl); r.p += nl;
+        T->n_dims = (int)rd_u(&r, 4);
+        if (T->n_dims < 1 || T->n_dims > 4) OR_FAIL("bad n_dims");
+        for (int d = 0; d < 4; ++d) T->ne[d] = 1;
+        for (int d = 0; d < T->n_dims; ++d) T->ne[d] = (int64_t)rd_u(&r, 8);
+        T->type = (int)rd_u(&r, 4);
+        T->offset = rd_u(&r, 8);
+    }
+    if (!r.ok) OR_FAIL("truncated tensor infos");
+    size_t data_start = (size_t)(r.p - m->map);
+    data_start = (data_start + alignment - 1) / alignment * alignment;
+    for (int i = 0; i < m->n_tensors; ++i) {
+        or_tensor* T = &m->tensors[i];
+        int64_t n = T->ne[0] * T->ne[1] * T->ne[2] * T->ne[3];
+        size_t bytes = (size_t)(n / or_block_size(T->type)) * or_type_size(T->type);
+        if (!or_type_size(T->type)) OR_FAIL("tensor %s: unsupported type %d", T->name, T->type);
+        if (data_start + T->offset + bytes > m->map_len) OR_FAIL("tensor %s out of file", T->name);
+        T->data = m->map + data_start + T->offset;
+    }
+    m->tok_embd = find_t(m, "token_embd.weight");
+    m->out_norm = find_t(m, "output_norm.weight");
+    m->output = find_t(m, "output.weight");
+    m->rope_freqs = find_t(m, "rope_freqs.weight");
+    if (!m->tok_embd || !m->out_norm) OR_FAIL("missing token_embd/output_norm");
+    if (!m->output) m->output = m->tok_embd;  /* tied embeddings */
+    m->n_vocab = (int)m->tok_embd->ne[1];
+    (void)arch_vocab; (void)toks_n;
+    m->L = calloc((size_t)m->n_layer, sizeof *m->L);
+    for (int l = 0; l < m->n_layer; ++l) {
+        char nm[96];
+#define LT(f, s) do { snprintf(nm, sizeof nm, "blk.%d.%s.weight", l, s); m->L[l].f = find_t(m, nm); \
+                      if (!m->L[l].f) OR_FAIL("missing %s", nm); } while (0)
+        LT(an, "attn_norm"); LT(wq, "attn_q"); LT(wk, "attn_k"); LT(wv, "attn_v"); LT(wo, "attn_output");
+        LT(fn, "ffn_norm"); LT(wg, "ffn_gate"); LT(wu, "ffn_up"); LT(wd, "ffn_down");
+#undef LT
+    }
+    if (!m->n_ff) m->n_ff = (int)m->L[0].wg->ne[1];
+    m->n_ctx = n_ctx > 0 ? n_ctx : 512;
+    const size_t kvd = (size_t)m->n_head_kv * m->head_dim;
+    m->kc = calloc((size_t)m->n_layer * m->n_ctx * kvd, 2);
+    m->vc = calloc((size_t)m->n_layer * m->n_ctx * kvd, 2);
+    const int E = m->n_embd, F = m->n_ff;
+    m->x = calloc(E, 4); m->xb = calloc(E, 4); m->q = calloc(E, 4);
+    m->k = calloc(kvd, 4); m->v = calloc(kvd, 4); m->att = calloc(E, 4);
+    m->hb = calloc(F, 4); m->hb2 = calloc(F, 4); m->tmp = calloc(E > F ? E : F, 4);
+    m->sc = calloc((size_t)m->n_head * m->n_ctx, 4);
+    m->tap_embd = calloc(E, 4); m->tap_final = calloc(E, 4);
+    if (!m->kc || !m->vc || !m->sc) OR_FAIL("out of memory");
+    return m;
+fail:
+    or_model_free(m);
+    return NULL;
+}
+
+void or_model_free(or_model* m) {
+    if (!m) return;
+    if (m->map) munmap(m->map, m->map_len);
+    if (m->fd >= 0) close(m->fd);
+    free(m->tensors); free(m->L); free(m->kc); free(m->vc);
+    free(m->x); free(m->xb); free(m->q); free(m->k); free(m->v); free(m->att);
+    free(m->hb); free(m->hb2); free(m->tmp); free(m->sc); free(m->tap_embd); free(m->tap_final);
+    free(m);
+}
+
+void or_model_info(const or_model* m, int64_t* o) {
+    o[0] = m->n_embd; o[1] = m->n_layer; o[2] = m->n_head; o[3] = m->n_head_kv; o[4] = m->n_ff;
+    o[5] = m->n_vocab; o[6] = m->n_rot; o[7] = m->n_ctx; o[8] = m->head_dim; o[9] = m->file_type;
+}
+
+void or_kv_clear(or_model* m) {
+    const size_t kvd = (size_t)m->n_head_kv * m->head_dim;
+    memset(m->kc, 0, (size_t)m->n_layer * m->n_ctx * kvd * 2);
+    memset(m->vc, 0, (size_t)m->n_layer * m->n_ctx * kvd * 2);
+}
+
+static size_t tensor_bytes(const or_tensor* T) {
+    int64_t n = T->ne[0] * T->ne[1] * T->ne[2] * T->ne[3];
+    return (size_t)(n / or_block_size(T->type)) * or_type_size(T->type);
+}
+
+double or_bytes_per_token(const or_model* m, int ctx) {
+    double b = 0;
+    for (int l = 0; l < m->n_layer; ++l) {
+        b += tensor_bytes(m->L[l].wq) + tensor_bytes(m->L[l].wk) + tensor_bytes(m->L[l].wv) + tensor_bytes(m->L[l].wo);
+        b += tensor_bytes(m->L[l].wg) + tensor_bytes(m->L[l].wu) + tensor_bytes(m->L[l].wd);
+        b += tensor_bytes(m->L[l].an) + tensor_bytes(m->L[l].fn);
+    }
+    b += tensor_bytes(m->output) + tensor_bytes(m->out_norm);
+    b += (double)tensor_bytes(m->tok_embd) / m->n_vocab;
+    b += (double)m->n_layer * 2.0 * m->n_head_kv * m->head_dim * 2.0 * (ctx + 1);
+    return b;
+}
+
+/* upstream ggml_rope_cache_init + rope_yarn (ext_factor 0, freq_scale 1, attn_factor 1)
+ * and the NORM-mode rotation of adjacent pairs in ggml_compute_forward_rope_f32.
+ * theta is built by iterative multiplication by theta_scale = powf(base, -2/n_dims). */
+static void rope_norm(float* v, int n_heads, int head_dim, int n_rot, int pos, float base, const float* ff) {
+    const float theta_scale = powf(base, -2.0f / n_rot);
+    float cache[1024];
+    float theta = (float)pos;
+    for (int i0 = 0; i0 < n_rot; i0 += 2) {
+        const float f = ff ? ff[i0 / 2] : 1.0f;
+        const float th = 1.0f * (theta / f);
+        cache[i0 + 0] = cosf(th) * 1.0f;
+        cache[i0 + 1] = sinf(th) * 1.0f;
+        theta *= theta_scale;
+    }
+    for (int h = 0; h < n_heads; ++h) {
+        float* s = v + (size_t)h * head_dim;
+        for (int i0 = 0; i0 < n_rot; i0 += 2) {
+            const float c = cache[i0], sn = cache[i0 + 1];
+            const float x0 = s[i0], x1 = s[i0 + 1];
+            s[i0] = x0 * c - x1 * sn;
+            s[i0 + 1] = x0 * sn + x1 * c;
+        }
+    }
+}
+
+static void matvec_t(const or_tensor* T, const float* x, float* y, int nth) {
+    or_matvec(T->type, T->data, T->ne[1], T->ne[0], x, y, nth);
+}
+
+/* One decode step of llm_build_llama [upstream llama-model.cpp] with the non-flash
+ * attention path: kq = mul_mat(K_f16, q) (q rounded to f16, ggml_vec_dot_f16),
+ * soft_max_ext(kq, scale = 1/sqrt(head_dim)) with double sum, kqv = mul_mat(V_f16,
+ * kq) (probabilities rounded to f16).  SURVEY.md §8a rows a10-a16. */
+int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
+    if (token < 0 || token >= m->n_vocab) { snprintf(g_err, sizeof g_err, "token %d out of range", token); return -1; }
+    if (pos < 0 || pos >= m->n_ctx) { snprintf(g_err, sizeof g_err, "pos %d out of ctx", pos); return 1; }
+    const int E = m->n_embd, H = m->n_head, HK = m->n_head_kv, D = m->head_dim, F = m->n_ff;
+    const int kvd = HK * D, gqa = H / HK, n_kv = pos + 1;
+    const float* ff = m->rope_freqs ? (const float*)m->rope_freqs->data : NULL;
+    /* get_rows(token_embd, token) -> dequantize one row */
+    {
+        const size_t rb = tensor_bytes(m->tok_embd) / m->n_vocab;
+        or_dequantize_row(m->tok_embd->type, m->tok_embd->data + (size_t)token * rb, m->x, E);
+        memcpy(m->tap_embd, m->x, (size_t)E * 4);
+    }
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    for (int l = 0; l < m->n_layer; ++l) {
+        or_rms_norm_mul(m->x, (const float*)m->L[l].an->data, m->xb, E, m->eps);
+        matvec_t(m->L[l].wq, m->xb, m->q, nth);
+        matvec_t(m->L[l].wk, m->xb, m->k, nth);
+        matvec_t(m->L[l].wv, m->xb, m->v, nth);
+        rope_norm(m->q, H, D, m->n_rot, pos, m->rope_base, ff);
+        rope_norm(m->k, HK, D, m->n_rot, pos, m->rope_base, ff);
+        uint16_t* kl = m->kc + ((size_t)l * m->n_ctx) * kvd;
+        uint16_t* vl = m->vc + ((size_t)l * m->n_ctx) * kvd;
+        for (int i = 0; i < kvd; ++i) { kl[(size_t)pos * kvd + i] = llmi_f2h(m->k[i]); vl[(size_t)pos * kvd + i] = llmi_f2h(m->v[i]); }
+#pragma omp parallel for schedule(static) num_threads(nth > 0 ? nth : 1)
+        for (int h = 0; h < H; ++h) {
+            const int g = h / gqa;
+            uint16_t qh[512];
+            for (int d = 0; d < D; ++d) qh[d] = llmi_f2h(m->q[(size_t)h * D + d]);
+            float* w = m->sc + (size_t)h * m->n_ctx;
+            float mx = -INFINITY;
+            for (int t = 0; t < n_kv; ++t) {
+                float s = vd_f16(D, kl + (size_t)t * kvd + (size_t)g * D, qh);
+                w[t] = s * kq_scale;
+                mx = fmaxf(mx, w[t]);
+            }
+            double sum = 0.0;
+            for (int t = 0; t < n_kv; ++t) { float e = llmi_expf(w[t] - mx); sum += (double)e; w[t] = e; }
+            const float inv = (float)(1.0 / sum);
+            for (int t = 0; t < n_kv; ++t) w[t] = w[t] * inv;
+            for (int d = 0; d < D; ++d) {
+                double acc = 0.0;
+                for (int t = 0; t < n_kv; ++t)
+                    acc += (double)(llmi_h2f(vl[(size_t)t * kvd + (size_t)g * D + d]) * llmi_h2f(llmi_f2h(w[t])));
+                m->att[(size_t)h * D + d] = (float)acc;
+            }
+        }
+        matvec_t(m->L[l].wo, m->att, m->tmp, nth);
+        for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
+        or_rms_norm_mul(m->x, (const float*)m->L[l].fn->data, m->xb, E, m->eps);
+        matvec_t(m->L[l].wg, m->xb, m->hb, nth);
+        matvec_t(m->L[l].wu, m->xb, m->hb2, nth);
+        for (int i = 0; i < F; ++i) m->hb[i] = llmi_silu(m->hb[i]) * m->hb2[i];
+        matvec_t(m->L[l].wd, m->hb, m->tmp, nth);
+        for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
+    }
+    memcpy(m->tap_final, m->x, (size_t)E * 4);
+    or_rms_norm_mul(m->x, (const float*)m->out_norm->data, m->xb, E, m->eps);
+    or_matvec(m->output->type, m->output->data, m->n_vocab, E, m->xb, logits, nth);
+    return 0;
+}
+
+int or_tap(const or_model* m, int which, float* out) {
+    if (which == 0) memcpy(out, m->tap_embd, (size_t)m->n_embd * 4);
+    else if (which == 1) memcpy(out, m->tap_final, (size_t)m->n_embd * 4);
+    else return -1;
+    return 0;
+}

@@ -1,0 +1,161 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (oracle/ggml_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this, as
+the checker.  PARITY UNPINNED by the reference (see ggml_oracle.h / SURVEY.md §8c).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libggml_oracle.so")
+
+F32, F16, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 8, 12, 13, 14, 15
+BLOCK_ELEMS = {F32: 1, F16: 1, Q8_0: 32, Q4_K: 256, Q5_K: 256, Q6_K: 256, Q8_K: 256}
+BLOCK_BYTES = {F32: 4, F16: 2, Q8_0: 34, Q4_K: 144, Q5_K: 176, Q6_K: 210, Q8_K: 292}
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    L = C.CDLL(LIB)
+    P = C.c_void_p
+    sig = {
+        "or_type_size": (C.c_size_t, [C.c_int]),
+        "or_block_size": (C.c_int, [C.c_int]),
+        "or_vec_dot_type": (C.c_int, [C.c_int]),
+        "or_fp16_to_fp32": (C.c_float, [C.c_uint16]),
+        "or_fp32_to_fp16": (C.c_uint16, [C.c_float]),
+        "or_expf": (C.c_float, [C.c_float]),
+        "or_dequantize_row": (C.c_int, [C.c_int, P, P, C.c_int64]),
+        "or_quantize_row_q8_K": (None, [P, P, C.c_int64]),
+        "or_quantize_row_q8_0": (None, [P, P, C.c_int64]),
+        "or_vec_dot": (C.c_float, [C.c_int, C.c_int, P, P]),
+        "or_matvec": (C.c_int, [C.c_int, P, C.c_int64, C.c_int64, P, P, C.c_int]),
+        "or_rms_norm_mul": (None, [P, P, P, C.c_int, C.c_float]),
+        "or_model_load": (P, [C.c_char_p, C.c_int]),
+        "or_model_free": (None, [P]),
+        "or_last_error": (C.c_char_p, []),
+        "or_model_info": (None, [P, P]),
+        "or_decode": (C.c_int, [P, C.c_int32, C.c_int32, P, C.c_int]),
+        "or_kv_clear": (None, [P]),
+        "or_tap": (C.c_int, [P, C.c_int, P]),
+        "or_bytes_per_token": (C.c_double, [P, C.c_int]),
+    }
+    for k, (r, a) in sig.items():
+        f = getattr(L, k)
+        f.restype = r
+        f.argtypes = a
+    _lib = L
+    return L
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def nthreads() -> int:
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def dequantize(type_: int, raw: np.ndarray, n: int) -> np.ndarray:
+    raw = np.ascontiguousarray(raw, dtype=np.uint8)
+    out = np.empty(n, dtype=np.float32)
+    assert lib().or_dequantize_row(type_, _p(raw), _p(out), n) == 0
+    return out
+
+
+def quantize_q8_K(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.zeros(x.size // 256 * 292, dtype=np.uint8)
+    lib().or_quantize_row_q8_K(_p(x), _p(out), x.size)
+    return out
+
+
+def quantize_q8_0(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.zeros(x.size // 32 * 34, dtype=np.uint8)
+    lib().or_quantize_row_q8_0(_p(x), _p(out), x.size)
+    return out
+
+
+def quantize_act(wtype: int, x: np.ndarray) -> np.ndarray:
+    return quantize_q8_0(x) if wtype == Q8_0 else quantize_q8_K(x)
+
+
+def rms_norm_mul(x: np.ndarray, w: np.ndarray, eps: float) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    y = np.empty_like(x)
+    lib().or_rms_norm_mul(_p(x), _p(w), _p(y), x.size, eps)
+    return y
+
+
+def matvec(type_: int, W: np.ndarray, rows: int, cols: int, x: np.ndarray, threads: int = 0) -> np.ndarray:
+    W = np.ascontiguousarray(W, dtype=np.uint8)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty(rows, dtype=np.float32)
+    assert lib().or_matvec(type_, _p(W), rows, cols, _p(x), _p(y), threads or nthreads()) == 0
+    return y
+
+
+def expf(x: float) -> float:
+    return float(lib().or_expf(x))
+
+
+class OracleModel:
+    """Whole-model decode (llm_build_llama order) on the CPU, f16 KV cache."""
+
+    def __init__(self, path: str, n_ctx: int = 512, threads: int = 0):
+        L = lib()
+        self._h = L.or_model_load(path.encode(), n_ctx)
+        if not self._h:
+            raise RuntimeError("oracle load failed: " + L.or_last_error().decode())
+        info = np.zeros(10, dtype=np.int64)
+        L.or_model_info(self._h, _p(info))
+        (self.n_embd, self.n_layer, self.n_head, self.n_head_kv, self.n_ff, self.n_vocab,
+         self.n_rot, self.n_ctx, self.head_dim, self.file_type) = (int(v) for v in info)
+        self.threads = threads or nthreads()
+
+    def decode(self, token: int, pos: int) -> np.ndarray:
+        out = np.empty(self.n_vocab, dtype=np.float32)
+        rc = lib().or_decode(self._h, int(token), int(pos), _p(out), self.threads)
+        if rc != 0:
+            raise RuntimeError(f"or_decode rc={rc}: " + lib().or_last_error().decode())
+        return out
+
+    def tap(self, which: int) -> np.ndarray:
+        out = np.empty(self.n_embd, dtype=np.float32)
+        lib().or_tap(self._h, which, _p(out))
+        return out
+
+    def kv_clear(self) -> None:
+        lib().or_kv_clear(self._h)
+
+    def bytes_per_token(self, ctx: int) -> float:
+        return float(lib().or_bytes_per_token(self._h, ctx))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().or_model_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

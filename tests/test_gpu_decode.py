@@ -1,0 +1,121 @@
+"""End-to-end parity of the HIP decode path (through the C ABI) against the CPU oracle.
+
+North-star bar (BASELINE.json): logits within 1e-3 (absolute) of the CPU path on the
+same GGUF and prompt, and bit-exact greedy token ids.  Models: the two tiny
+mixed-type presets (every quant type, head_dim 64/128, GQA 2, odd vocab) and
+reduced-depth Llama-3-8B / TinyLlama shapes (exact widths, 2 layers).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import llmi
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3  # north_star: "within 1e-3 logit tolerance"
+
+
+def run_parity(path, prompt, n_gen, n_ctx=128):
+    om = po.OracleModel(path, n_ctx=n_ctx)
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=n_ctx)
+    worst = 0.0
+    toks = list(prompt)
+    gpu_ids, ora_ids, margins = [], [], []
+    pos = 0
+    cur = toks[0]
+    for step in range(len(prompt) + n_gen - 1):
+        lo = om.decode(cur, pos)
+        assert c.decode([cur], pos=[pos]) == 0
+        lg = c.logits(-1)
+        d = float(np.abs(lg - lo).max())
+        worst = max(worst, d)
+        assert d <= LOGIT_TOL, f"step {step}: max |dlogit| {d:.3g}"
+        g_gpu = c.greedy(-1)
+        assert g_gpu == int(np.argmax(lg)), "device argmax disagrees with host argmax of the same logits"
+        srt = np.sort(lo)
+        margins.append(float(srt[-1] - srt[-2]))
+        pos += 1
+        if pos < len(prompt):
+            cur = prompt[pos]
+        else:
+            ora_ids.append(int(np.argmax(lo)))
+            gpu_ids.append(g_gpu)
+            cur = ora_ids[-1]
+    return worst, gpu_ids, ora_ids, margins, m, c
+
+
+@pytest.mark.parametrize("preset", ["tiny-mixed", "tiny-mixed-d128"])
+def test_decode_parity_tiny(gpu, tiny_models, preset):
+    path = tiny_models[preset]
+    rng = np.random.default_rng(2)
+    prompt = [1] + list(rng.integers(3, 700, 11))
+    worst, g, o, margins, m, c = run_parity(path, prompt, 16)
+    assert g == o, f"greedy ids differ: gpu {g} oracle {o}"
+    print(f"{preset}: worst |dlogit| {worst:.2e}, min top-2 margin {min(margins):.2e}")
+
+
+def test_generate_greedy_matches_stepwise(gpu, tiny_models):
+    path = tiny_models["tiny-mixed-d128"]
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=256)
+    prompt = [1, 5, 9, 400, 77]
+    assert c.decode(prompt) == 0
+    first = c.greedy(-1)
+    seq = c.generate_greedy(first, len(prompt), 40)
+    # stepwise through llama_decode
+    c2 = llmi.Context(m, n_ctx=256)
+    assert c2.decode(prompt) == 0
+    t = c2.greedy(-1)
+    step = []
+    for k in range(40):
+        assert c2.decode([t], pos=[len(prompt) + k]) == 0
+        t = c2.greedy(-1)
+        step.append(t)
+    assert seq == step
+
+
+def test_batch_decode_equals_single(gpu, tiny_models):
+    """A multi-token llama_decode batch gives bit-identical logits to one-by-one calls,
+    and graph replay equals eager launches bit for bit."""
+    path = tiny_models["tiny-mixed"]
+    m = llmi.Model(path)
+    prompt = [1, 17, 300, 42, 999, 5, 6]
+    a = llmi.Context(m, n_ctx=64)
+    assert a.decode(prompt, logits_all=True) == 0
+    la = [a.logits(i) for i in range(len(prompt))]
+    b = llmi.Context(m, n_ctx=64, use_graphs=False)
+    for i, t in enumerate(prompt):
+        assert b.decode([t], pos=[i]) == 0
+        assert np.array_equal(b.logits(-1), la[i])
+
+
+def test_decode_error_codes(gpu, tiny_models):
+    m = llmi.Model(tiny_models["tiny-mixed"])
+    c = llmi.Context(m, n_ctx=32)
+    assert c.decode([1], pos=[32]) == 1          # no KV slot
+    assert c.decode([m.n_vocab]) == -1            # invalid token
+    assert c.decode([1, 2, 3]) == 0
+    assert c.eval([4, 5], 3) == 0
+    with pytest.raises(llmi.LlmiError):
+        llmi.Model(tiny_models["tiny-mixed"], n_gpu_layers=0)   # no CPU fallback
+    c.kv_clear()
+    assert c.decode([1]) == 0
+
+
+@pytest.mark.parametrize("preset,n_layer,n_vocab", [("llama3-8b-q4km", 2, 0), ("tinyllama-q8_0", 2, 0),
+                                                    ("mistral7b-q5km", 2, 0)])
+def test_decode_parity_real_widths(gpu, synth_dir, preset, n_layer, n_vocab):
+    """Exact Llama-3-8B / TinyLlama / Mistral widths (E, FF, heads, vocab), 2 layers."""
+    path = str(synth_dir / f"{preset}-L{n_layer}.gguf")
+    llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=n_layer, n_vocab=n_vocab)
+    prompt = [1, 100, 2000, 31000]
+    worst, g, o, margins, m, c = run_parity(path, prompt, 4, n_ctx=64)
+    for k, (a, b) in enumerate(zip(g, o)):
+        if a != b:
+            assert margins[len(prompt) - 1 + k] < 2 * LOGIT_TOL, f"id mismatch at {k} with margin"
+            break
+    print(f"{preset}: worst |dlogit| {worst:.2e}")
