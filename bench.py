@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py — decode tokens/sec + achieved HBM GB/s, Llama-3-8B Q4_K_M, 1->8 MI355X.
+
+BASELINE.json `metric` on `configs[1]`: Llama-3-8B-Instruct Q4_K_M, 128-token prompt ->
+greedy decode, one model replica per GPU.  A STEP is one decoded token (one pass of the
+hot path: 194 kernel launches replayed from a HIP graph; the next token is fed back on
+the device).  Workload per rank: prefill the 128-token prompt (untimed), W warmup
+tokens, then K timed tokens (defaults W=32, K=480: 512 generated tokens, 128->640 ctx).
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): replicas only — each rank
+decodes its own stream (prompt seed 4+rank) with no data-path collective; rank 0's
+weights are fanned out to the other ranks by one RCCL broadcast over xGMI
+(llmi_model_fanout), outside the timed region.  value = N*K / max-over-ranks time.
+
+Synthetic data: a GGUF with the exact Llama-3-8B Q4_K_M shapes and type table,
+random-init blocks (llmi_synth.h); there is no network for real checkpoints.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "llama-gguf-inference_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak per GPU (MI355X_MICROARCH.md)
+DOMINANT = "ffn_gate_up"  # k_matvec<0,true,3>: fused ffn_gate+ffn_up Q4_K matvec + SwiGLU
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=480)
+    ap.add_argument("--warmup", type=int, default=32)
+    ap.add_argument("--prompt", type=int, default=128)
+    ap.add_argument("--preset", default="llama3-8b-q4km")
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--model-dir", default=os.environ.get("LLMI_BENCH_DIR", "/tmp/llmi_bench"))
+    ap.add_argument("--profile-steps", type=int, default=8)
+    ap.add_argument("--cpu-sample-tokens", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args(argv)
+
+
+class Dist:
+    """Barrier / max-reduce / broadcast over torch.distributed when WORLD_SIZE > 1."""
+
+    def __init__(self, backend: str):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if backend == "nccl":
+                torch.cuda.set_device(self.local_rank)
+            dist.init_process_group(backend=backend)
+            self.dist = dist
+            self.backend = backend
+
+    def barrier(self):
+        if self.dist:
+            if self.backend == "nccl":
+                import torch
+
+                self.dist.barrier(device_ids=[self.local_rank])
+                torch.cuda.synchronize()
+            else:
+                self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if not self.dist:
+            return v
+        import torch
+
+        dev = f"cuda:{self.local_rank}" if self.backend == "nccl" else "cpu"
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed_decode(engine, dist: Dist, steps: int, warmup: int) -> tuple[float, float]:
+    """The contract's timed region: W untimed warmup steps, then exactly K steps bracketed
+    by barrier + device sync on both sides; returns (this rank's seconds, max over ranks)."""
+    engine.warmup(warmup)
+    dist.barrier()
+    engine.sync()
+    t0 = time.perf_counter()
+    engine.run(steps)
+    engine.sync()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    return dt, dist.max(dt)
+
+
+class LlmiEngine:
+    """One replica on this rank's GPU driven through the C ABI (libllmi.so)."""
+
+    def __init__(self, args, dist: Dist):
+        import numpy as np
+
+        import llmi
+
+        self.llmi = llmi
+        self.args = args
+        self.dist = dist
+        path = os.path.join(args.model_dir, f"{args.preset}-s{args.seed}.gguf")
+        if dist.local_rank == 0 and not os.path.exists(path):
+            os.makedirs(args.model_dir, exist_ok=True)
+            tmp = path + f".tmp{os.getpid()}"
+            t = time.perf_counter()
+            llmi.write_synthetic_gguf(tmp, args.preset, seed=args.seed)
+            os.replace(tmp, path)
+            log(f"wrote {path} in {time.perf_counter() - t:.1f}s")
+        dist.barrier()
+        self.path = path
+        t = time.perf_counter()
+        self.model = llmi.Model(path, main_gpu=dist.local_rank, no_upload=dist.rank != 0)
+        self.load_s = time.perf_counter() - t
+        self.fanout_s = 0.0
+        if dist.world > 1:
+            uid = dist.bcast_bytes(llmi.rccl_unique_id() if dist.rank == 0 else None)
+            t = time.perf_counter()
+            self.model.fanout(uid, dist.world, dist.rank)
+            self.fanout_s = time.perf_counter() - t
+        n_ctx = ((args.prompt + args.warmup + args.steps + args.profile_steps + 2 + 255) // 256) * 256
+        self.ctx = llmi.Context(self.model, n_ctx=n_ctx)
+        rng = np.random.default_rng(4 + dist.rank)
+        bos = self.model.bos if self.model.bos >= 0 else 1
+        self.prompt = [bos] + [int(t) for t in rng.integers(0, min(128000, self.model.n_vocab), args.prompt - 1)]
+        t = time.perf_counter()
+        assert self.ctx.decode(self.prompt) == 0
+        self.prefill_s = time.perf_counter() - t
+        self.next = self.ctx.greedy(-1)
+        self.pos = len(self.prompt)
+        self.generated: list[int] = []
+
+    def warmup(self, n):
+        if n > 0:
+            self.run(n)
+
+    def run(self, n):
+        toks = self.ctx.generate_greedy(self.next, self.pos, n)
+        self.generated += toks
+        self.pos += n
+        self.next = toks[-1]
+        self.bytes, self.us = self.ctx.stats()
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize()
+
+    def profile(self, n):
+        prof = self.ctx.profile_kernels(self.next, self.pos, n)
+        self.pos += n
+        return prof
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
+    """The oracle (CPU restatement of the reference's NGL=0 numerics, oracle/) timed on
+    this host: n_tokens greedy decode steps of the same GGUF after a 1-token prompt."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import pyoracle as po
+
+    threads = po.nthreads()
+    om = po.OracleModel(path, n_ctx=n_tokens + 2, threads=threads)
+    lg = om.decode(prompt[0], 0)  # page-in + first step, untimed
+    t = int(np.argmax(lg))
+    t0 = time.perf_counter()
+    for k in range(n_tokens):
+        lg = om.decode(t, k + 1)
+        t = int(np.argmax(lg))
+    dt = time.perf_counter() - t0
+    om.close()
+    return {"value": n_tokens / dt, "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{n_tokens} greedy decode steps (ctx 2..{n_tokens + 1}) of the same synthetic "
+                      f"{os.path.basename(path)}; oracle/ggml_oracle.c generic scalar C, OpenMP {threads} threads"}
+
+
+def main(argv=None):
+    args = parse(argv)
+    dist = Dist("nccl")
+    if dist.world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={dist.world}; using WORLD_SIZE")
+    n = dist.world
+    eng = LlmiEngine(args, dist)
+    log(f"rank {dist.rank}: {eng.model.desc} load {eng.load_s:.1f}s fanout {eng.fanout_s:.2f}s prefill "
+        f"{args.prompt} tok {eng.prefill_s:.2f}s")
+    dt, dt_max = timed_decode(eng, dist, args.steps, args.warmup)
+    tok_s = n * args.steps / dt_max
+    # end-to-end roofline: algorithmic bytes of the timed tokens / time (this rank)
+    e2e_gbps = eng.bytes / (eng.us * 1e-6) / 1e9 if eng.us > 0 else 0.0
+    prof = eng.profile(args.profile_steps) if args.profile_steps > 0 else {}
+    result = None
+    if dist.rank == 0:
+        k = prof.get(DOMINANT, {"us": 0.0, "bytes": 0.0})
+        achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9 if k["us"] > 0 else 0.0
+        traffic = None
+        if os.path.exists(args.traffic_file):
+            try:
+                traffic = json.load(open(args.traffic_file)).get(DOMINANT, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if n == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(eng.path, args.cpu_sample_tokens, eng.prompt)
+            except Exception as e:  # the baseline is reported, never required
+                log(f"cpu baseline failed: {e}")
+        result = {
+            "metric": "decode tokens/sec + achieved HBM GB/s, Llama-3-8B Q4_K_M, 1->8 MI355X",
+            "value": round(tok_s, 2),
+            "unit": "tokens/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic: random-init GGUF blocks with the exact Llama-3-8B Q4_K_M shapes/type table "
+                    "(llmi_synth.h); random 128-token prompts",
+            "config": {"workload": f"{args.preset}: {args.prompt}-token prompt -> greedy decode "
+                                   f"{args.warmup}+{args.steps} tokens, 1 replica per GPU",
+                       "model": args.preset, "prompt_tokens": args.prompt, "ctx_end": eng.pos,
+                       "parallelism": f"replicas x{n} (RCCL weight fan-out)", "global_batch": n},
+            "roofline": {"bound": "hbm", "kernel": "k_matvec<0,true,3> (ffn_gate+ffn_up Q4_K + SwiGLU)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "bytes_per_launch": k["bytes"], "us_per_launch": round(k["us"], 3)},
+            "hbm_end_to_end": {"achieved_GBps": round(e2e_gbps, 1),
+                               "frac_of_peak": round(e2e_gbps / HBM_PEAK_GBPS, 4),
+                               "bytes_per_token": eng.bytes / max(1, args.steps)},
+            "kernels": {k2: {"us": round(v["us"], 3), "GBps": round(v["GBps"], 1),
+                             "per_step": v["launches_per_step"]} for k2, v in prof.items()},
+            "load_s": round(eng.load_s, 2),
+            "fanout_s": round(eng.fanout_s, 3),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    dist.close()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -137,6 +137,14 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
 /* Roofline accounting of the last llama_decode / llmi_generate_greedy call:
  * algorithmic HBM bytes it streamed and its device time in microseconds. */
 void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec);
+/* Per-kernel-class device timing (roofline evidence): runs n_steps EAGER decode steps
+ * (greedy feedback) from (first, pos0) with a HIP event pair around every launch on the
+ * context's stream.  For class k in [0,7): us[k] = mean device microseconds per launch,
+ * bytes[k] = mean algorithmic HBM bytes per launch, launches[k] = launches per step.
+ * Classes: 0 embed, 1 qkv(+RoPE, KV write), 2 attention, 3 attn_output(+residual),
+ * 4 ffn_gate_up(+SwiGLU), 5 ffn_down(+residual), 6 output(+argmax).  0 on success. */
+int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps,
+                             double* us, double* bytes, int32_t* launches);
 /* Algorithmic bytes of one decode step at KV length n_kv (weights + one embedding row
  * + norms + KV read/write), the numerator of achieved GB/s. */
 double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv);
@@ -145,6 +153,14 @@ int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64
 /* In-process replica fan-out: copies model's arena to devices[0..n) with an RCCL
  * broadcast over xGMI and returns one model handle per device (out[i]). 0 on success. */
 int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_t n, struct llama_model** out);
+
+/* Multi-process replica fan-out (one process per GPU): rank 0 holds the
+ * uploaded weights, ranks 1..n-1 loaded the same GGUF with params.no_upload.  Every rank
+ * calls llmi_model_fanout with the same 128-byte RCCL unique id (made by rank 0 with
+ * llmi_rccl_unique_id and shared by any out-of-band channel); the arena is broadcast
+ * from rank 0 over xGMI with one ncclBroadcast.  Returns 0 on success. */
+int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n);
+int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank);
 
 /* Synthetic GGUF writer: preset = "llama3-8b-q4km", "tinyllama-q8_0",
  * "mistral7b-q6k", "mistral7b-q5km", "llama3-70b-q4km", or "tiny-mixed" (2 layers, E=256,

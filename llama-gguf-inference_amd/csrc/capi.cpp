@@ -343,6 +343,48 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
     API_CATCH(-5)
 }
 
+int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps, double* us,
+                             double* bytes, int32_t* launches) {
+    API_TRY
+    if (!ctx || n_steps <= 0 || !us || !bytes || !launches) { set_err("llmi_profile_kernels: bad arguments"); return -1; }
+    Context& c = ctx->c;
+    if (first < 0 || first >= c.m->hp.n_vocab || pos0 < 0 || pos0 + n_steps > c.n_ctx) {
+        set_err("llmi_profile_kernels: token/position out of range");
+        return -1;
+    }
+    (void)hipSetDevice(c.m->device);
+    Prof prof;
+    std::string err;
+    if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
+    c.prof = &prof;
+    bool ok = true;
+    for (int k = 0; k < n_steps && ok; ++k) {
+        const int pos = pos0 + k;
+        prof.n_kv = pos + 1;
+        ok = step_enqueue(c, std::min(c.n_ctx, (pos / 256 + 1) * 256), err);
+    }
+    c.prof = nullptr;
+    hipError_t e = hipStreamSynchronize(c.stream);
+    if (!ok || e != hipSuccess) { set_err("llmi_profile_kernels: " + (ok ? hip_err(e) : err)); return -3; }
+    double t[K_NCLASS] = {0}, b[K_NCLASS] = {0};
+    int n[K_NCLASS] = {0};
+    for (size_t i = 0; i < prof.used; ++i) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, prof.ev[2 * i], prof.ev[2 * i + 1]);
+        t[prof.cls[i]] += ms * 1e3;
+        b[prof.cls[i]] += prof.bytes[i];
+        n[prof.cls[i]] += 1;
+    }
+    for (int k = 0; k < K_NCLASS; ++k) {
+        us[k] = n[k] ? t[k] / n[k] : 0.0;
+        bytes[k] = n[k] ? b[k] / n[k] : 0.0;
+        launches[k] = n[k] / n_steps;
+    }
+    c.n_past = pos0 + n_steps;
+    return 0;
+    API_CATCH(-5)
+}
+
 void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec) {
     if (!ctx) return;
     if (bytes) *bytes = ctx->c.last_bytes;
@@ -403,6 +445,37 @@ int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_
         return -4;
     }
     for (int i = 0; i < n; ++i) out[i] = reps[(size_t)i];
+    return 0;
+    API_CATCH(-5)
+}
+
+int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n) {
+    if (!out || n < (int32_t)sizeof(ncclUniqueId)) { set_err("llmi_rccl_unique_id: buffer too small"); return -1; }
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) { set_err("ncclGetUniqueId failed"); return -2; }
+    std::memcpy(out, &id, sizeof id);
+    return 0;
+}
+
+int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank) {
+    API_TRY
+    if (!model || !uid || nranks <= 0 || rank < 0 || rank >= nranks || !model->m.arena) {
+        set_err("llmi_model_fanout: bad arguments");
+        return -1;
+    }
+    if (nranks == 1) return 0;
+    (void)hipSetDevice(model->m.device);
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof id);
+    ncclComm_t comm;
+    if (ncclCommInitRank(&comm, nranks, id, rank) != ncclSuccess) { set_err("ncclCommInitRank failed"); return -2; }
+    hipStream_t s;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    ncclResult_t r = ncclBroadcast(model->m.arena, model->m.arena, model->m.arena_bytes, ncclUint8, 0, comm, s);
+    hipError_t e = hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    ncclCommDestroy(comm);
+    if (r != ncclSuccess || e != hipSuccess) { set_err("llmi_model_fanout: broadcast failed"); return -3; }
     return 0;
     API_CATCH(-5)
 }

@@ -41,6 +41,20 @@ struct Model {
     ~Model();
 };
 
+// Per-launch device timing of one eager decode step (llmi_profile_kernels): an event
+// pair around every launch on the context stream, binned by kernel class.
+enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_NCLASS };
+struct Prof {
+    std::vector<hipEvent_t> ev;  // pool, 2 per launch
+    std::vector<int> cls;
+    std::vector<double> bytes;
+    size_t used = 0;
+    int n_kv = 0;                // KV length of the step being recorded
+    bool begin(hipStream_t s);
+    void end(hipStream_t s, int k, double b);
+    ~Prof();
+};
+
 struct Context {
     Model* m = nullptr;
     int n_ctx = 0;
@@ -62,6 +76,7 @@ struct Context {
     std::map<int, hipGraphExec_t> graphs;   // by KV bucket
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_bytes = 0, last_us = 0;
+    Prof* prof = nullptr;                   // non-null only inside llmi_profile_kernels
     ~Context();
 };
 

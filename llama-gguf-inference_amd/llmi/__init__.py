@@ -27,6 +27,13 @@ class LlmiError(RuntimeError):
     pass
 
 
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    if lib().llmi_rccl_unique_id(buf, 128) != 0:
+        raise LlmiError(last_error())
+    return buf.raw
+
+
 def device_count() -> int:
     return int(lib().llmi_device_count())
 
@@ -110,6 +117,11 @@ class Model:
             raise LlmiError(last_error())
         return [Model._from_handle(out[i], self.path, devices[i]) for i in range(n)]
 
+    def fanout(self, uid: bytes, nranks: int, rank: int) -> None:
+        """Multi-process replica fan-out: RCCL broadcast of rank 0's arena."""
+        if lib().llmi_model_fanout(self._h, uid, int(nranks), int(rank)) != 0:
+            raise LlmiError(last_error())
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().llama_model_free(self._h)
@@ -182,6 +194,17 @@ class Context:
         b, u = C.c_double(), C.c_double()
         lib().llmi_last_step_stats(self._h, C.byref(b), C.byref(u))
         return b.value, u.value
+
+    KERNEL_CLASSES = ("embed", "qkv", "attention", "attn_output", "ffn_gate_up", "ffn_down", "output")
+
+    def profile_kernels(self, first: int, pos0: int, n_steps: int) -> dict:
+        """Per-kernel-class mean device time / algorithmic bytes per launch (eager steps)."""
+        us, by, nl = (C.c_double * 7)(), (C.c_double * 7)(), (C.c_int32 * 7)()
+        if lib().llmi_profile_kernels(self._h, int(first), int(pos0), int(n_steps), us, by, nl) != 0:
+            raise LlmiError(last_error())
+        return {k: {"us": us[i], "bytes": by[i], "launches_per_step": nl[i],
+                    "GBps": (by[i] / (us[i] * 1e-6) / 1e9) if us[i] > 0 else 0.0}
+                for i, k in enumerate(self.KERNEL_CLASSES)}
 
     def kv_clear(self) -> None:
         lib().llama_kv_self_clear(self._h)

@@ -89,8 +89,12 @@ SIGNATURES = {
     "llmi_generate_greedy": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
     "llmi_last_step_stats": (None, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "llmi_bytes_per_token": (C.c_double, [_P, C.c_int32]),
+    "llmi_profile_kernels": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_double),
+                                         C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "llmi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "llmi_replicate": (C.c_int32, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_void_p)]),
+    "llmi_rccl_unique_id": (C.c_int32, [C.c_char_p, C.c_int32]),
+    "llmi_model_fanout": (C.c_int32, [_P, C.c_char_p, C.c_int32, C.c_int32]),
     "llmi_synth_write_gguf": (C.c_int64, [C.c_char_p, C.c_char_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32]),
     "llmi_device_layout_bytes": (C.c_int64, [C.c_int32, C.c_int64, C.c_int64]),
     "llmi_repack": (C.c_int32, [C.c_int32, _P, _P, C.c_int64, C.c_int64]),

@@ -43,6 +43,7 @@ def gpu():
     import torch
 
     assert torch.cuda.is_available(), "gpu-marked test needs a visible HIP device"
+    torch.zeros(1, device="cuda")  # initialise torch's HIP state before any libllmi call
     import llmi
 
     assert llmi.device_count() > 0

@@ -3,9 +3,9 @@
 - activation quantization (the matvec prologue, RMSNorm fused): BIT-EXACT vs
   quantize_row_q8_K_ref / quantize_row_q8_0_ref, incl. edge cases (all-zero block,
   +/- ties for the signed max, .5 rounding boundaries, tiny/huge magnitudes);
-- quantized matvec per type: integer block sums are exact, the fp32 combine order
-  differs from ggml's generic loop, so |y_gpu - y_oracle| <= 1e-5 * max|y| (written
-  tolerance; observed ~1e-7);
+- quantized matvec per type: BIT-EXACT against the oracle in device order (same
+  integer block math, the kernel's fp32 association), and within
+  |y_gpu - y_oracle| <= 1e-5 * max|y| of ggml's generic fp32 order (written tolerance);
 - the load-time repack is checked through the matvec and through get_rows elsewhere.
 """
 from __future__ import annotations
@@ -54,7 +54,8 @@ def edge_inputs(cols, rng):
     xs.append(("zero_block", z))
     t = rng.standard_normal(cols).astype(np.float32) * 0.5
     t[3], t[200] = -2.0, 2.0  # equal |max| with opposite signs: first one (negative) wins
-    t[256 + 7], t[256 + 9] = 3.0, -3.0
+    if cols >= 512:
+        t[256 + 7], t[256 + 9] = 3.0, -3.0
     xs.append(("ties", t))
     # values whose scaled image lands exactly on .5: -127/max * x = k + 0.5
     h = np.zeros(cols, dtype=np.float32)
@@ -116,11 +117,18 @@ def test_matvec_vs_oracle(gpu, qtype, rows, cols):
     rng = np.random.default_rng(rows * 131 + cols + qtype)
     raw = random_blocks(qtype, rows, cols, rng)
     x = rng.standard_normal(cols).astype(np.float32)
-    ref = po.matvec(qtype, raw, rows, cols, x)
     got = gpu_matvec(qtype, raw, rows, cols, x)
+    po.set_dot_order(po.GENERIC)
+    ref = po.matvec(qtype, raw, rows, cols, x)
     tol = 1e-5 * float(np.abs(ref).max())
     err = float(np.abs(got - ref).max())
-    assert err <= tol, f"max |err| {err:.3g} > {tol:.3g}"
+    assert err <= tol, f"max |err| vs generic order {err:.3g} > {tol:.3g}"
+    po.set_dot_order(po.DEVICE_ORDER)
+    try:
+        exact = po.matvec(qtype, raw, rows, cols, x)
+    finally:
+        po.set_dot_order(po.GENERIC)
+    assert np.array_equal(got, exact), "not bit-exact vs device-order oracle"
 
 
 @pytest.mark.parametrize("qtype", QTYPES, ids=[TNAME[t] for t in QTYPES])
