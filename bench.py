@@ -26,6 +26,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "llama-gguf-inference_amd"))
 
+import torch  # noqa: E402  (before libllmi: one HIP runtime per process, see llmi/_lib.py)
+
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak per GPU (MI355X_MICROARCH.md)
 DOMINANT = "ffn_gate_up"  # k_matvec<0,true,3>: fused ffn_gate+ffn_up Q4_K matvec + SwiGLU
 

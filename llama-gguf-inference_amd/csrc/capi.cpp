@@ -234,7 +234,7 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
         if (r >= 0) {
             (void)hipMemcpyAsync(ctx->outs + (size_t)r * hp.n_vocab * 4, c.logits, (size_t)hp.n_vocab * 4,
                                  hipMemcpyDeviceToDevice, c.stream);
-            (void)hipMemcpyAsync(ctx->keys_pinned + r, &c.st->argmax_key, 8, hipMemcpyDeviceToHost, c.stream);
+            (void)hipMemcpyAsync(ctx->keys_pinned + r, &c.st->key[pos & 1], 8, hipMemcpyDeviceToHost, c.stream);
         }
         last_pos = std::max(last_pos, pos);
     }
@@ -328,7 +328,7 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
     unsigned long long key = 0;
     if (n_gen > 1)
         (void)hipMemcpyAsync(h.data(), c.hist + pos0 + 1, (size_t)(n_gen - 1) * 4, hipMemcpyDeviceToHost, c.stream);
-    (void)hipMemcpyAsync(&key, &c.st->argmax_key, 8, hipMemcpyDeviceToHost, c.stream);
+    (void)hipMemcpyAsync(&key, &c.st->key[(pos0 + n_gen - 1) & 1], 8, hipMemcpyDeviceToHost, c.stream);
     hipError_t e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess) { set_err("llmi_generate_greedy: " + hip_err(e)); return -4; }
     for (int k = 0; k + 1 < n_gen; ++k) out[k] = h[(size_t)k];
@@ -353,28 +353,55 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
         return -1;
     }
     (void)hipSetDevice(c.m->device);
+    // The step is captured into a HIP graph WITH an event-record node pair around every
+    // kernel, then replayed step by step: kernels run exactly as in the timed graph
+    // replays (same grid, same back-to-back dependent launches), only the per-step host
+    // sync differs.
     Prof prof;
+    if (!prof.reserve((size_t)(8 + 8 * c.m->hp.n_layer))) { set_err("hipEventCreate failed"); return -3; }
     std::string err;
     if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
-    c.prof = &prof;
-    bool ok = true;
-    for (int k = 0; k < n_steps && ok; ++k) {
-        const int pos = pos0 + k;
-        prof.n_kv = pos + 1;
-        ok = step_enqueue(c, std::min(c.n_ctx, (pos / 256 + 1) * 256), err);
-    }
-    c.prof = nullptr;
-    hipError_t e = hipStreamSynchronize(c.stream);
-    if (!ok || e != hipSuccess) { set_err("llmi_profile_kernels: " + (ok ? hip_err(e) : err)); return -3; }
     double t[K_NCLASS] = {0}, b[K_NCLASS] = {0};
     int n[K_NCLASS] = {0};
-    for (size_t i = 0; i < prof.used; ++i) {
-        float ms = 0.f;
-        hipEventElapsedTime(&ms, prof.ev[2 * i], prof.ev[2 * i + 1]);
-        t[prof.cls[i]] += ms * 1e3;
-        b[prof.cls[i]] += prof.bytes[i];
-        n[prof.cls[i]] += 1;
+    hipGraphExec_t ex = nullptr;
+    int ex_bucket = -1;
+    for (int k = 0; k < n_steps; ++k) {
+        const int pos = pos0 + k, bucket = pos / 256;
+        if (bucket != ex_bucket) {
+            if (ex) (void)hipGraphExecDestroy(ex);
+            ex = nullptr;
+            prof.reset();
+            hipGraph_t g = nullptr;
+            if (hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                set_err("capture begin failed");
+                return -3;
+            }
+            c.prof = &prof;
+            const bool ok = step_enqueue(c, std::min(c.n_ctx, (bucket + 1) * 256), err);
+            c.prof = nullptr;
+            const hipError_t ec = hipStreamEndCapture(c.stream, &g);
+            if (!ok || ec != hipSuccess || hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                set_err("llmi_profile_kernels: capture failed " + err);
+                return -3;
+            }
+            (void)hipGraphDestroy(g);
+            ex_bucket = bucket;
+        }
+        if (hipGraphLaunch(ex, c.stream) != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess) {
+            (void)hipGraphExecDestroy(ex);
+            set_err("llmi_profile_kernels: replay failed");
+            return -4;
+        }
+        for (size_t i = 0; i < prof.used; ++i) {
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, prof.ev[2 * i], prof.ev[2 * i + 1]);
+            t[prof.cls[i]] += ms * 1e3;
+            b[prof.cls[i]] += prof.bytes[i] + prof.per_kv[i] * (pos + 1);
+            n[prof.cls[i]] += 1;
+        }
     }
+    if (ex) (void)hipGraphExecDestroy(ex);
     for (int k = 0; k < K_NCLASS; ++k) {
         us[k] = n[k] ? t[k] / n[k] : 0.0;
         bytes[k] = n[k] ? b[k] / n[k] : 0.0;

@@ -82,14 +82,21 @@ inline size_t plan_planes(DevMat& m, size_t base) {
     return m.off_a + m.bytes;
 }
 
-// On-device decode state (one per context).  The first kernel of a step selects the
-// token (host-fed, or the previous step's on-device argmax) and advances pos.
+// On-device decode state (one per context).  Step s at position p:
+//   k_embed (every workgroup): p = pos_next; token = (token_in_pos == p) ? token_in
+//           : argmax of key[(p-1)&1]; workgroup 0 publishes pos/token/hist[p] and
+//           clears key[p&1];
+//   logits kernel: atomicMax into key[p&1]; its workgroup 0 sets pos_next = p+1.
+// Every field is written by exactly one workgroup and never read by another workgroup
+// of the same launch, so no intra-kernel synchronisation is needed.
 struct StepState {
-    int32_t token_in;        // >= 0: host-provided token; -1: take argmax of previous step
+    int32_t token_in;        // host-provided token ...
+    int32_t token_in_pos;    // ... valid for the step at this position (else greedy feedback)
     int32_t pos_next;        // position of the next step
-    int32_t pos;             // position of the current step (written by the embed kernel)
+    int32_t pos;             // position of the current step (written by k_embed)
     int32_t token;           // token of the current step
-    unsigned long long argmax_key;  // (ordered logit << 32) | (0xffffffff - row)
+    int32_t pad;
+    unsigned long long key[2];  // per-parity argmax key: (ordered logit << 32) | (0xffffffff - row)
 };
 
 }  // namespace llmi

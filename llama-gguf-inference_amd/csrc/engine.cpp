@@ -295,24 +295,29 @@ void context_clear(Context& c) {
     (void)hipMemsetAsync(c.kc, 0, kv_elems * 2, c.stream);
     (void)hipMemsetAsync(c.vc, 0, kv_elems * 2, c.stream);
     (void)hipMemsetAsync(c.hist, 0, (size_t)c.n_ctx * 4, c.stream);
-    StepState s0{-1, 0, 0, 0, 0ull};
+    StepState s0{-1, -1, 0, 0, 0, 0, {0ull, 0ull}};
     (void)hipMemcpyAsync(c.st, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
     (void)hipStreamSynchronize(c.stream);
     c.n_past = 0;
 }
 
-bool Prof::begin(hipStream_t s) {
-    while (ev.size() < 2 * (used + 1)) {
+bool Prof::reserve(size_t launches) {
+    while (ev.size() < 2 * launches) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return false;
         ev.push_back(e);
     }
+    return true;
+}
+bool Prof::begin(hipStream_t s) {
+    if (!reserve(used + 1)) return false;
     return hipEventRecord(ev[2 * used], s) == hipSuccess;
 }
-void Prof::end(hipStream_t s, int k, double b) {
+void Prof::end(hipStream_t s, int k, double b, double b_per_kv) {
     (void)hipEventRecord(ev[2 * used + 1], s);
     cls.push_back(k);
     bytes.push_back(b);
+    per_kv.push_back(b_per_kv);
     ++used;
 }
 Prof::~Prof() {
@@ -380,7 +385,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
         if (P) P->begin(c.stream);
         HIPC(launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
-        if (P) P->end(c.stream, K_ATTN, 2.0 * kvpos * (P->n_kv) + 8.0 * nq);
+        if (P) P->end(c.stream, K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---
         MVArgs o;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
@@ -405,7 +410,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     MVArgs lo;
     lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
     lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
-    lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = &c.st->argmax_key;
+    lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = c.st->key; lo.st = c.st;
     if (P) P->begin(c.stream);
     HIPC(launch_matvec(lo, EPI_LOGITS, c.max_blocks, c.stream));
     if (P) P->end(c.stream, K_OUTPUT, (double)m.output.bytes + 8.0 * E + 4.0 * hp.n_vocab);

@@ -45,13 +45,15 @@ struct Model {
 // pair around every launch on the context stream, binned by kernel class.
 enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_NCLASS };
 struct Prof {
-    std::vector<hipEvent_t> ev;  // pool, 2 per launch
+    std::vector<hipEvent_t> ev;  // pool, 2 per launch (pre-created: recorded inside a graph capture)
     std::vector<int> cls;
-    std::vector<double> bytes;
+    std::vector<double> bytes;   // fixed algorithmic bytes of the launch
+    std::vector<double> per_kv;  // + per_kv * n_kv (attention: K and V rows read)
     size_t used = 0;
-    int n_kv = 0;                // KV length of the step being recorded
+    bool reserve(size_t launches);
     bool begin(hipStream_t s);
-    void end(hipStream_t s, int k, double b);
+    void end(hipStream_t s, int k, double b, double b_per_kv = 0.0);
+    void reset() { used = 0; cls.clear(); bytes.clear(); per_kv.clear(); }
     ~Prof();
 };
 

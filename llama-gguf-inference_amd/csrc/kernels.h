@@ -9,7 +9,8 @@
 
 namespace llmi {
 
-constexpr int kMVThreads = 256;  // 4 waves of 64; each wave owns one row pair at a time
+constexpr int kMVThreads = 256;        // 4 waves of 64; each wave owns one row pair at a time
+constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
 
 enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
 
@@ -36,7 +37,7 @@ struct MVArgs {
     uint16_t* kc = nullptr;      // layer K cache [HK][n_ctx][D]
     uint16_t* vc = nullptr;      // layer V cache, transposed [HK][D][n_ctx]
     const float* rope = nullptr; // [n_ctx][n_rot/2][cos,sin]
-    const StepState* st = nullptr;
+    StepState* st = nullptr;     // QKV reads pos; LOGITS reads pos and advances pos_next
     int head_dim = 0, n_rot = 0, n_ctx = 0, nq = 0, nk = 0;
     unsigned long long* argmax = nullptr;  // LOGITS
 };

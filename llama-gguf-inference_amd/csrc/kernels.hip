@@ -336,33 +336,13 @@ __device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, const Lds
     }
 }
 
-// Both rows of a pair share the activation chunk reads.
-template <int T>
-__device__ __forceinline__ void pair_rows(const Seg& sa, int ra, const Seg& sb, int rb, bool vb, int cols,
-                                          const Lds& L, float& acc_a, float& acc_b) {
-    const int cpr = cols >> 6;
-    const int nb = (T == T_Q8_0) ? (cols >> 5) : (cols >> 8);
-    const int lane = threadIdx.x & 63;
-    for (int ci = lane; ci < cpr; ci += 64) {
-        const Raw wa = load_chunk<T>(sa, ra, ci, nb);
-        Raw wb;
-        if (vb) wb = load_chunk<T>(sb, rb, ci, nb);
-        const Act act = load_act(L, ci);
-        acc_a += dot_chunk<T>(wa, act, L, ci);
-        if (vb) acc_b += dot_chunk<T>(wb, act, L, ci);
-    }
-}
-
-__device__ __forceinline__ void row_any(int type, const Seg& s, int r, int cols, const Lds& L, float& acc) {
-    float dummy = 0.f;
-    switch (type) {
-        case T_Q4_K: pair_rows<T_Q4_K>(s, r, s, r, false, cols, L, acc, dummy); break;
-        case T_Q5_K: pair_rows<T_Q5_K>(s, r, s, r, false, cols, L, acc, dummy); break;
-        case T_Q6_K: pair_rows<T_Q6_K>(s, r, s, r, false, cols, L, acc, dummy); break;
-        default: break;
-    }
-}
-
+// ----------------------------------------------------------------------------------
+// Row-pair work items.  A wave streams its pairs p = w0, w0+G, ... (G = 4*gridDim.x);
+// each pair is NJ = ceil(cols/4096) items (lane chunk ci = lane + 64*j).  Items of the
+// kernel's primary weight type T are software-pipelined: the next item's weights are
+// in flight while the current one is reduced, and the wave's first item is issued
+// BEFORE the activation prologue so HBM latency overlaps it.
+// ----------------------------------------------------------------------------------
 __device__ __forceinline__ Seg pick(const MVArgs& A, int si) {
     Seg s;
     s.a = si == 0 ? A.seg[0].a : si == 1 ? A.seg[1].a : A.seg[2].a;
@@ -374,6 +354,65 @@ __device__ __forceinline__ Seg pick(const MVArgs& A, int si) {
     return s;
 }
 
+struct PairRef {
+    Seg sa, sb;
+    int ra, rb;
+    bool vb;
+    int type;  // common type of both rows, or -1 if they differ
+};
+
+template <int EPI>
+__device__ __forceinline__ PairRef pair_ref(const MVArgs& A, int p) {
+    PairRef r;
+    if constexpr (EPI == EPI_SWIGLU) {
+        r.sa = pick(A, 0);
+        r.sb = pick(A, 1);
+        r.ra = r.rb = p;
+        r.vb = true;
+    } else {
+        const int g = A.seg[0].row0 + 2 * p;
+        int si = 0;
+        if (A.nseg > 1 && g >= A.seg[1].row0) si = 1;
+        if (A.nseg > 2 && g >= A.seg[2].row0) si = 2;
+        r.sa = pick(A, si);
+        r.sb = r.sa;
+        r.ra = g - r.sa.row0;
+        r.rb = r.ra + 1;
+        r.vb = r.rb < r.sa.rows;
+    }
+    r.type = r.sa.type == r.sb.type ? r.sa.type : -1;
+    return r;
+}
+
+template <int T>
+struct PairRaw {
+    Raw a, b;
+};
+
+template <int T>
+__device__ __forceinline__ PairRaw<T> load_item(const PairRef& r, int ci, int cpr, int nb) {
+    PairRaw<T> w;
+    if (ci < cpr) {
+        w.a = load_chunk<T>(r.sa, r.ra, ci, nb);
+        if (r.vb) w.b = load_chunk<T>(r.sb, r.rb, ci, nb);
+    }
+    return w;
+}
+
+// Two-row 64-lane butterfly in 6 shuffles: step 1 exchanges across the halves (lane
+// L<32 keeps row a, L>=32 row b), steps 2-6 reduce each half.  Per row this is exactly
+// the xor-butterfly tree (pairs (L, L^32), then ^16 ... ^1), so the oracle's device
+// order models it; row a lands in lane 0, row b in lane 32.
+__device__ __forceinline__ float reduce_pair(float acc_a, float acc_b) {
+    const int lane = threadIdx.x & 63;
+    const float send = lane < 32 ? acc_b : acc_a;
+    const float recv = __shfl_xor(send, 32);
+    float v = (lane < 32 ? acc_a : acc_b) + recv;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
 // ordered key of (logit, row): larger logit wins, ties -> smaller row (first max wins,
 // as upstream llama_sampler_greedy's strict '>' scan)
 __device__ __forceinline__ unsigned long long argmax_key(float v, int row) {
@@ -383,93 +422,153 @@ __device__ __forceinline__ unsigned long long argmax_key(float v, int row) {
     return ((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
 }
 
-template <int ACT, bool NORM, int EPI>
+// Epilogue of one finished pair; `v` holds row a in lane 0 and row b in lane 32.
+template <int EPI>
+__device__ __forceinline__ void epilogue(const MVArgs& A, const PairRef& r, int p, float v, int pos,
+                                         unsigned long long& best) {
+    const int lane = threadIdx.x & 63;
+    const float va = __shfl(v, 0), vb = __shfl(v, 32);
+    if (lane != 0) return;
+    if constexpr (EPI == EPI_STORE) {
+        A.y[r.sa.row0 + r.ra] = va;
+        if (r.vb) A.y[r.sa.row0 + r.rb] = vb;
+    } else if constexpr (EPI == EPI_ADD) {
+        A.y[r.sa.row0 + r.ra] += va;
+        if (r.vb) A.y[r.sa.row0 + r.rb] += vb;
+    } else if constexpr (EPI == EPI_LOGITS) {
+        A.y[r.ra] = va;
+        unsigned long long k = argmax_key(va, r.ra);
+        best = k > best ? k : best;
+        if (r.vb) {
+            A.y[r.rb] = vb;
+            k = argmax_key(vb, r.rb);
+            best = k > best ? k : best;
+        }
+    } else if constexpr (EPI == EPI_SWIGLU) {
+        A.y[p] = llmi_silu(va) * vb;
+    } else if constexpr (EPI == EPI_QKV) {
+        // sa.row0 tells q (0), k (nq) or v (nq+nk); rows (ra, ra+1) are a RoPE pair
+        const int hd = A.head_dim;
+        const int h = r.ra / hd, d = r.ra - h * hd;
+        if (r.sa.row0 < A.nq + A.nk) {
+            float o0 = va, o1 = vb;
+            if (d < A.n_rot) {  // ggml rope NORM mode on the adjacent pair (d, d+1)
+                const float2 cs = *(const float2*)(A.rope + ((size_t)pos * (A.n_rot / 2) + d / 2) * 2);
+                o0 = va * cs.x - vb * cs.y;
+                o1 = va * cs.y + vb * cs.x;
+            }
+            if (r.sa.row0 == 0) {
+                A.y[r.ra] = o0;
+                A.y[r.ra + 1] = o1;
+            } else {
+                const uint32_t w = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
+                *(uint32_t*)(A.kc + ((size_t)h * A.n_ctx + pos) * hd + d) = w;
+            }
+        } else {
+            A.vc[((size_t)h * hd + d) * A.n_ctx + pos] = f2h(va);
+            A.vc[((size_t)h * hd + d + 1) * A.n_ctx + pos] = f2h(vb);
+        }
+    }
+}
+
+// Non-pipelined fallback for pairs whose type is not the kernel's primary type (the
+// Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs).
+template <int T>
+__device__ __forceinline__ float generic_row(const Seg& s, int row, int cols, const Lds& L) {
+    const int cpr = cols >> 6, nb = (T == T_Q8_0) ? (cols >> 5) : (cols >> 8);
+    float acc = 0.f;
+    for (int ci = threadIdx.x & 63; ci < cpr; ci += 64) {
+        const Raw w = load_chunk<T>(s, row, ci, nb);
+        acc += dot_chunk<T>(w, load_act(L, ci), L, ci);
+    }
+    return acc;
+}
+template <int ACT>
+__device__ __forceinline__ float generic_row_any(int type, const Seg& s, int row, int cols, const Lds& L) {
+    if constexpr (ACT == 1) {
+        return generic_row<T_Q8_0>(s, row, cols, L);
+    } else {
+        switch (type) {
+            case T_Q4_K: return generic_row<T_Q4_K>(s, row, cols, L);
+            case T_Q5_K: return generic_row<T_Q5_K>(s, row, cols, L);
+            case T_Q6_K: return generic_row<T_Q6_K>(s, row, cols, L);
+            default: return 0.f;
+        }
+    }
+}
+
+template <int ACT, bool NORM, int EPI, int T>
 __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Lds L = carve(smem, ACT, A.cols);
-    mv_prologue<ACT, NORM>(A, L);
-    __syncthreads();
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
+    const int G = gridDim.x * 4;
+    const int cpr = A.cols >> 6, NJ = (cpr + 63) >> 6;
+    const int nb = (T == T_Q8_0) ? (A.cols >> 5) : (A.cols >> 8);
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
-    for (int p = blockIdx.x * 4 + wave; p < A.npairs; p += gridDim.x * 4) {
-        Seg sa, sb;
-        int ra, rb;
-        bool vb;
-        if constexpr (EPI == EPI_SWIGLU) {
-            sa = pick(A, 0); sb = pick(A, 1);
-            ra = rb = p; vb = true;
-        } else {
-            const int g = A.seg[0].row0 + 2 * p;
-            int si = 0;
-            if (A.nseg > 1 && g >= A.seg[1].row0) si = 1;
-            if (A.nseg > 2 && g >= A.seg[2].row0) si = 2;
-            sa = pick(A, si); sb = sa;
-            ra = g - sa.row0; rb = ra + 1; vb = rb < sa.rows;
-        }
+
+    int p = blockIdx.x * 4 + wave;
+    PairRef r;
+    bool pipe = false;
+    PairRaw<T> cur;
+    if (p < A.npairs) {
+        r = pair_ref<EPI>(A, p);
+        pipe = r.type == T;
+        if (pipe) cur = load_item<T>(r, lane, cpr, nb);  // issued before the prologue
+    }
+    mv_prologue<ACT, NORM>(A, L);
+    __syncthreads();
+
+    if (pipe) {
+        int j = 0;
         float acc_a = 0.f, acc_b = 0.f;
-        if constexpr (ACT == 1) {
-            pair_rows<T_Q8_0>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b);
-        } else if (sa.type == sb.type) {
-            switch (sa.type) {
-                case T_Q4_K: pair_rows<T_Q4_K>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b); break;
-                case T_Q5_K: pair_rows<T_Q5_K>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b); break;
-                case T_Q6_K: pair_rows<T_Q6_K>(sa, ra, sb, rb, vb, A.cols, L, acc_a, acc_b); break;
-                default: break;
+        for (;;) {
+            // next work item: (p, j+1) or (p+G, 0)
+            int pn = p, jn = j + 1;
+            PairRef rn = r;
+            if (jn == NJ) {
+                jn = 0;
+                pn = p + G;
+                if (pn < A.npairs) rn = pair_ref<EPI>(A, pn);
             }
-        } else {  // gate/up of different K-quant types
-            row_any(sa.type, sa, ra, A.cols, L, acc_a);
-            if (vb) row_any(sb.type, sb, rb, A.cols, L, acc_b);
-        }
-        acc_a = wave_sum(acc_a);
-        acc_b = wave_sum(acc_b);
-        if (lane == 0) {
-            if constexpr (EPI == EPI_STORE) {
-                A.y[sa.row0 + ra] = acc_a;
-                if (vb) A.y[sa.row0 + rb] = acc_b;
-            } else if constexpr (EPI == EPI_ADD) {
-                A.y[sa.row0 + ra] += acc_a;
-                if (vb) A.y[sa.row0 + rb] += acc_b;
-            } else if constexpr (EPI == EPI_LOGITS) {
-                A.y[ra] = acc_a;
-                unsigned long long k = argmax_key(acc_a, ra);
-                best = k > best ? k : best;
-                if (vb) {
-                    A.y[rb] = acc_b;
-                    k = argmax_key(acc_b, rb);
-                    best = k > best ? k : best;
-                }
-            } else if constexpr (EPI == EPI_SWIGLU) {
-                A.y[p] = llmi_silu(acc_a) * acc_b;
-            } else if constexpr (EPI == EPI_QKV) {
-                // sa.row0 tells q (0), k (nq) or v (nq+nk)
-                const int hd = A.head_dim;
-                const int h = ra / hd, d = ra - h * hd;
-                if (sa.row0 < A.nq + A.nk) {
-                    float o0 = acc_a, o1 = acc_b;
-                    if (d < A.n_rot) {  // ggml rope NORM mode on the adjacent pair (d, d+1)
-                        const float2 cs = *(const float2*)(A.rope + ((size_t)pos * (A.n_rot / 2) + d / 2) * 2);
-                        o0 = acc_a * cs.x - acc_b * cs.y;
-                        o1 = acc_a * cs.y + acc_b * cs.x;
-                    }
-                    if (sa.row0 == 0) {
-                        A.y[ra] = o0;
-                        A.y[ra + 1] = o1;
-                    } else {
-                        const uint32_t w = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
-                        *(uint32_t*)(A.kc + ((size_t)h * A.n_ctx + pos) * hd + d) = w;
-                    }
-                } else {
-                    A.vc[((size_t)h * hd + d) * A.n_ctx + pos] = f2h(acc_a);
-                    A.vc[((size_t)h * hd + d + 1) * A.n_ctx + pos] = f2h(acc_b);
-                }
+            const bool has_next = pn < A.npairs && rn.type == T;
+            PairRaw<T> nxt;
+            if (has_next) nxt = load_item<T>(rn, lane + 64 * jn, cpr, nb);
+            const int ci = lane + 64 * j;
+            if (ci < cpr) {
+                const Act act = load_act(L, ci);
+                acc_a += dot_chunk<T>(cur.a, act, L, ci);
+                if (r.vb) acc_b += dot_chunk<T>(cur.b, act, L, ci);
             }
+            if (j == NJ - 1) {
+                epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
+                acc_a = acc_b = 0.f;
+            }
+            if (!has_next) {
+                p = pn;
+                if (jn == 0 && pn < A.npairs) r = rn;
+                break;
+            }
+            cur = nxt;
+            p = pn;
+            j = jn;
+            r = rn;
         }
     }
+    // remaining pairs of other types (or all pairs if the first was not of type T)
+    for (; p < A.npairs; p += G) {
+        r = pair_ref<EPI>(A, p);
+        const float acc_a = generic_row_any<ACT>(r.sa.type, r.sa, r.ra, A.cols, L);
+        const float acc_b = r.vb ? generic_row_any<ACT>(r.sb.type, r.sb, r.rb, A.cols, L) : 0.f;
+        epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
+    }
     if constexpr (EPI == EPI_LOGITS) {
-        if (lane == 0 && best) atomicMax(A.argmax, best);
+        const int cur = A.st->pos;
+        if (lane == 0 && best) atomicMax(&A.argmax[cur & 1], best);
+        if (blockIdx.x == 0 && threadIdx.x == 0) A.st->pos_next = cur + 1;
     }
 }
 
@@ -608,6 +707,78 @@ __global__ __launch_bounds__(256) void k_attn_pv(AttnArgs a) {
         }
 }
 
+// Fused single-launch attention for KV lengths that fit in LDS (kv_bound <= 8192):
+// one 1024-thread workgroup per query head; scores, softmax statistics and the
+// f16-rounded probabilities stay in LDS, so the only global traffic is one K and one V
+// read per head (the G heads of a KV group are dealt to one XCD: blockIdx % HK = group,
+// so 3 of 4 K/V reads hit that XCD's L2).  Same numerics as the two-kernel path above.
+template <int D>
+__global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) {
+    extern __shared__ __attribute__((aligned(16))) float sp_lds[];
+    __shared__ float qs[D];
+    __shared__ double redd[16];
+    __shared__ float redf[16];
+    const int b = blockIdx.x;
+    const int g = b % HK, h = g * G + b / HK;
+    const int n_kv = a.st->pos + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < D) qs[tid] = h2f(f2h(a.q[(size_t)h * D + tid]));
+    __syncthreads();
+    // scores: one position per thread, K row read straight from HBM/L2 (16 x 16 B)
+    const uint16_t* kb = a.kc + (size_t)g * a.n_ctx * D;
+    float mx = -INFINITY;
+    for (int t = tid; t < n_kv; t += 1024) {
+        const uint16_t* kr = kb + (size_t)t * D;
+        double acc = 0.0;
+#pragma unroll 4
+        for (int d = 0; d < D; d += 8) {
+            const u32x4 kv = *(const u32x4*)(kr + d);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc += (double)(h2f(kv[j]) * qs[d + 2 * j]);
+                acc += (double)(h2f(kv[j] >> 16) * qs[d + 2 * j + 1]);
+            }
+        }
+        const float w = (float)acc * a.scale;
+        sp_lds[t] = w;
+        mx = fmaxf(mx, w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    mx = redf[0];
+#pragma unroll
+    for (int w = 1; w < 16; ++w) mx = fmaxf(mx, redf[w]);
+    double s = 0.0;
+    for (int t = tid; t < n_kv; t += 1024) s += (double)llmi_expf(sp_lds[t] - mx);
+    s = wave_sum_d(s);
+    if (lane == 0) redd[wave] = s;
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) tot += redd[w];
+    const float inv = (float)(1.0 / tot);
+    for (int t = tid; t < n_kv; t += 1024) sp_lds[t] = h2f(f2h(llmi_expf(sp_lds[t] - mx) * inv));
+    __syncthreads();
+    // PV over the transposed V cache: SL threads per output dim, 8 positions (16 B) each
+    constexpr int SL = 1024 / D;
+    const int d = tid / SL, sl = tid % SL;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    double acc = 0.0;
+    for (int t0 = 8 * sl; t0 < n_kv; t0 += 8 * SL) {
+        const u32x4 vv = *(const u32x4*)(vr + t0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (t0 + 2 * j < n_kv) acc += (double)(h2f(vv[j]) * sp_lds[t0 + 2 * j]);
+            if (t0 + 2 * j + 1 < n_kv) acc += (double)(h2f(vv[j] >> 16) * sp_lds[t0 + 2 * j + 1]);
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < SL; o <<= 1) acc += __shfl_xor(acc, o);
+    if (sl == 0) a.out[(size_t)h * D + d] = (float)acc;
+}
+
 // ----------------------------------------------------------------------------------
 // Step entry: choose the token, advance pos, dequantize its embedding row
 // (upstream ggml_get_rows + dequantize_row_*; bit-exact).
@@ -651,28 +822,24 @@ __device__ float dequant_elem(const Seg& w, int row, int e, int cols) {
 }
 
 __global__ __launch_bounds__(256) void k_embed(EmbArgs a) {
-    __shared__ int s_tok;
-    if (threadIdx.x == 0) {
-        StepState* st = a.st;
-        int tok = st->token_in;
-        if (tok < 0) tok = (int)(0xffffffffu - (uint32_t)(st->argmax_key & 0xffffffffull));
-        if (tok < 0 || tok >= a.vocab) tok = 0;
-        const int pos = st->pos_next;
-        st->pos = pos;
-        st->pos_next = pos + 1;
-        st->token = tok;
-        st->token_in = -1;
-        st->argmax_key = 0;
+    const StepState* st = a.st;
+    const int pos = st->pos_next;
+    int tok = st->token_in_pos == pos ? st->token_in
+                                      : (int)(0xffffffffu - (uint32_t)(st->key[(pos + 1) & 1] & 0xffffffffull));
+    if (tok < 0 || tok >= a.vocab) tok = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.st->pos = pos;
+        a.st->token = tok;
+        a.st->key[pos & 1] = 0;
         if (pos >= 0 && pos < a.n_ctx) a.hist[pos] = tok;
-        s_tok = tok;
     }
-    __syncthreads();
-    const int tok = s_tok;
-    for (int e = threadIdx.x; e < a.cols; e += 256) a.x[e] = dequant_elem(a.w, tok, e, a.cols);
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e < a.cols) a.x[e] = dequant_elem(a.w, tok, e, a.cols);
 }
 
 __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
     st->token_in = token_in;
+    st->token_in_pos = pos_next;
     st->pos_next = pos_next;
 }
 
@@ -717,17 +884,36 @@ __global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_
 // ----------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------
-template <int ACT, bool NORM>
+template <int ACT, bool NORM, int T>
 static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
     switch (epi) {
-        case EPI_STORE: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_STORE>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_ADD: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_ADD>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_QKV: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_QKV>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_SWIGLU: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_SWIGLU>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_LOGITS: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_LOGITS>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_STORE: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_STORE, T>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_ADD: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_ADD, T>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_QKV: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_QKV, T>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_SWIGLU: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_SWIGLU, T>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_LOGITS: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_LOGITS, T>), grid, dim3(kMVThreads), lds, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+template <bool NORM>
+static hipError_t mv_dispatch_type(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
+    // primary (pipelined) type = the type owning the most rows of the launch
+    int best = a.seg[0].type, best_rows = 0;
+    for (int i = 0; i < a.nseg; ++i) {
+        int rows = 0;
+        for (int k = 0; k < a.nseg; ++k)
+            if (a.seg[k].type == a.seg[i].type) rows += a.seg[k].rows;
+        if (rows > best_rows) { best_rows = rows; best = a.seg[i].type; }
+    }
+    switch (best) {
+        case T_Q4_K: return mv_dispatch_epi<0, NORM, T_Q4_K>(a, epi, grid, lds, s);
+        case T_Q5_K: return mv_dispatch_epi<0, NORM, T_Q5_K>(a, epi, grid, lds, s);
+        case T_Q6_K: return mv_dispatch_epi<0, NORM, T_Q6_K>(a, epi, grid, lds, s);
+        case T_Q8_0: return mv_dispatch_epi<1, NORM, T_Q8_0>(a, epi, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s) {
@@ -739,9 +925,7 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
     int blocks = (a.npairs + 3) / 4;
     if (blocks > max_blocks) blocks = max_blocks;
     const dim3 grid(blocks);
-    const bool norm = a.nw != nullptr;
-    if (act == 0) return norm ? mv_dispatch_epi<0, true>(a, epi, grid, lds, s) : mv_dispatch_epi<0, false>(a, epi, grid, lds, s);
-    return norm ? mv_dispatch_epi<1, true>(a, epi, grid, lds, s) : mv_dispatch_epi<1, false>(a, epi, grid, lds, s);
+    return a.nw ? mv_dispatch_type<true>(a, epi, grid, lds, s) : mv_dispatch_type<false>(a, epi, grid, lds, s);
 }
 
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t s) {
@@ -771,13 +955,20 @@ static hipError_t attn_dispatch_g(const AttnArgs& a, int g, int hk, int kv_bound
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     const int g = n_head / n_head_kv;
+    if (kv_bound <= kFusedAttnMaxKV) {
+        const size_t lds = (size_t)kv_bound * 4;
+        if (head_dim == 128) hipLaunchKernelGGL((k_attn_fused<128>), dim3(n_head), dim3(1024), lds, s, a, g, n_head_kv);
+        else if (head_dim == 64) hipLaunchKernelGGL((k_attn_fused<64>), dim3(n_head), dim3(1024), lds, s, a, g, n_head_kv);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (head_dim == 128) return attn_dispatch_g<128>(a, g, n_head_kv, kv_bound, s);
     if (head_dim == 64) return attn_dispatch_g<64>(a, g, n_head_kv, kv_bound, s);
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_embed(const EmbArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_embed, dim3(1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_embed, dim3((a.cols + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

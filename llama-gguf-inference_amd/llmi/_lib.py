@@ -111,6 +111,14 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (same soname
+    # libamdhip64.so.7).  If torch is installed, load it first so libllmi binds to the
+    # already-loaded runtime instead of pulling in a second copy (two runtimes in one
+    # process make torch's device init fail: "No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise LlmiLibraryError(
             f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
