@@ -188,6 +188,10 @@ int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x_dev, const 
 double llmi_bench_matvec(int32_t type, const void* w_dev, int32_t n_mats, int64_t rows, int64_t cols,
                          const float* x_dev, float* y_dev, int32_t reps);
 
+/* streaming-read reference: average microseconds to read `bytes` from each of n_bufs
+ * distinct buffers (stride `stride` bytes) with coalesced 16-B/lane loads */
+double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint64_t bytes, int32_t reps, int32_t blocks);
+
 #pragma GCC visibility pop
 
 #ifdef __cplusplus

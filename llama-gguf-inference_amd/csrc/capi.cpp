@@ -552,6 +552,7 @@ static Seg seg_at(int32_t type, const void* w, int64_t rows, int64_t cols) {
     plan_planes(dm, 0);
     Seg s;
     s.a = (const uint8_t*)w + dm.off_a;
+    s.h = (const uint8_t*)w + dm.off_h;
     s.s = (const uint8_t*)w + dm.off_s;
     s.d = (const uint8_t*)w + dm.off_d;
     s.type = type;
@@ -573,9 +574,9 @@ int32_t llmi_repack(int32_t type, const void* raw, void* w, int64_t rows, int64_
     dm.type = type; dm.rows = rows; dm.cols = cols;
     plan_planes(dm, 0);
     hipError_t e;
-    if (type == T_Q6_K || type == T_Q8_0) {
-        e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_s, (uint8_t*)w + dm.off_d,
-                          rows * (cols / block_elems(type)), nullptr);
+    if (needs_repack(type)) {
+        e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_h, (uint8_t*)w + dm.off_s,
+                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), nullptr);
     } else {
         e = hipMemcpy(w, raw, dm.bytes, hipMemcpyDeviceToDevice);
     }
@@ -646,6 +647,25 @@ double llmi_bench_matvec(int32_t type, const void* w, int32_t n_mats, int64_t ro
     hipEventElapsedTime(&ms, e0, e1);
     hipEventDestroy(e0);
     hipEventDestroy(e1);
+    return (double)ms * 1e3 / reps;
+}
+
+double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint64_t bytes, int32_t reps, int32_t blocks) {
+    unsigned* out = nullptr;
+    if (hipMalloc(&out, 16) != hipSuccess) return -1.0;
+    for (int k = 0; k < n_bufs; ++k) (void)launch_stream_read((const uint8_t*)dev + stride * k, bytes, out, blocks, nullptr);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, nullptr);
+    for (int r = 0; r < reps; ++r) (void)launch_stream_read((const uint8_t*)dev + stride * (r % n_bufs), bytes, out, blocks, nullptr);
+    hipEventRecord(e1, nullptr);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    (void)hipFree(out);
     return (double)ms * 1e3 / reps;
 }
 

@@ -1,16 +1,17 @@
 // common.h — shared host/device definitions of the llmi decode path.
 //
 // Device weight layouts (DESIGN.md §Data layout in HBM).  Every quantized matrix is
-// stored row-major by 256- (K-quants) or 32- (Q8_0) element blocks; the algorithmic
-// byte count of every layout equals the GGUF byte count exactly:
-//   Q4_K  native 144-B blocks (16-B aligned: 144 = 9*16)             [planes: A]
-//   Q5_K  native 176-B blocks (176 = 11*16)                            [A]
-//   Q6_K  "Q6R": the 210-B block is not 16-B aligned, so it is repacked at load into
-//         A = 192 B/block: 4 chunks x {32 B low nibbles, 16 B 2-bit highs} in the
-//             64-weight chunk order every K-quant kernel lane uses,
-//         S = 16 B/block int8 scales, D = 2 B/block fp16 d              [A, S, D]
-//   Q8_0  "Q80R": Q = 32 B/block int8, D = 2 B/block fp16 d               [A, D]
-//   F32/F16 plain.
+// repacked once at load into "piece-planar" form: a PIECE is 32 weights of one block
+// (K-quants: 16 weights of scale group 2c and the 16 weights 32 positions later, i.e.
+// the low and high nibbles of 16 consecutive native qs bytes; Q8_0: 16 weights), and
+// each plane stores one field of all pieces of a row contiguously, so a wave64 load of
+// 16 B/lane reads 1 KiB of consecutive bytes.  Byte counts equal GGUF exactly.
+//   Q4_K  A: qs 128 B/block (= native qs)            S: header {d, dmin, scales[12]} 16 B/block
+//   Q5_K  A: qs 128 B/block   H: 4 B/piece (32 fifth bits)   S: header 16 B/block
+//   Q6_K  A: ql 128 B/block (piece order)  H: 8 B/piece (2-bit highs, shift-decodable)
+//         S: scales 16 B/block   D: fp16 d 2 B/block
+//   Q8_0  A: qs 32 B/block     D: fp16 d 2 B/block
+//   F32/F16 plain (A).
 #pragma once
 
 #include <cstddef>
@@ -59,7 +60,7 @@ inline size_t tensor_bytes(int t, int64_t rows, int64_t cols) {
 struct DevMat {
     int type = -1;
     int64_t rows = 0, cols = 0;
-    size_t off_a = 0, off_s = 0, off_d = 0;  // plane offsets (arena-relative)
+    size_t off_a = 0, off_h = 0, off_s = 0, off_d = 0;  // plane offsets (arena-relative)
     size_t bytes = 0;                          // algorithmic bytes
 };
 
@@ -68,19 +69,28 @@ inline size_t plan_planes(DevMat& m, size_t base) {
     const size_t nblk = (size_t)m.rows * (size_t)(m.cols / block_elems(m.type));
     m.bytes = tensor_bytes(m.type, m.rows, m.cols);
     m.off_a = align_up(base, 256);
-    if (m.type == T_Q6_K) {
-        m.off_s = align_up(m.off_a + nblk * 192, 256);
-        m.off_d = align_up(m.off_s + nblk * 16, 256);
-        return m.off_d + nblk * 2;
+    m.off_h = m.off_s = m.off_d = m.off_a;
+    switch (m.type) {
+        case T_Q4_K:
+            m.off_s = align_up(m.off_a + nblk * 128, 256);
+            return m.off_s + nblk * 16;
+        case T_Q5_K:
+            m.off_h = align_up(m.off_a + nblk * 128, 256);
+            m.off_s = align_up(m.off_h + nblk * 32, 256);
+            return m.off_s + nblk * 16;
+        case T_Q6_K:
+            m.off_h = align_up(m.off_a + nblk * 128, 256);
+            m.off_s = align_up(m.off_h + nblk * 64, 256);
+            m.off_d = align_up(m.off_s + nblk * 16, 256);
+            return m.off_d + nblk * 2;
+        case T_Q8_0:
+            m.off_d = align_up(m.off_a + nblk * 32, 256);
+            return m.off_d + nblk * 2;
+        default:
+            return m.off_a + m.bytes;
     }
-    if (m.type == T_Q8_0) {
-        m.off_d = align_up(m.off_a + nblk * 32, 256);
-        m.off_s = m.off_d;
-        return m.off_d + nblk * 2;
-    }
-    m.off_s = m.off_d = m.off_a;
-    return m.off_a + m.bytes;
 }
+inline bool needs_repack(int t) { return t == T_Q4_K || t == T_Q5_K || t == T_Q6_K || t == T_Q8_0; }
 
 // On-device decode state (one per context).  Step s at position p:
 //   k_embed (every workgroup): p = pos_next; token = (token_in_pos == p) ? token_in

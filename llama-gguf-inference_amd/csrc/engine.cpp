@@ -202,18 +202,18 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
     }
     size_t stage_bytes = 0;
     for (const Item& it : items)
-        if (it.m->type == T_Q6_K || it.m->type == T_Q8_0) stage_bytes = std::max(stage_bytes, it.t->nbytes);
+        if (needs_repack(it.m->type)) stage_bytes = std::max(stage_bytes, it.t->nbytes);
     uint8_t* stage = nullptr;
     if (stage_bytes) HIPC(hipMalloc(&stage, stage_bytes));
     bool ok = true;
     for (const Item& it : items) {
         hipError_t e;
-        if (it.m->type == T_Q6_K || it.m->type == T_Q8_0) {
+        if (needs_repack(it.m->type)) {
             e = hipMemcpy(stage, it.t->data, it.t->nbytes, hipMemcpyHostToDevice);
             if (e == hipSuccess) {
                 const int64_t nblk = it.m->rows * (it.m->cols / block_elems(it.m->type));
-                e = launch_repack(it.m->type, stage, M.arena + it.m->off_a, M.arena + it.m->off_s, M.arena + it.m->off_d,
-                                  nblk, nullptr);
+                e = launch_repack(it.m->type, stage, M.arena + it.m->off_a, M.arena + it.m->off_h, M.arena + it.m->off_s,
+                                  M.arena + it.m->off_d, nblk, nullptr);
                 if (e == hipSuccess) e = hipDeviceSynchronize();
             }
         } else {
@@ -329,6 +329,7 @@ namespace {
 Seg seg_of(const Model& m, const DevMat& d, int row0) {
     Seg s;
     s.a = m.arena + d.off_a;
+    s.h = m.arena + d.off_h;
     s.s = m.arena + d.off_s;
     s.d = m.arena + d.off_d;
     s.type = d.type;

@@ -16,9 +16,10 @@ enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LO
 
 // One weight matrix of a fused matvec launch.
 struct Seg {
-    const uint8_t* a = nullptr;  // plane A (blocks / Q6R chunks / Q80R quants)
-    const uint8_t* s = nullptr;  // Q6R scales
-    const uint8_t* d = nullptr;  // Q6R / Q80R fp16 d
+    const uint8_t* a = nullptr;  // plane A: quants in piece order
+    const uint8_t* h = nullptr;  // plane H: Q5_K fifth bits / Q6_K 2-bit highs
+    const uint8_t* s = nullptr;  // plane S: Q4_K/Q5_K headers, Q6_K scales
+    const uint8_t* d = nullptr;  // plane D: Q6_K / Q8_0 fp16 d
     int type = -1;
     int rows = 0;
     int row0 = 0;                // first row of this segment in the launch's output space
@@ -71,9 +72,10 @@ size_t mv_lds_bytes(int act, int cols);
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t stream);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
-hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* s, uint8_t* d, int64_t nblk, hipStream_t stream);
+hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, hipStream_t stream);
 // writes the prologue's quantized activation in ggml block form (test hook)
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);
+hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int blocks, hipStream_t stream);
 hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream_t stream);
 
 }  // namespace llmi

@@ -7,20 +7,21 @@
 //
 //   k_matvec  one launch per fused weight group (QKV, O, gate+up, down, output head).
 //     prologue  every workgroup re-derives the quantized activation in LDS from the
-//               f32 input (L2-resident, 16-57 KB): optional RMSNorm (double sum, as
+//               f32 input (L2/MALL-resident, 16-57 KB): optional RMSNorm (double sum, as
 //               ggml_compute_forward_rms_norm) then quantize_row_q8_K_ref /
-//               quantize_row_q8_0_ref bit-exactly.  This replaces a separate norm +
-//               quantize launch (~1.2-1.9 us dependent-kernel boundary on MI355X).
-//     body      a wave owns a PAIR of rows; lane i owns 64-weight chunk i (+64k) of
-//               both rows: 16-B nontemporal loads of the quantized weights, integer
-//               v_dot4c_i32_i8 against the LDS activation (read conflict-free through
-//               an 80-B-per-chunk padded layout), exact int32 per-chunk sums combined
-//               in fp32 exactly as ggml_vec_dot_*_q8_K (d_w*d_a*isum - dmin_w*d_a*imin),
-//               then a 64-lane butterfly reduction.
+//               quantize_row_q8_0_ref, bit-exactly.  This replaces a separate
+//               norm+quantize launch (a 1.2-1.9 us dependent-kernel boundary on MI355X).
+//     body      a wave owns a PAIR of rows; lane L owns pieces L, L+64, ... of both rows
+//               (a piece = 32 weights, common.h): 16-B loads that cover 1 KiB of
+//               consecutive bytes per wave instruction, integer v_dot4c_i32_i8 against
+//               the LDS activation (stored in the same piece order: conflict-free
+//               ds_read_b128), exact int32 per-piece sums combined in fp32 as
+//               ggml_vec_dot_*_q8_K does (d_w*d_a*isum - dmin_w*d_a*imin), then a
+//               64-lane butterfly.  The next piece's weights are in flight while the
+//               current one is reduced, and a wave's first piece is issued before the
+//               prologue so HBM latency overlaps it.
 //     epilogue  store / residual add / RoPE + f16 KV write / SwiGLU / logits + argmax.
-//   k_attn_scores, k_attn_pv   decode attention over the f16 KV cache with ggml's
-//               non-flash numerics (q rounded to f16, softmax with double sum,
-//               probabilities rounded to f16) — exact f16 products summed in double.
+//   k_attn_*   decode attention over the f16 KV cache with ggml's non-flash numerics.
 //   k_embed    token selection (host token or previous argmax) + get_rows dequant.
 //   k_repack_* one-time load-time layout transforms (common.h).
 #include "kernels.h"
@@ -30,9 +31,16 @@
 namespace llmi {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr bool kNontemporalWeights = true;  // weights are read once per token (MI355X_MICROARCH nt-weights)
+// Weight loads use the default cache policy: a wave reads each header line from
+// several lanes/instructions, and measured nontemporal loads were 5-25% slower
+// (profiles/r01/mvbench_nt.md).
+#ifndef LLMI_NT
+#define LLMI_NT 0
+#endif
+constexpr bool kNontemporalWeights = LLMI_NT != 0;
 
 __device__ __forceinline__ float h2f(uint32_t h) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
@@ -43,10 +51,8 @@ __device__ __forceinline__ u32x4 ldw(const uint8_t* p) {
     if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x4*)p);
     else return *(const u32x4*)p;
 }
-__device__ __forceinline__ uint32_t ldw32(const uint8_t* p) {
-    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const uint32_t*)p);
-    else return *(const uint32_t*)p;
-}
+__device__ __forceinline__ u32x2 ldw8(const uint8_t* p) { return *(const u32x2*)p; }
+__device__ __forceinline__ uint32_t ldw4(const uint8_t* p) { return *(const uint32_t*)p; }
 __device__ __forceinline__ int dot4(uint32_t a, int b, int c) {
     return __builtin_amdgcn_sdot4((int)a, b, c, false);
 }
@@ -63,34 +69,37 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ----------------------------------------------------------------------------------
-// LDS carve for the quantized activation
-//   qs: (cols/64) chunks x 80 B (64 B of int8 + 16 B pad: lane i reads chunk i at
-//       80*i + 16*k, which maps 16 consecutive lanes of a ds_read_b128 group to 16
-//       distinct 16-B bank slots -> conflict-free)
-//   d : per-block activation scale (f32; Q8_K per 256, Q8_0 per 32, f16-rounded)
-//   bs: Q8_K bsums (int16 per 16 elements)
+// LDS image of the quantized activation, in piece order (common.h):
+//   K-quants (block_q8_K):  LO[P], HI[P]: 16 int8 each for the low-/high-nibble weights
+//     of piece P; BS[P] = {bsum(lo 16), bsum(hi 16)} as two int16; D[b] per 256-block.
+//   Q8_0 (block_q8_0):      LO[P]: 16 int8 of elements 16P..16P+15; D[b] per 32-block
+//     (f16-rounded, as stored by quantize_row_q8_0).
+// Lane L reads LO[L + 64k] / HI[L + 64k]: 16 consecutive 16-B slots per ds_read_b128
+// lane group -> conflict-free.
 // ----------------------------------------------------------------------------------
 struct Lds {
-    uint8_t* qs;
-    float* d;
+    uint8_t* lo;
+    uint8_t* hi;
     int16_t* bs;
+    float* d;
     double* red;
 };
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t lds_d_off(int cols) { return a16((size_t)(cols / 64) * 80); }
-__host__ __device__ inline size_t lds_bs_off(int act, int cols) {
-    return a16(lds_d_off(cols) + (size_t)(act ? cols / 32 : cols / 256) * 4);
-}
+// byte offsets of the regions; act 0 = q8_K (K-quant weights), 1 = q8_0
+__host__ __device__ inline size_t lds_hi_off(int act, int cols) { return act ? (size_t)cols : (size_t)cols / 2; }
+__host__ __device__ inline size_t lds_bs_off(int act, int cols) { return (size_t)cols; }
+__host__ __device__ inline size_t lds_d_off(int act, int cols) { return a16((size_t)cols + (act ? 0 : (size_t)cols / 8)); }
 __host__ __device__ inline size_t lds_red_off(int act, int cols) {
-    return a16(lds_bs_off(act, cols) + (size_t)(act ? 0 : cols / 16) * 2);
+    return a16(lds_d_off(act, cols) + (size_t)(act ? cols / 32 : cols / 256) * 4);
 }
 size_t mv_lds_bytes(int act, int cols) { return lds_red_off(act, cols) + 8 * sizeof(double); }
 
 __device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
     Lds l;
-    l.qs = smem;
-    l.d = (float*)(smem + lds_d_off(cols));
+    l.lo = smem;
+    l.hi = smem + lds_hi_off(act, cols);
     l.bs = (int16_t*)(smem + lds_bs_off(act, cols));
+    l.d = (float*)(smem + lds_d_off(act, cols));
     l.red = (double*)(smem + lds_red_off(act, cols));
     return l;
 }
@@ -117,21 +126,24 @@ __device__ double block_sum_d(double v, double* red) {
 template <int ACT, bool NORM>
 __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
     const int tid = threadIdx.x, cols = A.cols;
+    const int nsub = cols / 16;
     float scale = 1.0f;
     if constexpr (NORM) {
         double s = 0.0;
-        for (int i = tid * 4; i < cols; i += kMVThreads * 4) {
-            const float4 v = *(const float4*)(A.x + i);
-            s += (double)(v.x * v.x);
-            s += (double)(v.y * v.y);
-            s += (double)(v.z * v.z);
-            s += (double)(v.w * v.w);
+        for (int sb = tid; sb < nsub; sb += kMVThreads) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = *(const float4*)(A.x + sb * 16 + 4 * k);
+                s += (double)(v.x * v.x);
+                s += (double)(v.y * v.y);
+                s += (double)(v.z * v.z);
+                s += (double)(v.w * v.w);
+            }
         }
         s = block_sum_d(s, L.red);
         const float mean = (float)(s / (double)cols);
         scale = 1.0f / sqrtf(mean + A.eps);
     }
-    const int nsub = cols / 16;
     for (int sb = tid; sb < nsub; sb += kMVThreads) {
         float v[16];
 #pragma unroll
@@ -150,6 +162,7 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
             }
         }
         int q[16];
+        uint8_t* dst;
         if constexpr (ACT == 0) {
             float am = 0.f, mv = 0.f;
             int gi = sb * 16;
@@ -179,7 +192,11 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
                 }
                 dval = 1.0f / iscale;
             }
-            L.bs[sb] = (int16_t)bsum;
+            // sub-block s of block b: chunk c = s/4, quarter qq = s%4 -> piece 8b + 2c + (qq&1), lo if qq < 2
+            const int b = sb >> 4, s = sb & 15, P = 8 * b + 2 * (s >> 2) + (s & 1);
+            const bool is_hi = (s & 2) != 0;
+            dst = (is_hi ? L.hi : L.lo) + 16 * P;
+            L.bs[2 * P + (is_hi ? 1 : 0)] = (int16_t)bsum;
             if ((tid & 15) == 0) L.d[sb >> 4] = dval;
         } else {
             float am = 0.f;
@@ -191,36 +208,20 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
             if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
+            dst = L.lo + 16 * sb;
         }
         u32x4 pk;
 #pragma unroll
         for (int w = 0; w < 4; ++w)
             pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
                     ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
-        *(u32x4*)(L.qs + (sb >> 2) * 80 + (sb & 3) * 16) = pk;
+        *(u32x4*)dst = pk;
     }
 }
 
 // ----------------------------------------------------------------------------------
-// Per-type 64-weight chunk: load (global) and integer dot against the LDS activation
+// Per-type piece: load (global) and integer dot against the LDS activation
 // ----------------------------------------------------------------------------------
-struct Act {
-    i32x4 a0, a1, a2, a3;  // activation bytes 0-15, 16-31, 32-47, 48-63 of the chunk
-};
-__device__ __forceinline__ Act load_act(const Lds& L, int ci) {
-    const i32x4* p = (const i32x4*)(L.qs + ci * 80);
-    return {p[0], p[1], p[2], p[3]};
-}
-__device__ __forceinline__ int act_word(const Act& a, int w) {
-    const i32x4& v = w < 4 ? a.a0 : w < 8 ? a.a1 : w < 12 ? a.a2 : a.a3;
-    return v[w & 3];
-}
-
-struct Raw {
-    u32x4 v0, v1, v2, v3, v4;
-    uint32_t e0, e1;
-};
-
 constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u, M1 = 0x01010101u;
 
 // upstream get_scale_min_k4 on the 12 scale bytes held as three words
@@ -234,118 +235,113 @@ __device__ __forceinline__ void scale_min(int j, uint32_t s0, uint32_t s1, uint3
         m = (int)((b2 >> 4) | ((b1 >> 6) << 4));
     }
 }
+// 4 bits -> the low bit of 4 bytes
+__device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x00204081u) & M1; }
 
+// pieces per row and lanes' work items
 template <int T>
-__device__ __forceinline__ Raw load_chunk(const Seg& s, int row, int ci, int nb) {
+__host__ __device__ constexpr int piece_elems() { return T == T_Q8_0 ? 16 : 32; }
+
+struct Raw {
+    u32x4 q;        // 16 B of quants (A plane)
+    u32x4 hdr;      // Q4_K/Q5_K header; Q8_0: .x = fp16 d pair not used
+    u32x2 qh;       // Q5_K (.x) / Q6_K (.x lo, .y hi) high bits
+    uint32_t e0;    // Q6_K scales dword; Q8_0 d
+    uint32_t e1;    // Q6_K d
+};
+
+// Load piece P of row `row`: nbr = blocks per row (K: cols/256, Q8_0: cols/32),
+// npr = pieces per row.
+template <int T>
+__device__ __forceinline__ Raw load_piece(const Seg& s, int row, int P, int nbr, int npr) {
     Raw r;
-    const int c = ci & 3;
-    if constexpr (T == T_Q4_K) {
-        const uint8_t* blk = s.a + ((size_t)row * nb + (ci >> 2)) * 144;
-        r.v0 = ldw(blk);
-        r.v1 = ldw(blk + 16 + 32 * c);
-        r.v2 = ldw(blk + 32 + 32 * c);
-    } else if constexpr (T == T_Q5_K) {
-        const uint8_t* blk = s.a + ((size_t)row * nb + (ci >> 2)) * 176;
-        r.v0 = ldw(blk);
-        r.v1 = ldw(blk + 16);
-        r.v2 = ldw(blk + 32);
-        r.v3 = ldw(blk + 48 + 32 * c);
-        r.v4 = ldw(blk + 64 + 32 * c);
+    const size_t gp = (size_t)row * npr + P;          // global piece index
+    r.q = ldw(s.a + gp * 16);
+    if constexpr (T == T_Q4_K || T == T_Q5_K) {
+        const size_t gb = (size_t)row * nbr + (P >> 3);
+        r.hdr = ldw(s.s + gb * 16);
+        if constexpr (T == T_Q5_K) r.qh.x = ldw4(s.h + gp * 4);
     } else if constexpr (T == T_Q6_K) {
-        const size_t rb = (size_t)row * nb + (ci >> 2);
-        const uint8_t* ch = s.a + rb * 192 + 48 * c;
-        r.v0 = ldw(ch);
-        r.v1 = ldw(ch + 16);
-        r.v2 = ldw(ch + 32);
-        r.e0 = ldw32(s.s + rb * 16 + 4 * c);
-        r.e1 = *(const uint16_t*)(s.d + rb * 2);
-    } else {  // Q8_0: two 32-weight blocks
-        const size_t b0 = (size_t)row * nb + 2 * (size_t)ci;
-        const uint8_t* q = s.a + b0 * 32;
-        r.v0 = ldw(q);
-        r.v1 = ldw(q + 16);
-        r.v2 = ldw(q + 32);
-        r.v3 = ldw(q + 48);
-        r.e0 = ldw32(s.d + b0 * 2);
+        const size_t gb = (size_t)row * nbr + (P >> 3);
+        r.qh = ldw8(s.h + gp * 8);
+        r.e0 = ldw4(s.s + gb * 16 + 4 * ((P & 7) >> 1));
+        r.e1 = *(const uint16_t*)(s.d + gb * 2);
+    } else {  // Q8_0: piece = half block
+        const size_t gb = (size_t)row * nbr + (P >> 1);
+        r.e0 = *(const uint16_t*)(s.d + gb * 2);
     }
     return r;
 }
 
-// ggml_vec_dot_q4_K_q8_K restricted to one 64-weight chunk (sub-blocks 2c, 2c+1)
+struct Act {
+    i32x4 lo, hi;
+    int bs_lo, bs_hi;
+    float d;
+};
+template <int ACT>
+__device__ __forceinline__ Act load_act(const Lds& L, int P) {
+    Act a;
+    a.lo = *(const i32x4*)(L.lo + 16 * P);
+    if constexpr (ACT == 0) {
+        a.hi = *(const i32x4*)(L.hi + 16 * P);
+        const uint32_t bw = *(const uint32_t*)(L.bs + 2 * P);
+        a.bs_lo = (int16_t)(bw & 0xffff);
+        a.bs_hi = (int16_t)(bw >> 16);
+        a.d = L.d[P >> 3];
+    } else {
+        a.d = L.d[P >> 1];
+    }
+    return a;
+}
+
+// Exact integer dot of one piece, combined in fp32 as ggml's per-block formula.
 template <int T>
-__device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, const Lds& L, int ci) {
-    const int c = ci & 3;
+__device__ __forceinline__ float dot_piece(const Raw& r, const Act& a, int P) {
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
+        const int c = (P & 7) >> 1;
         int sc0, m0, sc1, m1;
-        scale_min(2 * c, r.v0.y, r.v0.z, r.v0.w, sc0, m0);
-        scale_min(2 * c + 1, r.v0.y, r.v0.z, r.v0.w, sc1, m1);
-        const u32x4 qa = (T == T_Q4_K) ? r.v1 : r.v3;
-        const u32x4 qb = (T == T_Q4_K) ? r.v2 : r.v4;
+        scale_min(2 * c, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
+        scale_min(2 * c + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
         int lo = 0, hi = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t qw = k < 4 ? qa[k] : qb[k - 4];
-            uint32_t l4 = qw & M4, h4 = (qw >> 4) & M4;
+        for (int k = 0; k < 4; ++k) {
+            uint32_t l4 = r.q[k] & M4, h4 = (r.q[k] >> 4) & M4;
             if constexpr (T == T_Q5_K) {
-                const uint32_t hw = k < 4 ? r.v1[k] : r.v2[k - 4];
-                l4 |= ((hw >> (2 * c)) & M1) << 4;
-                h4 |= ((hw >> (2 * c + 1)) & M1) << 4;
+                l4 |= spread4((r.qh.x >> (4 * k)) & 0xFu) << 4;
+                h4 |= spread4((r.qh.x >> (16 + 4 * k)) & 0xFu) << 4;
             }
-            lo = dot4(l4, act_word(a, k), lo);
-            hi = dot4(h4, act_word(a, 8 + k), hi);
+            lo = dot4(l4, a.lo[k], lo);
+            hi = dot4(h4, a.hi[k], hi);
         }
         const int isum = sc0 * lo + sc1 * hi;
-        const uint2 bw = *(const uint2*)(L.bs + ci * 4);
-        const int b0 = (int16_t)(bw.x & 0xffff), b1 = (int16_t)(bw.x >> 16);
-        const int b2 = (int16_t)(bw.y & 0xffff), b3 = (int16_t)(bw.y >> 16);
-        const int imin = m0 * (b0 + b1) + m1 * (b2 + b3);
-        const float dA = L.d[ci >> 2];
-        const float d = h2f(r.v0.x), dmin = h2f(r.v0.x >> 16);
-        return (d * dA) * (float)isum - (dmin * dA) * (float)imin;
+        const int imin = m0 * a.bs_lo + m1 * a.bs_hi;
+        const float d = h2f(r.hdr.x), dmin = h2f(r.hdr.x >> 16);
+        return (d * a.d) * (float)isum - (dmin * a.d) * (float)imin;
     } else if constexpr (T == T_Q6_K) {
-        const uint32_t Q[8] = {r.v0.x, r.v0.y, r.v0.z, r.v0.w, r.v1.x, r.v1.y, r.v1.z, r.v1.w};
-        const uint32_t H[4] = {r.v2.x, r.v2.y, r.v2.z, r.v2.w};
-        int dm[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int sh = 2 * (k >> 2);
-            const uint32_t ulo = (Q[k] & M4) | (((H[k & 3] >> sh) & M2) << 4);
-            const uint32_t uhi = ((Q[k] >> 4) & M4) | (((H[k & 3] >> (4 + sh)) & M2) << 4);
-            dm[k >> 2] = dot4(ulo, act_word(a, k), dm[k >> 2]);
-            dm[2 + (k >> 2)] = dot4(uhi, act_word(a, 8 + k), dm[2 + (k >> 2)]);
-        }
-        const uint2 bw = *(const uint2*)(L.bs + ci * 4);
-        const int bsv[4] = {(int16_t)(bw.x & 0xffff), (int16_t)(bw.x >> 16), (int16_t)(bw.y & 0xffff),
-                            (int16_t)(bw.y >> 16)};
-        int isum = 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) isum += (int)(int8_t)(r.e0 >> (8 * m)) * (dm[m] - 32 * bsv[m]);
-        const float dA = L.d[ci >> 2];
-        return (h2f(r.e1) * dA) * (float)isum;
-    } else {
-        int s0 = 0, s1 = 0;
+        int lo = 0, hi = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            s0 = dot4(r.v0[k], a.a0[k], s0);
-            s0 = dot4(r.v1[k], a.a1[k], s0);
-            s1 = dot4(r.v2[k], a.a2[k], s1);
-            s1 = dot4(r.v3[k], a.a3[k], s1);
+            const uint32_t ulo = (r.q[k] & M4) | (((r.qh.x >> (2 * k)) & M2) << 4);
+            const uint32_t uhi = ((r.q[k] >> 4) & M4) | (((r.qh.y >> (2 * k)) & M2) << 4);
+            lo = dot4(ulo, a.lo[k], lo);
+            hi = dot4(uhi, a.hi[k], hi);
         }
-        const float dA0 = L.d[2 * ci], dA1 = L.d[2 * ci + 1];
-        return (float)s0 * (h2f(r.e0) * dA0) + (float)s1 * (h2f(r.e0 >> 16) * dA1);
+        const int half = P & 1;
+        const int sc0 = (int8_t)(r.e0 >> (8 * half)), sc1 = (int8_t)(r.e0 >> (8 * (2 + half)));
+        const int isum = sc0 * (lo - 32 * a.bs_lo) + sc1 * (hi - 32 * a.bs_hi);
+        return (h2f(r.e1) * a.d) * (float)isum;
+    } else {
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s = dot4(r.q[k], a.lo[k], s);
+        return (float)s * (h2f(r.e0) * a.d);
     }
 }
 
-// ----------------------------------------------------------------------------------
-// Row-pair work items.  A wave streams its pairs p = w0, w0+G, ... (G = 4*gridDim.x);
-// each pair is NJ = ceil(cols/4096) items (lane chunk ci = lane + 64*j).  Items of the
-// kernel's primary weight type T are software-pipelined: the next item's weights are
-// in flight while the current one is reduced, and the wave's first item is issued
-// BEFORE the activation prologue so HBM latency overlaps it.
-// ----------------------------------------------------------------------------------
 __device__ __forceinline__ Seg pick(const MVArgs& A, int si) {
     Seg s;
     s.a = si == 0 ? A.seg[0].a : si == 1 ? A.seg[1].a : A.seg[2].a;
+    s.h = si == 0 ? A.seg[0].h : si == 1 ? A.seg[1].h : A.seg[2].h;
     s.s = si == 0 ? A.seg[0].s : si == 1 ? A.seg[1].s : A.seg[2].s;
     s.d = si == 0 ? A.seg[0].d : si == 1 ? A.seg[1].d : A.seg[2].d;
     s.type = si == 0 ? A.seg[0].type : si == 1 ? A.seg[1].type : A.seg[2].type;
@@ -354,6 +350,10 @@ __device__ __forceinline__ Seg pick(const MVArgs& A, int si) {
     return s;
 }
 
+// ----------------------------------------------------------------------------------
+// Row-pair work items.  A wave streams its pairs p = w0, w0+G, ... (G = 4*gridDim.x);
+// item j of a pair is piece P = lane + 64*j of both rows (NJ = ceil(pieces/64)).
+// ----------------------------------------------------------------------------------
 struct PairRef {
     Seg sa, sb;
     int ra, rb;
@@ -390,19 +390,19 @@ struct PairRaw {
 };
 
 template <int T>
-__device__ __forceinline__ PairRaw<T> load_item(const PairRef& r, int ci, int cpr, int nb) {
+__device__ __forceinline__ PairRaw<T> load_item(const PairRef& r, int P, int npr, int nbr) {
     PairRaw<T> w;
-    if (ci < cpr) {
-        w.a = load_chunk<T>(r.sa, r.ra, ci, nb);
-        if (r.vb) w.b = load_chunk<T>(r.sb, r.rb, ci, nb);
+    if (P < npr) {
+        w.a = load_piece<T>(r.sa, r.ra, P, nbr, npr);
+        if (r.vb) w.b = load_piece<T>(r.sb, r.rb, P, nbr, npr);
     }
     return w;
 }
 
 // Two-row 64-lane butterfly in 6 shuffles: step 1 exchanges across the halves (lane
 // L<32 keeps row a, L>=32 row b), steps 2-6 reduce each half.  Per row this is exactly
-// the xor-butterfly tree (pairs (L, L^32), then ^16 ... ^1), so the oracle's device
-// order models it; row a lands in lane 0, row b in lane 32.
+// the xor-butterfly tree (pairs (L, L^32), then ^16 ... ^1), which the oracle's device
+// order models; row a lands in lane 0, row b in lane 32.
 __device__ __forceinline__ float reduce_pair(float acc_a, float acc_b) {
     const int lane = threadIdx.x & 63;
     const float send = lane < 32 ? acc_b : acc_a;
@@ -473,25 +473,25 @@ __device__ __forceinline__ void epilogue(const MVArgs& A, const PairRef& r, int 
 
 // Non-pipelined fallback for pairs whose type is not the kernel's primary type (the
 // Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs).
-template <int T>
+template <int ACT, int T>
 __device__ __forceinline__ float generic_row(const Seg& s, int row, int cols, const Lds& L) {
-    const int cpr = cols >> 6, nb = (T == T_Q8_0) ? (cols >> 5) : (cols >> 8);
+    const int npr = cols / piece_elems<T>(), nbr = (T == T_Q8_0) ? (cols >> 5) : (cols >> 8);
     float acc = 0.f;
-    for (int ci = threadIdx.x & 63; ci < cpr; ci += 64) {
-        const Raw w = load_chunk<T>(s, row, ci, nb);
-        acc += dot_chunk<T>(w, load_act(L, ci), L, ci);
+    for (int P = threadIdx.x & 63; P < npr; P += 64) {
+        const Raw w = load_piece<T>(s, row, P, nbr, npr);
+        acc += dot_piece<T>(w, load_act<ACT>(L, P), P);
     }
     return acc;
 }
 template <int ACT>
 __device__ __forceinline__ float generic_row_any(int type, const Seg& s, int row, int cols, const Lds& L) {
     if constexpr (ACT == 1) {
-        return generic_row<T_Q8_0>(s, row, cols, L);
+        return generic_row<1, T_Q8_0>(s, row, cols, L);
     } else {
         switch (type) {
-            case T_Q4_K: return generic_row<T_Q4_K>(s, row, cols, L);
-            case T_Q5_K: return generic_row<T_Q5_K>(s, row, cols, L);
-            case T_Q6_K: return generic_row<T_Q6_K>(s, row, cols, L);
+            case T_Q4_K: return generic_row<0, T_Q4_K>(s, row, cols, L);
+            case T_Q5_K: return generic_row<0, T_Q5_K>(s, row, cols, L);
+            case T_Q6_K: return generic_row<0, T_Q6_K>(s, row, cols, L);
             default: return 0.f;
         }
     }
@@ -504,8 +504,8 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int G = gridDim.x * 4;
-    const int cpr = A.cols >> 6, NJ = (cpr + 63) >> 6;
-    const int nb = (T == T_Q8_0) ? (A.cols >> 5) : (A.cols >> 8);
+    const int npr = A.cols / piece_elems<T>(), NJ = (npr + 63) >> 6;
+    const int nbr = (T == T_Q8_0) ? (A.cols >> 5) : (A.cols >> 8);
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     if (p < A.npairs) {
         r = pair_ref<EPI>(A, p);
         pipe = r.type == T;
-        if (pipe) cur = load_item<T>(r, lane, cpr, nb);  // issued before the prologue
+        if (pipe) cur = load_item<T>(r, lane, npr, nbr);  // issued before the prologue
     }
     mv_prologue<ACT, NORM>(A, L);
     __syncthreads();
@@ -536,12 +536,12 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             }
             const bool has_next = pn < A.npairs && rn.type == T;
             PairRaw<T> nxt;
-            if (has_next) nxt = load_item<T>(rn, lane + 64 * jn, cpr, nb);
-            const int ci = lane + 64 * j;
-            if (ci < cpr) {
-                const Act act = load_act(L, ci);
-                acc_a += dot_chunk<T>(cur.a, act, L, ci);
-                if (r.vb) acc_b += dot_chunk<T>(cur.b, act, L, ci);
+            if (has_next) nxt = load_item<T>(rn, lane + 64 * jn, npr, nbr);
+            const int P = lane + 64 * j;
+            if (P < npr) {
+                const Act act = load_act<ACT>(L, P);
+                acc_a += dot_piece<T>(cur.a, act, P);
+                if (r.vb) acc_b += dot_piece<T>(cur.b, act, P);
             }
             if (j == NJ - 1) {
                 epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
@@ -549,7 +549,6 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             }
             if (!has_next) {
                 p = pn;
-                if (jn == 0 && pn < A.npairs) r = rn;
                 break;
             }
             cur = nxt;
@@ -566,12 +565,13 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
     }
     if constexpr (EPI == EPI_LOGITS) {
-        const int cur = A.st->pos;
-        if (lane == 0 && best) atomicMax(&A.argmax[cur & 1], best);
-        if (blockIdx.x == 0 && threadIdx.x == 0) A.st->pos_next = cur + 1;
+        const int cur_pos = A.st->pos;
+        if (lane == 0 && best) atomicMax(&A.argmax[cur_pos & 1], best);
+        if (blockIdx.x == 0 && threadIdx.x == 0) A.st->pos_next = cur_pos + 1;
     }
 }
 
+// The prologue's quantized activation written out in ggml block form (test hook).
 template <int ACT>
 __global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -581,14 +581,21 @@ __global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* ou
     __syncthreads();
     const int cols = A.cols;
     for (int e = threadIdx.x; e < cols; e += blockDim.x) {
-        const int8_t qv = (int8_t)L.qs[(e >> 6) * 80 + (e & 63)];
-        if (ACT == 0) out[(size_t)(e >> 8) * 292 + 4 + (e & 255)] = (uint8_t)qv;
-        else out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = (uint8_t)qv;
+        if (ACT == 0) {
+            const int b = e >> 8, w = e & 255, c = w >> 6, t = w & 63, half = (t & 31) >> 4;
+            const int P = 8 * b + 2 * c + half;
+            const int8_t qv = (int8_t)((t < 32 ? L.lo : L.hi)[16 * P + (t & 15)]);
+            out[(size_t)b * 292 + 4 + w] = (uint8_t)qv;
+        } else {
+            out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = L.lo[e];
+        }
     }
     if (ACT == 0) {
         for (int b = threadIdx.x; b < cols / 256; b += blockDim.x) *(float*)(out + (size_t)b * 292) = L.d[b];
-        for (int s = threadIdx.x; s < cols / 16; s += blockDim.x)
-            *(int16_t*)(out + (size_t)(s >> 4) * 292 + 260 + 2 * (s & 15)) = L.bs[s];
+        for (int sb = threadIdx.x; sb < cols / 16; sb += blockDim.x) {
+            const int b = sb >> 4, s = sb & 15, P = 8 * b + 2 * (s >> 2) + (s & 1);
+            *(int16_t*)(out + (size_t)b * 292 + 260 + 2 * s) = L.bs[2 * P + ((s & 2) ? 1 : 0)];
+        }
     } else {
         for (int b = threadIdx.x; b < cols / 32; b += blockDim.x) *(uint16_t*)(out + (size_t)b * 34) = f2h(L.d[b]);
     }
@@ -782,36 +789,35 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
 // ----------------------------------------------------------------------------------
 // Step entry: choose the token, advance pos, dequantize its embedding row
 // (upstream ggml_get_rows + dequantize_row_*; bit-exact).
+// Reads the piece-planar device layout (common.h).
 // ----------------------------------------------------------------------------------
 __device__ float dequant_elem(const Seg& w, int row, int e, int cols) {
     switch (w.type) {
         case T_F32: return ((const float*)w.a)[(size_t)row * cols + e];
         case T_F16: return h2f(((const uint16_t*)w.a)[(size_t)row * cols + e]);
         case T_Q4_K:
-        case T_Q5_K: {
-            const int bb = w.type == T_Q4_K ? 144 : 176;
-            const uint8_t* blk = w.a + ((size_t)row * (cols / 256) + e / 256) * bb;
-            const int i = e & 255, c = i >> 6, l = i & 63, hi = l >= 32;
-            const uint32_t* s32 = (const uint32_t*)(blk + 4);
+        case T_Q5_K:
+        case T_Q6_K: {
+            const int nbr = cols / 256, npr = cols / 32;
+            const int b = e / 256, i = e & 255, c = i >> 6, t = i & 63, hi = t >= 32, l = t & 31, half = l >> 4;
+            const int P = 8 * b + 2 * c + half, k = l & 15;                 // piece and byte within it
+            const size_t gp = (size_t)row * npr + P, gb = (size_t)row * nbr + b;
+            const uint8_t qb = w.a[gp * 16 + k];
+            int q = hi ? (qb >> 4) : (qb & 0xF);
+            if (w.type == T_Q6_K) {
+                const uint8_t hb = w.h[gp * 8 + (hi ? 4 : 0) + (k & 3)];
+                q |= ((hb >> (2 * (k >> 2))) & 3) << 4;
+                const float d = h2f(*(const uint16_t*)(w.d + gb * 2));
+                const int sc = (int8_t)w.s[gb * 16 + (i >> 4)];
+                return d * (float)sc * (float)(q - 32);
+            }
+            const uint32_t* s32 = (const uint32_t*)(w.s + gb * 16);
             int sc, m;
-            scale_min(2 * c + hi, s32[0], s32[1], s32[2], sc, m);
-            const float d = h2f(*(const uint16_t*)blk), dmin = h2f(*(const uint16_t*)(blk + 2));
-            const uint8_t* qs = blk + (w.type == T_Q4_K ? 16 : 48) + 32 * c;
-            int q = hi ? (qs[l - 32] >> 4) : (qs[l] & 0xF);
-            if (w.type == T_Q5_K) q += ((blk[16 + (l & 31)] >> (2 * c + hi)) & 1) ? 16 : 0;
+            scale_min(2 * c + hi, s32[1], s32[2], s32[3], sc, m);
+            if (w.type == T_Q5_K) q += ((ldw4(w.h + gp * 4) >> (16 * hi + k)) & 1) << 4;
+            const float d = h2f(s32[0]), dmin = h2f(s32[0] >> 16);
             const float d1 = d * (float)sc, m1 = dmin * (float)m;
             return d1 * (float)q - m1;
-        }
-        case T_Q6_K: {
-            const size_t rb = (size_t)row * (cols / 256) + e / 256;
-            const int i = e & 255, c = i >> 6, t = i & 63;
-            const uint8_t* ch = w.a + rb * 192 + 48 * c;
-            const int lo4 = t < 32 ? (ch[t] & 0xF) : (ch[t - 32] >> 4);
-            const int hi2 = (ch[32 + (t & 15)] >> (2 * (t >> 4))) & 3;
-            const int q = (lo4 | (hi2 << 4)) - 32;
-            const float d = h2f(*(const uint16_t*)(w.d + rb * 2));
-            const int sc = (int8_t)w.s[rb * 16 + (i >> 4)];
-            return d * (float)sc * (float)q;
         }
         case T_Q8_0: {
             const size_t b = (size_t)row * (cols / 32) + e / 32;
@@ -844,32 +850,60 @@ __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
 }
 
 // ----------------------------------------------------------------------------------
-// Load-time repack (common.h): Q6_K 210-B blocks -> Q6R planes; Q8_0 -> Q80R planes.
+// Load-time repack of GGUF blocks into the piece-planar layout (common.h).
+// One thread per (block, piece r in 0..7).
 // ----------------------------------------------------------------------------------
-__global__ void k_repack_q6k(const uint8_t* raw, uint8_t* A, uint8_t* S, uint8_t* Dp, int64_t nblk) {
+__global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H, uint8_t* S, uint8_t* Dp, int64_t nblk) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t b = gid >> 2;
-    const int c = (int)(gid & 3);
+    const int64_t b = gid >> 3;
+    const int r = (int)(gid & 7), c = r >> 1, half = r & 1;
     if (b >= nblk) return;
-    const uint8_t* x = raw + b * 210;
-    const uint8_t* ql = x;
-    const uint8_t* qh = x + 128;
-    auto u6 = [&](int w) -> int {  // 6-bit unsigned value of weight w of the block
-        const int n = w >> 7, r = w & 127, quad = r >> 5, l = r & 31;
-        const uint8_t qlb = ql[64 * n + l + 32 * (quad & 1)];
-        const int lo = (quad >> 1) ? (qlb >> 4) : (qlb & 0xF);
-        const int hi = (qh[32 * n + l] >> (2 * quad)) & 3;
-        return lo | (hi << 4);
-    };
-    uint8_t* o = A + b * 192 + 48 * c;
-    for (int t = 0; t < 32; ++t) o[t] = (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
-    for (int s = 0; s < 16; ++s) {
-        uint8_t v = 0;
-        for (int j = 0; j < 4; ++j) v |= (uint8_t)((u6(64 * c + 16 * j + s) >> 4) << (2 * j));
-        o[32 + s] = v;
+    if (type == T_Q4_K || type == T_Q5_K) {
+        const int bb = type == T_Q4_K ? 144 : 176;
+        const uint8_t* x = raw + b * bb;
+        const uint8_t* qs = x + (type == T_Q4_K ? 16 : 48);
+        for (int i = 0; i < 16; ++i) A[(b * 8 + r) * 16 + i] = qs[16 * r + i];
+        if (r == 0)
+            for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[i];
+        if (type == T_Q5_K) {
+            const uint8_t* qh = x + 16;
+            uint32_t bits = 0;
+            for (int i = 0; i < 16; ++i) {
+                bits |= (uint32_t)((qh[16 * half + i] >> (2 * c)) & 1) << i;
+                bits |= (uint32_t)((qh[16 * half + i] >> (2 * c + 1)) & 1) << (16 + i);
+            }
+            for (int k = 0; k < 4; ++k) H[(b * 8 + r) * 4 + k] = (uint8_t)(bits >> (8 * k));
+        }
+    } else {  // Q6_K
+        const uint8_t* x = raw + b * 210;
+        const uint8_t* ql = x;
+        const uint8_t* qh = x + 128;
+        auto u6 = [&](int w) -> int {  // 6-bit unsigned value of weight w of the block
+            const int n = w >> 7, rr = w & 127, quad = rr >> 5, l = rr & 31;
+            const uint8_t qlb = ql[64 * n + l + 32 * (quad & 1)];
+            const int lo = (quad >> 1) ? (qlb >> 4) : (qlb & 0xF);
+            const int hi = (qh[32 * n + l] >> (2 * quad)) & 3;
+            return lo | (hi << 4);
+        };
+        const int wlo = 64 * c + 16 * half, whi = wlo + 32;
+        uint8_t* o = A + (b * 8 + r) * 16;
+        for (int i = 0; i < 16; ++i) o[i] = (uint8_t)((u6(wlo + i) & 15) | ((u6(whi + i) & 15) << 4));
+        uint8_t* h = H + (b * 8 + r) * 8;
+        for (int j = 0; j < 4; ++j) {  // byte j bits [2m,2m+1] = high2 of weight 4m+j
+            uint8_t vlo = 0, vhi = 0;
+            for (int m = 0; m < 4; ++m) {
+                vlo |= (uint8_t)((u6(wlo + 4 * m + j) >> 4) << (2 * m));
+                vhi |= (uint8_t)((u6(whi + 4 * m + j) >> 4) << (2 * m));
+            }
+            h[j] = vlo;
+            h[4 + j] = vhi;
+        }
+        if (r == 0) {
+            for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[192 + i];
+            Dp[b * 2] = x[208];
+            Dp[b * 2 + 1] = x[209];
+        }
     }
-    for (int i = 0; i < 4; ++i) S[b * 16 + 4 * c + i] = x[192 + 4 * c + i];
-    if (c == 0) { Dp[b * 2] = x[208]; Dp[b * 2 + 1] = x[209]; }
 }
 
 __global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nblk) {
@@ -879,6 +913,22 @@ __global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_
     for (int i = 0; i < 32; ++i) A[b * 32 + i] = x[2 + i];
     Dp[b * 2] = x[0];
     Dp[b * 2 + 1] = x[1];
+}
+
+// Streaming-read reference (achievable HBM rate for a perfectly coalesced 16-B/lane
+// read of the same bytes): each thread sums dwords of grid-strided 16-B pieces.
+__global__ __launch_bounds__(256) void k_stream_read(const u32x4* p, size_t n16, unsigned* out) {
+    unsigned acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        const u32x4 v = ldw((const uint8_t*)(p + i));
+        acc += v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;  // keep the loads alive
+}
+
+hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int blocks, hipStream_t s) {
+    hipLaunchKernelGGL(k_stream_read, dim3(blocks), dim3(256), 0, s, (const u32x4*)p, bytes / 16, out);
+    return hipGetLastError();
 }
 
 // ----------------------------------------------------------------------------------
@@ -977,11 +1027,13 @@ hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* sp, uint8_t* d, int64_t nblk, hipStream_t s) {
+hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* sp, uint8_t* d, int64_t nblk,
+                         hipStream_t s) {
     if (nblk <= 0) return hipSuccess;
-    if (type == T_Q6_K) {
-        const int64_t thr = nblk * 4;
-        hipLaunchKernelGGL(k_repack_q6k, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, sp, d, nblk);
+    if (type == T_Q4_K || type == T_Q5_K || type == T_Q6_K) {
+        const int64_t thr = nblk * 8;
+        hipLaunchKernelGGL(k_repack_kq, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, type, (const uint8_t*)raw, a,
+                           h, sp, d, nblk);
     } else if (type == T_Q8_0) {
         hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d, nblk);
     } else {

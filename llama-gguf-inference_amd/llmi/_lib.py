@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libllmi.so")
+LIB_PATH = os.environ.get("LLMI_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libllmi.so")
 
 
 class LlmiLibraryError(RuntimeError):
@@ -100,6 +100,7 @@ SIGNATURES = {
     "llmi_repack": (C.c_int32, [C.c_int32, _P, _P, C.c_int64, C.c_int64]),
     "llmi_matvec": (C.c_int32, [C.c_int32, _P, C.c_int64, C.c_int64, _P, _P, C.c_float, _P, C.c_int32]),
     "llmi_quantize_act": (C.c_int32, [C.c_int32, C.c_int64, _P, _P, C.c_float, _P]),
+    "llmi_bench_stream": (C.c_double, [_P, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32, C.c_int32]),
     "llmi_bench_matvec": (C.c_double, [C.c_int32, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, C.c_int32]),
 }
 

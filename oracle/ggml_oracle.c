@@ -345,11 +345,13 @@ static float vd_f32(int n, const float* x, const float* y) {
 
 /* ---------------------------------------------------------------------------
  * Device-order dot (or_set_dot_order(1)): the SAME exact integer block math as the
- * generic functions above, restricted to 64-weight chunks, with the fp32 association
- * the HIP kernel uses: chunk ci contributes
+ * generic functions above, split into 32-weight PIECES (the HIP kernel's unit; piece r
+ * of a K-quant block = the 16 weights 64c+16h+i of scale group 2c and the 16 weights
+ * 32 positions later, c = r/2, h = r%2; a Q8_0 piece = 16 weights), with the fp32
+ * association the kernel uses: piece P contributes
  *   K-quants: (d*dA)*(float)isum - (dmin*dA)*(float)imin      (Q6_K: no min term)
- *   Q8_0    : (float)s0*(d0*dA0) + (float)s1*(d1*dA1)           (two 32-blocks)
- * lane L = ci % 64 accumulates its chunks in order, then a 64-lane xor butterfly.
+ *   Q8_0    : (float)isum * (d*dA)
+ * lane L = P % 64 accumulates its pieces in order, then a 64-lane xor butterfly.
  * Integer sums are ggml's exactly; only fp32 rounding order differs from the
  * generic loop (whose own order differs again from every SIMD variant upstream).
  * --------------------------------------------------------------------------- */
@@ -357,23 +359,23 @@ static int g_dot_order = 0;
 void or_set_dot_order(int mode) { g_dot_order = mode; }
 int or_get_dot_order(void) { return g_dot_order; }
 
-static float chunk_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int c) {
-    const int8_t* a = y->qs + 64 * c;
+static int q6_u6(const block_q6_K* x, int w) {
+    const int n = w >> 7, r = w & 127, quad = r >> 5, l = r & 31;
+    const uint8_t qlb = x->ql[64 * n + l + 32 * (quad & 1)];
+    const int lo = (quad >> 1) ? (qlb >> 4) : (qlb & 0xF);
+    const int hi = (x->qh[32 * n + l] >> (2 * quad)) & 3;
+    return lo | (hi << 4);
+}
+
+static float piece_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int r) {
+    const int c = r >> 1, half = r & 1, wlo = 64 * c + 16 * half, whi = wlo + 32;
+    const int8_t* a = y->qs;
+    const int bl = y->bsums[4 * c + half], bh = y->bsums[4 * c + 2 + half];
     if (wtype == OR_Q6_K) {
         const block_q6_K* x = (const block_q6_K*)blk;
-        int isum = 0;
-        for (int m = 0; m < 4; ++m) {
-            int dot = 0;
-            for (int t = 0; t < 16; ++t) {
-                const int w = 64 * c + 16 * m + t;          /* weight index in block */
-                const int n = w >> 7, r = w & 127, quad = r >> 5, l = r & 31;
-                const uint8_t qlb = x->ql[64 * n + l + 32 * (quad & 1)];
-                const int lo = (quad >> 1) ? (qlb >> 4) : (qlb & 0xF);
-                const int hi = (x->qh[32 * n + l] >> (2 * quad)) & 3;
-                dot += (lo | (hi << 4)) * a[16 * m + t];
-            }
-            isum += x->scales[4 * c + m] * (dot - 32 * y->bsums[4 * c + m]);
-        }
+        int lo = 0, hi = 0;
+        for (int i = 0; i < 16; ++i) { lo += q6_u6(x, wlo + i) * a[wlo + i]; hi += q6_u6(x, whi + i) * a[whi + i]; }
+        const int isum = x->scales[4 * c + half] * (lo - 32 * bl) + x->scales[4 * c + 2 + half] * (hi - 32 * bh);
         return (llmi_h2f(x->d) * y->d) * (float)isum;
     }
     const uint8_t* scales; const uint8_t* qs; const uint8_t* qh = NULL; uint16_t d16, m16;
@@ -383,14 +385,15 @@ static float chunk_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int c)
     get_scale_min_k4(2 * c, scales, &sc0, &m0);
     get_scale_min_k4(2 * c + 1, scales, &sc1, &m1);
     int lo = 0, hi = 0;
-    for (int t = 0; t < 32; ++t) {
-        int ql = qs[32 * c + t] & 0xF, qq = qs[32 * c + t] >> 4;
-        if (qh) { ql += ((qh[t] >> (2 * c)) & 1) << 4; qq += ((qh[t] >> (2 * c + 1)) & 1) << 4; }
-        lo += ql * a[t];
-        hi += qq * a[32 + t];
+    for (int i = 0; i < 16; ++i) {
+        const int l = 16 * half + i;                 /* native qs/qh byte within chunk c */
+        int ql = qs[32 * c + l] & 0xF, qq = qs[32 * c + l] >> 4;
+        if (qh) { ql += ((qh[l] >> (2 * c)) & 1) << 4; qq += ((qh[l] >> (2 * c + 1)) & 1) << 4; }
+        lo += ql * a[wlo + i];
+        hi += qq * a[whi + i];
     }
     const int isum = sc0 * lo + sc1 * hi;
-    const int imin = m0 * (y->bsums[4 * c] + y->bsums[4 * c + 1]) + m1 * (y->bsums[4 * c + 2] + y->bsums[4 * c + 3]);
+    const int imin = m0 * bl + m1 * bh;
     const float dA = y->d;
     return (llmi_h2f(d16) * dA) * (float)isum - (llmi_h2f(m16) * dA) * (float)imin;
 }
@@ -398,20 +401,21 @@ static float chunk_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int c)
 static float vd_device_order(int wtype, int n, const void* w, const void* act) {
     float acc[64];
     for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
-    const int nch = n / 64;
-    for (int ci = 0; ci < nch; ++ci) {
+    const int np = wtype == OR_Q8_0 ? n / 16 : n / 32;
+    for (int P = 0; P < np; ++P) {
         float v;
         if (wtype == OR_Q8_0) {
-            const block_q8_0* x = (const block_q8_0*)w + 2 * ci;
-            const block_q8_0* y = (const block_q8_0*)act + 2 * ci;
-            int s0 = 0, s1 = 0;
-            for (int j = 0; j < 32; ++j) { s0 += x[0].qs[j] * y[0].qs[j]; s1 += x[1].qs[j] * y[1].qs[j]; }
-            v = (float)s0 * (llmi_h2f(x[0].d) * llmi_h2f(y[0].d)) + (float)s1 * (llmi_h2f(x[1].d) * llmi_h2f(y[1].d));
+            const block_q8_0* x = (const block_q8_0*)w + P / 2;
+            const block_q8_0* y = (const block_q8_0*)act + P / 2;
+            const int h = 16 * (P & 1);
+            int s0 = 0;
+            for (int j = 0; j < 16; ++j) s0 += x->qs[h + j] * y->qs[h + j];
+            v = (float)s0 * (llmi_h2f(x->d) * llmi_h2f(y->d));
         } else {
             const size_t bb = or_type_size(wtype);
-            v = chunk_kq(wtype, (const uint8_t*)w + (size_t)(ci / 4) * bb, (const block_q8_K*)act + ci / 4, ci % 4);
+            v = piece_kq(wtype, (const uint8_t*)w + (size_t)(P / 8) * bb, (const block_q8_K*)act + P / 8, P % 8);
         }
-        acc[ci % 64] = acc[ci % 64] + v;
+        acc[P % 64] = acc[P % 64] + v;
     }
     for (int o = 32; o >= 1; o >>= 1)
         for (int l = 0; l < o; ++l) acc[l] = acc[l] + acc[l + o];
@@ -419,7 +423,7 @@ static float vd_device_order(int wtype, int n, const void* w, const void* act) {
 }
 
 float or_vec_dot(int wtype, int n, const void* w, const void* a) {
-    if (g_dot_order == 1 && (wtype == OR_Q4_K || wtype == OR_Q5_K || wtype == OR_Q6_K || wtype == OR_Q8_0) && n % 64 == 0)
+    if (g_dot_order == 1 && (wtype == OR_Q4_K || wtype == OR_Q5_K || wtype == OR_Q6_K || wtype == OR_Q8_0) && n % 256 == 0)
         return vd_device_order(wtype, n, w, a);
     switch (wtype) {
         case OR_Q4_K: return vd_q4_K(n, w, a);
