@@ -576,7 +576,7 @@ int32_t llmi_repack(int32_t type, const void* raw, void* w, int64_t rows, int64_
     hipError_t e;
     if (needs_repack(type)) {
         e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_h, (uint8_t*)w + dm.off_s,
-                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), nullptr);
+                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), cols, nullptr);
     } else {
         e = hipMemcpy(w, raw, dm.bytes, hipMemcpyDeviceToDevice);
     }
@@ -601,7 +601,7 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
     (void)hipGetDevice(&dev);
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, dev);
-    hipError_t e = launch_matvec(a, mode == 1 ? EPI_ADD : EPI_STORE, std::max(64, prop.multiProcessorCount * 4), nullptr);
+    hipError_t e = launch_matvec(a, mode == 1 ? EPI_ADD : EPI_STORE, std::max(64, prop.multiProcessorCount * wg_per_cu()), nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
     return 0;
@@ -626,7 +626,7 @@ double llmi_bench_matvec(int32_t type, const void* w, int32_t n_mats, int64_t ro
     (void)hipGetDevice(&dev);
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, dev);
-    const int mb = std::max(64, prop.multiProcessorCount * 4);
+    const int mb = std::max(64, prop.multiProcessorCount * wg_per_cu());
     MVArgs a;
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
     for (int k = 0; k < n_mats; ++k) {  // warm-up (code, TLB)

@@ -1,16 +1,19 @@
 // common.h — shared host/device definitions of the llmi decode path.
 //
 // Device weight layouts (DESIGN.md §Data layout in HBM).  Every quantized matrix is
-// repacked once at load into "piece-planar" form: a PIECE is 32 weights of one block
-// (K-quants: 16 weights of scale group 2c and the 16 weights 32 positions later, i.e.
-// the low and high nibbles of 16 consecutive native qs bytes; Q8_0: 16 weights), and
-// each plane stores one field of all pieces of a row contiguously, so a wave64 load of
-// 16 B/lane reads 1 KiB of consecutive bytes.  Byte counts equal GGUF exactly.
-//   Q4_K  A: qs 128 B/block (= native qs)            S: header {d, dmin, scales[12]} 16 B/block
-//   Q5_K  A: qs 128 B/block   H: 4 B/piece (32 fifth bits)   S: header 16 B/block
-//   Q6_K  A: ql 128 B/block (piece order)  H: 8 B/piece (2-bit highs, shift-decodable)
-//         S: scales 16 B/block   D: fp16 d 2 B/block
-//   Q8_0  A: qs 32 B/block     D: fp16 d 2 B/block
+// repacked once at load into "chunk-planar" form.  A CHUNK is 64 consecutive weights of
+// a row (K-quants: quarter c of a 256-block, whose low nibbles are weights 64c+0..31 and
+// high nibbles 64c+32..63 of native qs[32c..32c+31]; Q8_0: two 32-blocks).  The quant
+// bytes of each chunk are split into 16-B parts k and stored part-major per row:
+//     A[row][k][chunk][16 B]      (k < 2 for K-quants, k < 4 for Q8_0)
+// so lane L reading part k of chunk L touches 1 KiB of consecutive bytes per wave
+// instruction.  Per-block headers / per-chunk high bits live in their own planes.
+// Byte counts equal GGUF exactly (the repack moves bytes, it never widens them):
+//   Q4_K  A: qs 128 B/block   S: header {d, dmin, scales[12]} 16 B/block
+//   Q5_K  A: qs 128 B/block   H: 8 B/chunk (fifth bits: lo 32 then hi 32)   S: header 16 B/block
+//   Q6_K  A: ql 128 B/block   H: 16 B/chunk (2-bit highs, shift-decodable)
+//         S: scales 16 B/block (= 4 B/chunk, native order)   D: fp16 d 2 B/block
+//   Q8_0  A: qs 32 B/block    D: fp16 d 2 B/block (= 4 B/chunk)
 //   F32/F16 plain (A).
 #pragma once
 

@@ -9,11 +9,21 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace llmi {
 
 std::string hip_err(hipError_t e) { return std::string(hipGetErrorString(e)); }
+
+int wg_per_cu() {
+    static const int v = [] {
+        const char* e = getenv("LLMI_WG_PER_CU");
+        const int n = e ? atoi(e) : 0;
+        return n > 0 ? n : 4;
+    }();
+    return v;
+}
 
 #define HIPC(expr)                                                         \
     do {                                                                   \
@@ -213,7 +223,7 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
             if (e == hipSuccess) {
                 const int64_t nblk = it.m->rows * (it.m->cols / block_elems(it.m->type));
                 e = launch_repack(it.m->type, stage, M.arena + it.m->off_a, M.arena + it.m->off_h, M.arena + it.m->off_s,
-                                  M.arena + it.m->off_d, nblk, nullptr);
+                                  M.arena + it.m->off_d, nblk, it.m->cols, nullptr);
                 if (e == hipSuccess) e = hipDeviceSynchronize();
             }
         } else {
@@ -250,7 +260,7 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string&
     HIPC(hipSetDevice(m->device));
     hipDeviceProp_t prop;
     HIPC(hipGetDeviceProperties(&prop, m->device));
-    c.max_blocks = std::max(64, prop.multiProcessorCount * 4);
+    c.max_blocks = std::max(64, prop.multiProcessorCount * wg_per_cu());
     HIPC(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     HIPC(hipEventCreate(&c.ev0));
     HIPC(hipEventCreate(&c.ev1));

@@ -72,7 +72,8 @@ size_t mv_lds_bytes(int act, int cols);
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t stream);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
-hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, hipStream_t stream);
+hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, int64_t cols,
+                         hipStream_t stream);
 // writes the prologue's quantized activation in ggml block form (test hook)
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);
 hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int blocks, hipStream_t stream);

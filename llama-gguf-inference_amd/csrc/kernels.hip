@@ -69,13 +69,15 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ----------------------------------------------------------------------------------
-// LDS image of the quantized activation, in piece order (common.h):
-//   K-quants (block_q8_K):  LO[P], HI[P]: 16 int8 each for the low-/high-nibble weights
-//     of piece P; BS[P] = {bsum(lo 16), bsum(hi 16)} as two int16; D[b] per 256-block.
-//   Q8_0 (block_q8_0):      LO[P]: 16 int8 of elements 16P..16P+15; D[b] per 32-block
+// LDS image of the quantized activation, in the weights' chunk-part order (common.h):
+//   K-quants (block_q8_K): LO[k][ch], HI[k][ch]: 16 int8 each = activation of the
+//     weights in the low / high nibbles of quant part k of chunk ch (chunk weights
+//     16k..16k+15 and 32+16k..32+16k+15); BS[4ch+i] = bsums in natural order;
+//     D[b] per 256-block.
+//   Q8_0 (block_q8_0): LO[k][ch] (k < 4) = elements 64ch+16k..+15; D[b] per 32-block
 //     (f16-rounded, as stored by quantize_row_q8_0).
-// Lane L reads LO[L + 64k] / HI[L + 64k]: 16 consecutive 16-B slots per ds_read_b128
-// lane group -> conflict-free.
+// Lane L reads LO[k][L + 64j]: 16 consecutive 16-B slots per ds_read_b128 lane group,
+// conflict-free.
 // ----------------------------------------------------------------------------------
 struct Lds {
     uint8_t* lo;
@@ -192,11 +194,10 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
                 }
                 dval = 1.0f / iscale;
             }
-            // sub-block s of block b: chunk c = s/4, quarter qq = s%4 -> piece 8b + 2c + (qq&1), lo if qq < 2
-            const int b = sb >> 4, s = sb & 15, P = 8 * b + 2 * (s >> 2) + (s & 1);
-            const bool is_hi = (s & 2) != 0;
-            dst = (is_hi ? L.hi : L.lo) + 16 * P;
-            L.bs[2 * P + (is_hi ? 1 : 0)] = (int16_t)bsum;
+            // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: lo part k=qq (qq<2), hi part k=qq-2
+            const int nch = cols >> 6, ch = sb >> 2, qq = sb & 3;
+            dst = (qq < 2 ? L.lo : L.hi) + 16 * ((qq & 1) * nch + ch);
+            L.bs[sb] = (int16_t)bsum;
             if ((tid & 15) == 0) L.d[sb >> 4] = dval;
         } else {
             float am = 0.f;
@@ -208,7 +209,8 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
             if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
-            dst = L.lo + 16 * sb;
+            const int nch = cols >> 6;
+            dst = L.lo + 16 * ((sb & 3) * nch + (sb >> 2));
         }
         u32x4 pk;
 #pragma unroll
@@ -220,7 +222,7 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
 }
 
 // ----------------------------------------------------------------------------------
-// Per-type piece: load (global) and integer dot against the LDS activation
+// Per-type 64-weight chunk: load (global) and integer dot against the LDS activation
 // ----------------------------------------------------------------------------------
 constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u, M1 = 0x01010101u;
 
@@ -238,103 +240,144 @@ __device__ __forceinline__ void scale_min(int j, uint32_t s0, uint32_t s1, uint3
 // 4 bits -> the low bit of 4 bytes
 __device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x00204081u) & M1; }
 
-// pieces per row and lanes' work items
 template <int T>
-__host__ __device__ constexpr int piece_elems() { return T == T_Q8_0 ? 16 : 32; }
+__host__ __device__ constexpr int kparts() { return T == T_Q8_0 ? 4 : 2; }
 
+// One chunk of one row in registers.
 struct Raw {
-    u32x4 q;        // 16 B of quants (A plane)
-    u32x4 hdr;      // Q4_K/Q5_K header; Q8_0: .x = fp16 d pair not used
-    u32x2 qh;       // Q5_K (.x) / Q6_K (.x lo, .y hi) high bits
-    uint32_t e0;    // Q6_K scales dword; Q8_0 d
-    uint32_t e1;    // Q6_K d
+    u32x4 q0, q1, q2, q3;  // quant parts (q2, q3: Q8_0 only)
+    u32x4 hdr;             // Q4_K/Q5_K block header; Q6_K: 2-bit highs (4 dwords)
+    u32x2 qh;              // Q5_K fifth bits (lo 32, hi 32)
+    uint32_t e0;           // Q6_K chunk scales (4 x int8); Q8_0: the two fp16 d
+    uint32_t e1;           // Q6_K fp16 d
 };
 
-// Load piece P of row `row`: nbr = blocks per row (K: cols/256, Q8_0: cols/32),
-// npr = pieces per row.
+// Row view: uniform per-row base pointers (SGPRs) so per-lane addressing is a small
+// 32-bit offset: quant part k of chunk ch at qa + (k*nch + ch)*16.
+struct RowPtr {
+    const uint8_t* qa;  // A plane, this row
+    const uint8_t* hb;  // H plane, this row
+    const uint8_t* sb;  // S plane, this row
+    const uint8_t* db;  // D plane, this row
+};
 template <int T>
-__device__ __forceinline__ Raw load_piece(const Seg& s, int row, int P, int nbr, int npr) {
+__device__ __forceinline__ RowPtr row_ptr(const Seg& s, int row, int cols) {
+    RowPtr r;
+    const size_t nch = (size_t)(cols >> 6), nblk = (T == T_Q8_0) ? (size_t)(cols >> 5) : (size_t)(cols >> 8);
+    r.qa = s.a + (size_t)row * nch * (T == T_Q8_0 ? 64 : 32);
+    r.hb = s.h + (size_t)row * nch * (T == T_Q6_K ? 16 : 8);
+    r.sb = s.s + (size_t)row * nblk * 16;
+    r.db = s.d + (size_t)row * nblk * 2;
+    return r;
+}
+
+template <int T>
+__device__ __forceinline__ Raw load_chunk(const RowPtr& rp, int ch, int nch) {
     Raw r;
-    const size_t gp = (size_t)row * npr + P;          // global piece index
-    r.q = ldw(s.a + gp * 16);
+    const uint32_t o = (uint32_t)ch * 16, step = (uint32_t)nch * 16;
+    r.q0 = ldw(rp.qa + o);
+    r.q1 = ldw(rp.qa + o + step);
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
-        const size_t gb = (size_t)row * nbr + (P >> 3);
-        r.hdr = ldw(s.s + gb * 16);
-        if constexpr (T == T_Q5_K) r.qh.x = ldw4(s.h + gp * 4);
+        r.hdr = ldw(rp.sb + (uint32_t)(ch >> 2) * 16);
+        if constexpr (T == T_Q5_K) r.qh = ldw8(rp.hb + (uint32_t)ch * 8);
     } else if constexpr (T == T_Q6_K) {
-        const size_t gb = (size_t)row * nbr + (P >> 3);
-        r.qh = ldw8(s.h + gp * 8);
-        r.e0 = ldw4(s.s + gb * 16 + 4 * ((P & 7) >> 1));
-        r.e1 = *(const uint16_t*)(s.d + gb * 2);
-    } else {  // Q8_0: piece = half block
-        const size_t gb = (size_t)row * nbr + (P >> 1);
-        r.e0 = *(const uint16_t*)(s.d + gb * 2);
+        r.hdr = ldw(rp.hb + (uint32_t)ch * 16);
+        r.e0 = ldw4(rp.sb + (uint32_t)ch * 4);
+        r.e1 = *(const uint16_t*)(rp.db + (uint32_t)(ch >> 2) * 2);
+    } else {
+        r.q2 = ldw(rp.qa + o + 2 * step);
+        r.q3 = ldw(rp.qa + o + 3 * step);
+        r.e0 = ldw4(rp.db + (uint32_t)ch * 4);
     }
     return r;
 }
 
 struct Act {
-    i32x4 lo, hi;
-    int bs_lo, bs_hi;
-    float d;
+    i32x4 a0, a1, a2, a3;  // K: lo part 0, lo part 1, hi part 0, hi part 1; Q8_0: parts 0..3
+    int bs[4];
+    float d0, d1;
 };
 template <int ACT>
-__device__ __forceinline__ Act load_act(const Lds& L, int P) {
+__device__ __forceinline__ Act load_act(const Lds& L, int ch, int nch) {
     Act a;
-    a.lo = *(const i32x4*)(L.lo + 16 * P);
+    const int step = nch * 16;
+    a.a0 = *(const i32x4*)(L.lo + 16 * ch);
+    a.a1 = *(const i32x4*)(L.lo + 16 * ch + step);
     if constexpr (ACT == 0) {
-        a.hi = *(const i32x4*)(L.hi + 16 * P);
-        const uint32_t bw = *(const uint32_t*)(L.bs + 2 * P);
-        a.bs_lo = (int16_t)(bw & 0xffff);
-        a.bs_hi = (int16_t)(bw >> 16);
-        a.d = L.d[P >> 3];
+        a.a2 = *(const i32x4*)(L.hi + 16 * ch);
+        a.a3 = *(const i32x4*)(L.hi + 16 * ch + step);
+        const uint2 bw = *(const uint2*)(L.bs + 4 * ch);
+        a.bs[0] = (int16_t)(bw.x & 0xffff); a.bs[1] = (int16_t)(bw.x >> 16);
+        a.bs[2] = (int16_t)(bw.y & 0xffff); a.bs[3] = (int16_t)(bw.y >> 16);
+        a.d0 = L.d[ch >> 2];
     } else {
-        a.d = L.d[P >> 1];
+        a.a2 = *(const i32x4*)(L.lo + 16 * ch + 2 * step);
+        a.a3 = *(const i32x4*)(L.lo + 16 * ch + 3 * step);
+        const float2 dd = *(const float2*)(L.d + 2 * ch);
+        a.d0 = dd.x;
+        a.d1 = dd.y;
     }
     return a;
 }
 
-// Exact integer dot of one piece, combined in fp32 as ggml's per-block formula.
+// ggml_vec_dot_<T>_q8_K restricted to one 64-weight chunk; exact int32 sums, fp32
+// combine exactly as ggml's per-block formula (d_w*d_a*isum - dmin_w*d_a*imin).
 template <int T>
-__device__ __forceinline__ float dot_piece(const Raw& r, const Act& a, int P) {
+__device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, int ch) {
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
-        const int c = (P & 7) >> 1;
+        const int c = ch & 3;
         int sc0, m0, sc1, m1;
         scale_min(2 * c, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
         scale_min(2 * c + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
         int lo = 0, hi = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint32_t l4 = r.q[k] & M4, h4 = (r.q[k] >> 4) & M4;
-            if constexpr (T == T_Q5_K) {
-                l4 |= spread4((r.qh.x >> (4 * k)) & 0xFu) << 4;
-                h4 |= spread4((r.qh.x >> (16 + 4 * k)) & 0xFu) << 4;
+        for (int k = 0; k < 2; ++k) {
+            const u32x4 q = k ? r.q1 : r.q0;
+            const i32x4 al = k ? a.a1 : a.a0, ah = k ? a.a3 : a.a2;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                uint32_t l4 = q[m] & M4, h4 = (q[m] >> 4) & M4;
+                if constexpr (T == T_Q5_K) {
+                    l4 |= spread4((r.qh.x >> (16 * k + 4 * m)) & 0xFu) << 4;
+                    h4 |= spread4((r.qh.y >> (16 * k + 4 * m)) & 0xFu) << 4;
+                }
+                lo = dot4(l4, al[m], lo);
+                hi = dot4(h4, ah[m], hi);
             }
-            lo = dot4(l4, a.lo[k], lo);
-            hi = dot4(h4, a.hi[k], hi);
         }
         const int isum = sc0 * lo + sc1 * hi;
-        const int imin = m0 * a.bs_lo + m1 * a.bs_hi;
+        const int imin = m0 * (a.bs[0] + a.bs[1]) + m1 * (a.bs[2] + a.bs[3]);
         const float d = h2f(r.hdr.x), dmin = h2f(r.hdr.x >> 16);
-        return (d * a.d) * (float)isum - (dmin * a.d) * (float)imin;
+        return (d * a.d0) * (float)isum - (dmin * a.d0) * (float)imin;
     } else if constexpr (T == T_Q6_K) {
-        int lo = 0, hi = 0;
+        int dm[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t ulo = (r.q[k] & M4) | (((r.qh.x >> (2 * k)) & M2) << 4);
-            const uint32_t uhi = ((r.q[k] >> 4) & M4) | (((r.qh.y >> (2 * k)) & M2) << 4);
-            lo = dot4(ulo, a.lo[k], lo);
-            hi = dot4(uhi, a.hi[k], hi);
+        for (int k = 0; k < 2; ++k) {
+            const u32x4 q = k ? r.q1 : r.q0;
+            const i32x4 al = k ? a.a1 : a.a0, ah = k ? a.a3 : a.a2;
+            const uint32_t hl = r.hdr[k], hh = r.hdr[2 + k];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t ulo = (q[m] & M4) | (((hl >> (2 * m)) & M2) << 4);
+                const uint32_t uhi = ((q[m] >> 4) & M4) | (((hh >> (2 * m)) & M2) << 4);
+                dm[k] = dot4(ulo, al[m], dm[k]);
+                dm[2 + k] = dot4(uhi, ah[m], dm[2 + k]);
+            }
         }
-        const int half = P & 1;
-        const int sc0 = (int8_t)(r.e0 >> (8 * half)), sc1 = (int8_t)(r.e0 >> (8 * (2 + half)));
-        const int isum = sc0 * (lo - 32 * a.bs_lo) + sc1 * (hi - 32 * a.bs_hi);
-        return (h2f(r.e1) * a.d) * (float)isum;
-    } else {
-        int s = 0;
+        int isum = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s = dot4(r.q[k], a.lo[k], s);
-        return (float)s * (h2f(r.e0) * a.d);
+        for (int m = 0; m < 4; ++m) isum += (int)(int8_t)(r.e0 >> (8 * m)) * (dm[m] - 32 * a.bs[m]);
+        return (h2f(r.e1) * a.d0) * (float)isum;
+    } else {
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            s0 = dot4(r.q0[m], a.a0[m], s0);
+            s0 = dot4(r.q1[m], a.a1[m], s0);
+            s1 = dot4(r.q2[m], a.a2[m], s1);
+            s1 = dot4(r.q3[m], a.a3[m], s1);
+        }
+        return (float)s0 * (h2f(r.e0) * a.d0) + (float)s1 * (h2f(r.e0 >> 16) * a.d1);
     }
 }
 
@@ -388,13 +431,25 @@ template <int T>
 struct PairRaw {
     Raw a, b;
 };
+template <int T>
+struct PairRows {
+    RowPtr a, b;
+};
 
 template <int T>
-__device__ __forceinline__ PairRaw<T> load_item(const PairRef& r, int P, int npr, int nbr) {
+__device__ __forceinline__ PairRows<T> pair_rows(const PairRef& r, int cols) {
+    PairRows<T> pr;
+    pr.a = row_ptr<T>(r.sa, r.ra, cols);
+    pr.b = row_ptr<T>(r.sb, r.vb ? r.rb : r.ra, cols);
+    return pr;
+}
+
+template <int T>
+__device__ __forceinline__ PairRaw<T> load_item(const PairRows<T>& pr, bool vb, int ch, int nch) {
     PairRaw<T> w;
-    if (P < npr) {
-        w.a = load_piece<T>(r.sa, r.ra, P, nbr, npr);
-        if (r.vb) w.b = load_piece<T>(r.sb, r.rb, P, nbr, npr);
+    if (ch < nch) {
+        w.a = load_chunk<T>(pr.a, ch, nch);
+        if (vb) w.b = load_chunk<T>(pr.b, ch, nch);
     }
     return w;
 }
@@ -475,11 +530,12 @@ __device__ __forceinline__ void epilogue(const MVArgs& A, const PairRef& r, int 
 // Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs).
 template <int ACT, int T>
 __device__ __forceinline__ float generic_row(const Seg& s, int row, int cols, const Lds& L) {
-    const int npr = cols / piece_elems<T>(), nbr = (T == T_Q8_0) ? (cols >> 5) : (cols >> 8);
+    const int nch = cols >> 6;
+    const RowPtr rp = row_ptr<T>(s, row, cols);
     float acc = 0.f;
-    for (int P = threadIdx.x & 63; P < npr; P += 64) {
-        const Raw w = load_piece<T>(s, row, P, nbr, npr);
-        acc += dot_piece<T>(w, load_act<ACT>(L, P), P);
+    for (int ch = threadIdx.x & 63; ch < nch; ch += 64) {
+        const Raw w = load_chunk<T>(rp, ch, nch);
+        acc += dot_chunk<T>(w, load_act<ACT>(L, ch, nch), ch);
     }
     return acc;
 }
@@ -504,20 +560,23 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int G = gridDim.x * 4;
-    const int npr = A.cols / piece_elems<T>(), NJ = (npr + 63) >> 6;
-    const int nbr = (T == T_Q8_0) ? (A.cols >> 5) : (A.cols >> 8);
+    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
 
     int p = blockIdx.x * 4 + wave;
     PairRef r;
+    PairRows<T> rows;
     bool pipe = false;
     PairRaw<T> cur;
     if (p < A.npairs) {
         r = pair_ref<EPI>(A, p);
         pipe = r.type == T;
-        if (pipe) cur = load_item<T>(r, lane, npr, nbr);  // issued before the prologue
+        if (pipe) {
+            rows = pair_rows<T>(r, A.cols);
+            cur = load_item<T>(rows, r.vb, lane, nch);  // issued before the prologue
+        }
     }
     mv_prologue<ACT, NORM>(A, L);
     __syncthreads();
@@ -529,19 +588,23 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             // next work item: (p, j+1) or (p+G, 0)
             int pn = p, jn = j + 1;
             PairRef rn = r;
+            PairRows<T> rowsn = rows;
             if (jn == NJ) {
                 jn = 0;
                 pn = p + G;
-                if (pn < A.npairs) rn = pair_ref<EPI>(A, pn);
+                if (pn < A.npairs) {
+                    rn = pair_ref<EPI>(A, pn);
+                    rowsn = pair_rows<T>(rn, A.cols);
+                }
             }
             const bool has_next = pn < A.npairs && rn.type == T;
             PairRaw<T> nxt;
-            if (has_next) nxt = load_item<T>(rn, lane + 64 * jn, npr, nbr);
-            const int P = lane + 64 * j;
-            if (P < npr) {
-                const Act act = load_act<ACT>(L, P);
-                acc_a += dot_piece<T>(cur.a, act, P);
-                if (r.vb) acc_b += dot_piece<T>(cur.b, act, P);
+            if (has_next) nxt = load_item<T>(rowsn, rn.vb, lane + 64 * jn, nch);
+            const int ch = lane + 64 * j;
+            if (ch < nch) {
+                const Act act = load_act<ACT>(L, ch, nch);
+                acc_a += dot_chunk<T>(cur.a, act, ch);
+                if (r.vb) acc_b += dot_chunk<T>(cur.b, act, ch);
             }
             if (j == NJ - 1) {
                 epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
@@ -555,6 +618,7 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             p = pn;
             j = jn;
             r = rn;
+            rows = rowsn;
         }
     }
     // remaining pairs of other types (or all pairs if the first was not of type T)
@@ -580,22 +644,21 @@ __global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* ou
     else mv_prologue<ACT, false>(A, L);
     __syncthreads();
     const int cols = A.cols;
+    const int nch = cols >> 6;
     for (int e = threadIdx.x; e < cols; e += blockDim.x) {
+        const int ch = e >> 6, t = e & 63;
         if (ACT == 0) {
-            const int b = e >> 8, w = e & 255, c = w >> 6, t = w & 63, half = (t & 31) >> 4;
-            const int P = 8 * b + 2 * c + half;
-            const int8_t qv = (int8_t)((t < 32 ? L.lo : L.hi)[16 * P + (t & 15)]);
-            out[(size_t)b * 292 + 4 + w] = (uint8_t)qv;
+            const int k = (t & 31) >> 4;
+            const int8_t qv = (int8_t)((t < 32 ? L.lo : L.hi)[16 * (k * nch + ch) + (t & 15)]);
+            out[(size_t)(e >> 8) * 292 + 4 + (e & 255)] = (uint8_t)qv;
         } else {
-            out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = L.lo[e];
+            out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = L.lo[16 * ((t >> 4) * nch + ch) + (t & 15)];
         }
     }
     if (ACT == 0) {
         for (int b = threadIdx.x; b < cols / 256; b += blockDim.x) *(float*)(out + (size_t)b * 292) = L.d[b];
-        for (int sb = threadIdx.x; sb < cols / 16; sb += blockDim.x) {
-            const int b = sb >> 4, s = sb & 15, P = 8 * b + 2 * (s >> 2) + (s & 1);
-            *(int16_t*)(out + (size_t)b * 292 + 260 + 2 * s) = L.bs[2 * P + ((s & 2) ? 1 : 0)];
-        }
+        for (int sb = threadIdx.x; sb < cols / 16; sb += blockDim.x)
+            *(int16_t*)(out + (size_t)(sb >> 4) * 292 + 260 + 2 * (sb & 15)) = L.bs[sb];
     } else {
         for (int b = threadIdx.x; b < cols / 32; b += blockDim.x) *(uint16_t*)(out + (size_t)b * 34) = f2h(L.d[b]);
     }
@@ -798,30 +861,30 @@ __device__ float dequant_elem(const Seg& w, int row, int e, int cols) {
         case T_Q4_K:
         case T_Q5_K:
         case T_Q6_K: {
-            const int nbr = cols / 256, npr = cols / 32;
-            const int b = e / 256, i = e & 255, c = i >> 6, t = i & 63, hi = t >= 32, l = t & 31, half = l >> 4;
-            const int P = 8 * b + 2 * c + half, k = l & 15;                 // piece and byte within it
-            const size_t gp = (size_t)row * npr + P, gb = (size_t)row * nbr + b;
-            const uint8_t qb = w.a[gp * 16 + k];
+            const int nch = cols >> 6, nbr = cols >> 8;
+            const int ch = e >> 6, t = e & 63, hi = t >= 32, l = t & 31, k = l >> 4, i = l & 15;
+            const size_t gb = (size_t)row * nbr + (e >> 8);
+            const uint8_t qb = w.a[(size_t)row * nch * 32 + (size_t)(k * nch + ch) * 16 + i];
             int q = hi ? (qb >> 4) : (qb & 0xF);
-            if (w.type == T_Q6_K) {
-                const uint8_t hb = w.h[gp * 8 + (hi ? 4 : 0) + (k & 3)];
-                q |= ((hb >> (2 * (k >> 2))) & 3) << 4;
+            if (w.type == T_Q6_K) {  // H dword (2*hi + k), byte i&3, bits 2*(i>>2)
+                const uint8_t hb = w.h[((size_t)row * nch + ch) * 16 + (2 * hi + k) * 4 + (i & 3)];
+                q |= ((hb >> (2 * (i >> 2))) & 3) << 4;
                 const float d = h2f(*(const uint16_t*)(w.d + gb * 2));
-                const int sc = (int8_t)w.s[gb * 16 + (i >> 4)];
+                const int sc = (int8_t)w.s[gb * 16 + ((e & 255) >> 4)];
                 return d * (float)sc * (float)(q - 32);
             }
             const uint32_t* s32 = (const uint32_t*)(w.s + gb * 16);
             int sc, m;
-            scale_min(2 * c + hi, s32[1], s32[2], s32[3], sc, m);
-            if (w.type == T_Q5_K) q += ((ldw4(w.h + gp * 4) >> (16 * hi + k)) & 1) << 4;
+            scale_min(2 * (ch & 3) + hi, s32[1], s32[2], s32[3], sc, m);
+            if (w.type == T_Q5_K) q += ((ldw4(w.h + ((size_t)row * nch + ch) * 8 + 4 * hi) >> l) & 1) << 4;
             const float d = h2f(s32[0]), dmin = h2f(s32[0] >> 16);
             const float d1 = d * (float)sc, m1 = dmin * (float)m;
             return d1 * (float)q - m1;
         }
         case T_Q8_0: {
-            const size_t b = (size_t)row * (cols / 32) + e / 32;
-            return (float)(int8_t)w.a[b * 32 + (e & 31)] * h2f(*(const uint16_t*)(w.d + b * 2));
+            const int nch = cols >> 6, ch = e >> 6, t = e & 63;
+            const uint8_t qb = w.a[(size_t)row * nch * 64 + (size_t)((t >> 4) * nch + ch) * 16 + (t & 15)];
+            return (float)(int8_t)qb * h2f(*(const uint16_t*)(w.d + ((size_t)row * (cols / 32) + e / 32) * 2));
         }
         default: return 0.f;
     }
@@ -850,29 +913,34 @@ __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
 }
 
 // ----------------------------------------------------------------------------------
-// Load-time repack of GGUF blocks into the piece-planar layout (common.h).
-// One thread per (block, piece r in 0..7).
+// Load-time repack of GGUF blocks into the chunk-planar layout (common.h).
+// One thread per (block, chunk c in 0..3); nbr = blocks per row.
 // ----------------------------------------------------------------------------------
-__global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H, uint8_t* S, uint8_t* Dp, int64_t nblk) {
+__global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H, uint8_t* S, uint8_t* Dp, int64_t nblk,
+                            int nbr) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t b = gid >> 3;
-    const int r = (int)(gid & 7), c = r >> 1, half = r & 1;
+    const int64_t b = gid >> 2;
+    const int c = (int)(gid & 3);
     if (b >= nblk) return;
+    const int64_t row = b / nbr, bi = b % nbr, nch = (int64_t)nbr * 4, ch = bi * 4 + c;
+    uint8_t* arow = A + row * nch * 32;
     if (type == T_Q4_K || type == T_Q5_K) {
         const int bb = type == T_Q4_K ? 144 : 176;
         const uint8_t* x = raw + b * bb;
         const uint8_t* qs = x + (type == T_Q4_K ? 16 : 48);
-        for (int i = 0; i < 16; ++i) A[(b * 8 + r) * 16 + i] = qs[16 * r + i];
-        if (r == 0)
+        for (int k = 0; k < 2; ++k)
+            for (int i = 0; i < 16; ++i) arow[(k * nch + ch) * 16 + i] = qs[32 * c + 16 * k + i];
+        if (c == 0)
             for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[i];
-        if (type == T_Q5_K) {
+        if (type == T_Q5_K) {  // bit l of the lo word: qh[l] bit 2c; hi word: bit 2c+1
             const uint8_t* qh = x + 16;
-            uint32_t bits = 0;
-            for (int i = 0; i < 16; ++i) {
-                bits |= (uint32_t)((qh[16 * half + i] >> (2 * c)) & 1) << i;
-                bits |= (uint32_t)((qh[16 * half + i] >> (2 * c + 1)) & 1) << (16 + i);
+            uint32_t lo = 0, hi = 0;
+            for (int l = 0; l < 32; ++l) {
+                lo |= (uint32_t)((qh[l] >> (2 * c)) & 1) << l;
+                hi |= (uint32_t)((qh[l] >> (2 * c + 1)) & 1) << l;
             }
-            for (int k = 0; k < 4; ++k) H[(b * 8 + r) * 4 + k] = (uint8_t)(bits >> (8 * k));
+            uint8_t* h = H + (row * nch + ch) * 8;
+            for (int k = 0; k < 4; ++k) { h[k] = (uint8_t)(lo >> (8 * k)); h[4 + k] = (uint8_t)(hi >> (8 * k)); }
         }
     } else {  // Q6_K
         const uint8_t* x = raw + b * 210;
@@ -885,34 +953,37 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
             const int hi = (qh[32 * n + l] >> (2 * quad)) & 3;
             return lo | (hi << 4);
         };
-        const int wlo = 64 * c + 16 * half, whi = wlo + 32;
-        uint8_t* o = A + (b * 8 + r) * 16;
-        for (int i = 0; i < 16; ++i) o[i] = (uint8_t)((u6(wlo + i) & 15) | ((u6(whi + i) & 15) << 4));
-        uint8_t* h = H + (b * 8 + r) * 8;
-        for (int j = 0; j < 4; ++j) {  // byte j bits [2m,2m+1] = high2 of weight 4m+j
-            uint8_t vlo = 0, vhi = 0;
-            for (int m = 0; m < 4; ++m) {
-                vlo |= (uint8_t)((u6(wlo + 4 * m + j) >> 4) << (2 * m));
-                vhi |= (uint8_t)((u6(whi + 4 * m + j) >> 4) << (2 * m));
+        for (int k = 0; k < 2; ++k)
+            for (int i = 0; i < 16; ++i) {
+                const int t = 16 * k + i;
+                arow[(k * nch + ch) * 16 + i] = (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
             }
-            h[j] = vlo;
-            h[4 + j] = vhi;
-        }
-        if (r == 0) {
-            for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[192 + i];
-            Dp[b * 2] = x[208];
-            Dp[b * 2 + 1] = x[209];
-        }
+        // H dword g = 2*hi + k: byte j bits [2m, 2m+1] = high2 of chunk weight 32*hi + 16k + 4m + j
+        uint8_t* h = H + (row * nch + ch) * 16;
+        for (int g = 0; g < 4; ++g)
+            for (int j = 0; j < 4; ++j) {
+                uint8_t v = 0;
+                for (int m = 0; m < 4; ++m) v |= (uint8_t)((u6(64 * c + 32 * (g >> 1) + 16 * (g & 1) + 4 * m + j) >> 4) << (2 * m));
+                h[4 * g + j] = v;
+            }
+        for (int i = 0; i < 4; ++i) S[b * 16 + 4 * c + i] = x[192 + 4 * c + i];
+        if (c == 0) { Dp[b * 2] = x[208]; Dp[b * 2 + 1] = x[209]; }
     }
 }
 
-__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nblk) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nblk) return;
-    const uint8_t* x = raw + b * 34;
-    for (int i = 0; i < 32; ++i) A[b * 32 + i] = x[2 + i];
-    Dp[b * 2] = x[0];
-    Dp[b * 2 + 1] = x[1];
+// Q8_0: one thread per 64-weight chunk (two blocks)
+__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nchunk, int nch_row) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nchunk) return;
+    const int64_t row = g / nch_row, ch = g % nch_row;
+    uint8_t* arow = A + row * nch_row * 64;
+    for (int half = 0; half < 2; ++half) {
+        const uint8_t* x = raw + (g * 2 + half) * 34;
+        for (int k = 0; k < 2; ++k)
+            for (int i = 0; i < 16; ++i) arow[((2 * half + k) * nch_row + ch) * 16 + i] = x[2 + 16 * k + i];
+        Dp[(g * 2 + half) * 2] = x[0];
+        Dp[(g * 2 + half) * 2 + 1] = x[1];
+    }
 }
 
 // Streaming-read reference (achievable HBM rate for a perfectly coalesced 16-B/lane
@@ -1028,14 +1099,17 @@ hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream
 }
 
 hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* sp, uint8_t* d, int64_t nblk,
-                         hipStream_t s) {
+                         int64_t cols, hipStream_t s) {
     if (nblk <= 0) return hipSuccess;
+    if (cols % 256) return hipErrorInvalidValue;
     if (type == T_Q4_K || type == T_Q5_K || type == T_Q6_K) {
-        const int64_t thr = nblk * 8;
+        const int64_t thr = nblk * 4;
         hipLaunchKernelGGL(k_repack_kq, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, type, (const uint8_t*)raw, a,
-                           h, sp, d, nblk);
+                           h, sp, d, nblk, (int)(cols / 256));
     } else if (type == T_Q8_0) {
-        hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d, nblk);
+        const int64_t nchunk = nblk / 2;
+        hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nchunk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d,
+                           nchunk, (int)(cols / 64));
     } else {
         return hipErrorInvalidValue;
     }

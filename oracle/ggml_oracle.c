@@ -345,13 +345,12 @@ static float vd_f32(int n, const float* x, const float* y) {
 
 /* ---------------------------------------------------------------------------
  * Device-order dot (or_set_dot_order(1)): the SAME exact integer block math as the
- * generic functions above, split into 32-weight PIECES (the HIP kernel's unit; piece r
- * of a K-quant block = the 16 weights 64c+16h+i of scale group 2c and the 16 weights
- * 32 positions later, c = r/2, h = r%2; a Q8_0 piece = 16 weights), with the fp32
- * association the kernel uses: piece P contributes
+ * generic functions above, split into 64-weight CHUNKS (the HIP kernel's unit: quarter
+ * c of a K-quant block, or two Q8_0 blocks), with the fp32 association the kernel uses
+ * (DESIGN.md §Numerics): chunk ci contributes
  *   K-quants: (d*dA)*(float)isum - (dmin*dA)*(float)imin      (Q6_K: no min term)
- *   Q8_0    : (float)isum * (d*dA)
- * lane L = P % 64 accumulates its pieces in order, then a 64-lane xor butterfly.
+ *   Q8_0    : (float)s0*(d0*dA0) + (float)s1*(d1*dA1)
+ * lane L = ci % 64 accumulates its chunks in order, then a 64-lane xor butterfly.
  * Integer sums are ggml's exactly; only fp32 rounding order differs from the
  * generic loop (whose own order differs again from every SIMD variant upstream).
  * --------------------------------------------------------------------------- */
@@ -367,15 +366,17 @@ static int q6_u6(const block_q6_K* x, int w) {
     return lo | (hi << 4);
 }
 
-static float piece_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int r) {
-    const int c = r >> 1, half = r & 1, wlo = 64 * c + 16 * half, whi = wlo + 32;
-    const int8_t* a = y->qs;
-    const int bl = y->bsums[4 * c + half], bh = y->bsums[4 * c + 2 + half];
+static float chunk_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int c) {
+    const int8_t* a = y->qs + 64 * c;
+    const int16_t* bs = y->bsums + 4 * c;
     if (wtype == OR_Q6_K) {
         const block_q6_K* x = (const block_q6_K*)blk;
-        int lo = 0, hi = 0;
-        for (int i = 0; i < 16; ++i) { lo += q6_u6(x, wlo + i) * a[wlo + i]; hi += q6_u6(x, whi + i) * a[whi + i]; }
-        const int isum = x->scales[4 * c + half] * (lo - 32 * bl) + x->scales[4 * c + 2 + half] * (hi - 32 * bh);
+        int isum = 0;
+        for (int m = 0; m < 4; ++m) {
+            int dot = 0;
+            for (int t = 0; t < 16; ++t) dot += q6_u6(x, 64 * c + 16 * m + t) * a[16 * m + t];
+            isum += x->scales[4 * c + m] * (dot - 32 * bs[m]);
+        }
         return (llmi_h2f(x->d) * y->d) * (float)isum;
     }
     const uint8_t* scales; const uint8_t* qs; const uint8_t* qh = NULL; uint16_t d16, m16;
@@ -385,15 +386,14 @@ static float piece_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int r)
     get_scale_min_k4(2 * c, scales, &sc0, &m0);
     get_scale_min_k4(2 * c + 1, scales, &sc1, &m1);
     int lo = 0, hi = 0;
-    for (int i = 0; i < 16; ++i) {
-        const int l = 16 * half + i;                 /* native qs/qh byte within chunk c */
-        int ql = qs[32 * c + l] & 0xF, qq = qs[32 * c + l] >> 4;
-        if (qh) { ql += ((qh[l] >> (2 * c)) & 1) << 4; qq += ((qh[l] >> (2 * c + 1)) & 1) << 4; }
-        lo += ql * a[wlo + i];
-        hi += qq * a[whi + i];
+    for (int t = 0; t < 32; ++t) {
+        int ql = qs[32 * c + t] & 0xF, qq = qs[32 * c + t] >> 4;
+        if (qh) { ql += ((qh[t] >> (2 * c)) & 1) << 4; qq += ((qh[t] >> (2 * c + 1)) & 1) << 4; }
+        lo += ql * a[t];
+        hi += qq * a[32 + t];
     }
     const int isum = sc0 * lo + sc1 * hi;
-    const int imin = m0 * bl + m1 * bh;
+    const int imin = m0 * (bs[0] + bs[1]) + m1 * (bs[2] + bs[3]);
     const float dA = y->d;
     return (llmi_h2f(d16) * dA) * (float)isum - (llmi_h2f(m16) * dA) * (float)imin;
 }
@@ -401,21 +401,20 @@ static float piece_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int r)
 static float vd_device_order(int wtype, int n, const void* w, const void* act) {
     float acc[64];
     for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
-    const int np = wtype == OR_Q8_0 ? n / 16 : n / 32;
-    for (int P = 0; P < np; ++P) {
+    const int nch = n / 64;
+    for (int ci = 0; ci < nch; ++ci) {
         float v;
         if (wtype == OR_Q8_0) {
-            const block_q8_0* x = (const block_q8_0*)w + P / 2;
-            const block_q8_0* y = (const block_q8_0*)act + P / 2;
-            const int h = 16 * (P & 1);
-            int s0 = 0;
-            for (int j = 0; j < 16; ++j) s0 += x->qs[h + j] * y->qs[h + j];
-            v = (float)s0 * (llmi_h2f(x->d) * llmi_h2f(y->d));
+            const block_q8_0* x = (const block_q8_0*)w + 2 * ci;
+            const block_q8_0* y = (const block_q8_0*)act + 2 * ci;
+            int s0 = 0, s1 = 0;
+            for (int j = 0; j < 32; ++j) { s0 += x[0].qs[j] * y[0].qs[j]; s1 += x[1].qs[j] * y[1].qs[j]; }
+            v = (float)s0 * (llmi_h2f(x[0].d) * llmi_h2f(y[0].d)) + (float)s1 * (llmi_h2f(x[1].d) * llmi_h2f(y[1].d));
         } else {
             const size_t bb = or_type_size(wtype);
-            v = piece_kq(wtype, (const uint8_t*)w + (size_t)(P / 8) * bb, (const block_q8_K*)act + P / 8, P % 8);
+            v = chunk_kq(wtype, (const uint8_t*)w + (size_t)(ci / 4) * bb, (const block_q8_K*)act + ci / 4, ci % 4);
         }
-        acc[P % 64] = acc[P % 64] + v;
+        acc[ci % 64] = acc[ci % 64] + v;
     }
     for (int o = 32; o >= 1; o >>= 1)
         for (int l = 0; l < o; ++l) acc[l] = acc[l] + acc[l + o];

@@ -13,6 +13,12 @@ P = lambda t: C.c_void_p(t.data_ptr())
 res = {}
 shapes = [(Q4_K, 28672, 4096), (Q4_K, 4096, 14336), (Q6_K, 4096, 14336), (Q6_K, 128256, 4096), (Q4_K, 6144, 4096),
           (Q5_K, 14336, 4096), (Q8_0, 5632, 2048)]
+if os.environ.get("MV_SHAPES"):  # e.g. "12:28672x4096,14:128256x4096"
+    shapes = []
+    for tok in os.environ["MV_SHAPES"].split(","):
+        t, rc = tok.split(":"); r, c = rc.split("x")
+        shapes.append((int(t), int(r), int(c)))
+REPS = int(os.environ.get("MV_REPS", "200"))
 rng = np.random.default_rng(0)
 for qt, rows, cols in shapes:
     lb = L.llmi_device_layout_bytes(qt, rows, cols)
@@ -24,9 +30,9 @@ for qt, rows, cols in shapes:
         assert L.llmi_repack(qt, P(raw), C.c_void_p(w.data_ptr() + stride * k), rows, cols) == 0
     x = torch.randn(cols, device="cuda"); y = torch.empty(rows, device="cuda")
     torch.cuda.synchronize()
-    us = L.llmi_bench_matvec(qt, P(w), n, rows, cols, P(x), P(y), 200)
+    us = L.llmi_bench_matvec(qt, P(w), n, rows, cols, P(x), P(y), REPS)
     alg = raw.numel()
-    us_s = L.llmi_bench_stream(P(w), n, stride, alg, 200, 2048)
+    us_s = L.llmi_bench_stream(P(w), n, stride, alg, REPS, 2048)
     key = f"{qt}:{rows}x{cols}"
     res[key] = {"us": us, "GBps": alg / us / 1e3, "stream_us": us_s, "stream_GBps": alg / us_s / 1e3}
     print(key, json.dumps(res[key]), flush=True)
