@@ -56,14 +56,67 @@ __device__ __forceinline__ uint32_t ldw4(const uint8_t* p) { return *(const uint
 __device__ __forceinline__ int dot4(uint32_t a, int b, int c) {
     return __builtin_amdgcn_sdot4((int)a, b, c, false);
 }
+// ---- cross-lane exchange without LDS round trips (VALU latency): DPP within 16-lane
+// rows, v_permlane16/32_swap across rows / halves (gfx950).  xor_partner<o>(v) returns
+// v of lane L^o for o in {1,2,4,8,16,32}; for o = 4 / 8 the DPP row_half_mirror /
+// row_mirror partner (lane 7-i / 15-i) is used, which equals lane L^4 / L^8 whenever
+// the value is already uniform over aligned 4- / 8-lane groups, i.e. inside a
+// butterfly after the xor-1/xor-2 (and xor-4) steps.  Every butterfly below runs the
+// steps in the order 1, 2, 4, 8, 16, 32; the oracle's device order models exactly that.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int O>
+__device__ __forceinline__ uint32_t xor_partner_u32(uint32_t v) {
+    if constexpr (O == 1) return dpp_u32<0xB1>(v);        // quad_perm [1,0,3,2]
+    else if constexpr (O == 2) return dpp_u32<0x4E>(v);   // quad_perm [2,3,0,1]
+    else if constexpr (O == 4) return dpp_u32<0x141>(v);  // row_half_mirror
+    else if constexpr (O == 8) return dpp_u32<0x140>(v);  // row_mirror
+    else if constexpr (O == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return ((threadIdx.x >> 4) & 1) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return ((threadIdx.x >> 5) & 1) ? r[0] : r[1];
+    }
+}
+template <int O>
+__device__ __forceinline__ float xor_partner(float v) { return __uint_as_float(xor_partner_u32<O>(__float_as_uint(v))); }
+template <int O>
+__device__ __forceinline__ int xor_partner_i(int v) { return (int)xor_partner_u32<O>((uint32_t)v); }
+template <int O>
+__device__ __forceinline__ double xor_partner_d(double v) {
+    const unsigned long long u = __double_as_longlong(v);
+    const uint32_t lo = xor_partner_u32<O>((uint32_t)u), hi = xor_partner_u32<O>((uint32_t)(u >> 32));
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+// 64-lane sum, all lanes receive the result (butterfly 1,2,4,8,16,32)
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v += xor_partner<1>(v);
+    v += xor_partner<2>(v);
+    v += xor_partner<4>(v);
+    v += xor_partner<8>(v);
+    v += xor_partner<16>(v);
+    v += xor_partner<32>(v);
     return v;
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v += xor_partner_d<1>(v);
+    v += xor_partner_d<2>(v);
+    v += xor_partner_d<4>(v);
+    v += xor_partner_d<8>(v);
+    v += xor_partner_d<16>(v);
+    v += xor_partner_d<32>(v);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, xor_partner<1>(v));
+    v = fmaxf(v, xor_partner<2>(v));
+    v = fmaxf(v, xor_partner<4>(v));
+    v = fmaxf(v, xor_partner<8>(v));
+    v = fmaxf(v, xor_partner<16>(v));
+    v = fmaxf(v, xor_partner<32>(v));
     return v;
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -125,100 +178,159 @@ __device__ double block_sum_d(double v, double* red) {
 //             bsums per 16; d = 1/iscale; all-zero block -> d = 0, q = 0 (quantize_row_q8_K_ref)
 //   q8_0:     d = amax/127 (stored f16), q = roundf(y * (d ? 1/d : 0))   (quantize_row_q8_0_ref)
 // ----------------------------------------------------------------------------------
+// Quantize one 16-element sub-block (values already normed) into the LDS image.
+template <int ACT>
+__device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const float (&v)[16]) {
+    const int tid = threadIdx.x;
+    int q[16];
+    uint8_t* dst;
+    if constexpr (ACT == 0) {
+        float am = 0.f, mv = 0.f;
+        int gi = sb * 16;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float ax = fabsf(v[j]);
+            if (ax > am) { am = ax; mv = v[j]; gi = sb * 16 + j; }
+        }
+        // 16-lane (one Q8_K block) arg-max of |y|, first index wins; each step compares
+        // with the (uniform-so-far) partner group, so mirror partners are exact
+#define LLMI_AMAX_STEP(O)                                                                  \
+        {                                                                                  \
+            const float am2 = xor_partner<O>(am), mv2 = xor_partner<O>(mv);                \
+            const int gi2 = xor_partner_i<O>(gi);                                          \
+            if (am2 > am || (am2 == am && gi2 < gi)) { am = am2; mv = mv2; gi = gi2; }     \
+        }
+        LLMI_AMAX_STEP(1) LLMI_AMAX_STEP(2) LLMI_AMAX_STEP(4) LLMI_AMAX_STEP(8)
+#undef LLMI_AMAX_STEP
+        float dval = 0.f;
+        int bsum = 0;
+        if (am == 0.f) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) q[j] = 0;
+        } else {
+            const float iscale = -127.f / mv;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int t = llmi_nearest_int(iscale * v[j]);
+                q[j] = t < 127 ? t : 127;
+                bsum += q[j];
+            }
+            dval = 1.0f / iscale;
+        }
+        // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: lo part k=qq (qq<2), hi part k=qq-2
+        const int nch = cols >> 6, ch = sb >> 2, qq = sb & 3;
+        const int hoff = qq < 2 ? 0 : (int)(L.hi - L.lo);  // (no pointer select: it spills to scratch)
+        dst = L.lo + hoff + 16 * ((qq & 1) * nch + ch);
+        L.bs[sb] = (int16_t)bsum;
+        if ((tid & 15) == 0) L.d[sb >> 4] = dval;
+    } else {
+        float am = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+        am = fmaxf(am, xor_partner<1>(am));
+        const float d = am / 127;
+        const float id = d != 0.f ? 1.0f / d : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
+        if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
+        const int nch = cols >> 6;
+        dst = L.lo + 16 * ((sb & 3) * nch + (sb >> 2));
+    }
+    u32x4 pk;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
+                ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
+    *(u32x4*)dst = pk;
+}
+
+// Prologue in two halves so a caller can put the weight prefetch between them:
+// issue() loads this thread's sub-blocks of x (and norm w) into registers (up to
+// NPRE of them: 4 without norm = cols <= 16384, 2 with norm = cols <= 8192);
+// finish() computes the norm, quantizes and writes LDS.  Sub-blocks beyond NPRE are
+// loaded inside finish() (correct, just not overlapped).
+template <bool NORM>
+struct ProRegs {
+    static constexpr int NPRE = NORM ? 2 : 4;
+    float x[NPRE][16];
+    float w[NORM ? NPRE : 1][16];
+};
+template <bool NORM>
+__device__ __forceinline__ void mv_prologue_issue(const MVArgs& A, ProRegs<NORM>& R) {
+    const int nsub = A.cols / 16;
+#pragma unroll
+    for (int i = 0; i < ProRegs<NORM>::NPRE; ++i) {
+        const int sb = threadIdx.x + i * kMVThreads;
+        if (sb < nsub) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
+                R.x[i][4 * k + 0] = xv.x; R.x[i][4 * k + 1] = xv.y; R.x[i][4 * k + 2] = xv.z; R.x[i][4 * k + 3] = xv.w;
+                if constexpr (NORM) {
+                    const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                    R.w[i][4 * k + 0] = wv.x; R.w[i][4 * k + 1] = wv.y; R.w[i][4 * k + 2] = wv.z; R.w[i][4 * k + 3] = wv.w;
+                }
+            }
+        }
+    }
+}
+template <bool NORM>
+__device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM>& R, int i, int sb, float (&v)[16],
+                                         float (&w)[16]) {
+    if (i < ProRegs<NORM>::NPRE) {
+#pragma unroll
+        for (int ii = 0; ii < ProRegs<NORM>::NPRE; ++ii)
+            if (ii == i) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    v[j] = R.x[ii][j];
+                    if constexpr (NORM) w[j] = R.w[ii][j];
+                }
+            }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
+            v[4 * k + 0] = xv.x; v[4 * k + 1] = xv.y; v[4 * k + 2] = xv.z; v[4 * k + 3] = xv.w;
+            if constexpr (NORM) {
+                const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                w[4 * k + 0] = wv.x; w[4 * k + 1] = wv.y; w[4 * k + 2] = wv.z; w[4 * k + 3] = wv.w;
+            }
+        }
+    }
+}
 template <int ACT, bool NORM>
-__device__ void mv_prologue(const MVArgs& A, const Lds& L) {
+__device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM>& R) {
     const int tid = threadIdx.x, cols = A.cols;
     const int nsub = cols / 16;
     float scale = 1.0f;
     if constexpr (NORM) {
         double s = 0.0;
-        for (int sb = tid; sb < nsub; sb += kMVThreads) {
+        for (int i = 0, sb = tid; sb < nsub; ++i, sb += kMVThreads) {
+            float v[16], w[16];
+            load_sub<NORM>(A, R, i, sb, v, w);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 v = *(const float4*)(A.x + sb * 16 + 4 * k);
-                s += (double)(v.x * v.x);
-                s += (double)(v.y * v.y);
-                s += (double)(v.z * v.z);
-                s += (double)(v.w * v.w);
-            }
+            for (int j = 0; j < 16; ++j) s += (double)(v[j] * v[j]);
         }
         s = block_sum_d(s, L.red);
         const float mean = (float)(s / (double)cols);
         scale = 1.0f / sqrtf(mean + A.eps);
     }
-    for (int sb = tid; sb < nsub; sb += kMVThreads) {
-        float v[16];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
-            v[4 * k + 0] = xv.x; v[4 * k + 1] = xv.y; v[4 * k + 2] = xv.z; v[4 * k + 3] = xv.w;
-        }
+    for (int i = 0, sb = tid; sb < nsub; ++i, sb += kMVThreads) {
+        float v[16], w[16];
+        load_sub<NORM>(A, R, i, sb, v, w);
         if constexpr (NORM) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
-                v[4 * k + 0] = (v[4 * k + 0] * scale) * wv.x;
-                v[4 * k + 1] = (v[4 * k + 1] * scale) * wv.y;
-                v[4 * k + 2] = (v[4 * k + 2] * scale) * wv.z;
-                v[4 * k + 3] = (v[4 * k + 3] * scale) * wv.w;
-            }
+            for (int j = 0; j < 16; ++j) v[j] = (v[j] * scale) * w[j];
         }
-        int q[16];
-        uint8_t* dst;
-        if constexpr (ACT == 0) {
-            float am = 0.f, mv = 0.f;
-            int gi = sb * 16;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const float ax = fabsf(v[j]);
-                if (ax > am) { am = ax; mv = v[j]; gi = sb * 16 + j; }
-            }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {  // 16-lane (one Q8_K block) arg-max, first index wins
-                const float am2 = __shfl_xor(am, o), mv2 = __shfl_xor(mv, o);
-                const int gi2 = __shfl_xor(gi, o);
-                if (am2 > am || (am2 == am && gi2 < gi)) { am = am2; mv = mv2; gi = gi2; }
-            }
-            float dval = 0.f;
-            int bsum = 0;
-            if (am == 0.f) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) q[j] = 0;
-            } else {
-                const float iscale = -127.f / mv;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int t = llmi_nearest_int(iscale * v[j]);
-                    q[j] = t < 127 ? t : 127;
-                    bsum += q[j];
-                }
-                dval = 1.0f / iscale;
-            }
-            // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: lo part k=qq (qq<2), hi part k=qq-2
-            const int nch = cols >> 6, ch = sb >> 2, qq = sb & 3;
-            dst = (qq < 2 ? L.lo : L.hi) + 16 * ((qq & 1) * nch + ch);
-            L.bs[sb] = (int16_t)bsum;
-            if ((tid & 15) == 0) L.d[sb >> 4] = dval;
-        } else {
-            float am = 0.f;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
-            am = fmaxf(am, __shfl_xor(am, 1));
-            const float d = am / 127;
-            const float id = d != 0.f ? 1.0f / d : 0.0f;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
-            if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
-            const int nch = cols >> 6;
-            dst = L.lo + 16 * ((sb & 3) * nch + (sb >> 2));
-        }
-        u32x4 pk;
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-            pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
-                    ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
-        *(u32x4*)dst = pk;
+        quant_sub<ACT>(L, cols, sb, v);
     }
+}
+template <int ACT, bool NORM>
+__device__ __forceinline__ void mv_prologue(const MVArgs& A, const Lds& L) {
+    ProRegs<NORM> R;
+    mv_prologue_issue<NORM>(A, R);
+    mv_prologue_finish<ACT, NORM>(A, L, R);
 }
 
 // ----------------------------------------------------------------------------------
@@ -226,16 +338,14 @@ __device__ void mv_prologue(const MVArgs& A, const Lds& L) {
 // ----------------------------------------------------------------------------------
 constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u, M1 = 0x01010101u;
 
-// upstream get_scale_min_k4 on the 12 scale bytes held as three words
+// upstream get_scale_min_k4 on the 12 scale bytes held as three words (branchless:
+// j varies per lane, so both forms are computed and selected)
 __device__ __forceinline__ void scale_min(int j, uint32_t s0, uint32_t s1, uint32_t s2, int& sc, int& m) {
     const int k = (j & 3) * 8;
     const uint32_t b0 = (s0 >> k) & 0xffu, b1 = (s1 >> k) & 0xffu, b2 = (s2 >> k) & 0xffu;
-    if (j < 4) {
-        sc = (int)(b0 & 63u); m = (int)(b1 & 63u);
-    } else {
-        sc = (int)((b2 & 0xFu) | ((b0 >> 6) << 4));
-        m = (int)((b2 >> 4) | ((b1 >> 6) << 4));
-    }
+    const uint32_t sc_hi = (b2 & 0xFu) | ((b0 >> 6) << 4), m_hi = (b2 >> 4) | ((b1 >> 6) << 4);
+    sc = (int)(j < 4 ? (b0 & 63u) : sc_hi);
+    m = (int)(j < 4 ? (b1 & 63u) : m_hi);
 }
 // 4 bits -> the low bit of 4 bytes
 __device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x00204081u) & M1; }
@@ -444,28 +554,25 @@ __device__ __forceinline__ PairRows<T> pair_rows(const PairRef& r, int cols) {
     return pr;
 }
 
+// Unconditional loads (the chunk index is clamped to a valid one; callers discard the
+// contribution of out-of-range lanes): straight-line code lets the compiler count
+// vmcnt exactly, so the next item's loads stay in flight while this one is reduced.
 template <int T>
-__device__ __forceinline__ PairRaw<T> load_item(const PairRows<T>& pr, bool vb, int ch, int nch) {
+__device__ __forceinline__ PairRaw<T> load_item(const PairRows<T>& pr, int ch, int nch) {
     PairRaw<T> w;
-    if (ch < nch) {
-        w.a = load_chunk<T>(pr.a, ch, nch);
-        if (vb) w.b = load_chunk<T>(pr.b, ch, nch);
-    }
+    const int c = ch < nch ? ch : nch - 1;
+    w.a = load_chunk<T>(pr.a, c, nch);
+    w.b = load_chunk<T>(pr.b, c, nch);
     return w;
 }
 
-// Two-row 64-lane butterfly in 6 shuffles: step 1 exchanges across the halves (lane
-// L<32 keeps row a, L>=32 row b), steps 2-6 reduce each half.  Per row this is exactly
-// the xor-butterfly tree (pairs (L, L^32), then ^16 ... ^1), which the oracle's device
-// order models; row a lands in lane 0, row b in lane 32.
-__device__ __forceinline__ float reduce_pair(float acc_a, float acc_b) {
-    const int lane = threadIdx.x & 63;
-    const float send = lane < 32 ? acc_b : acc_a;
-    const float recv = __shfl_xor(send, 32);
-    float v = (lane < 32 ? acc_a : acc_b) + recv;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+// Row sums of a pair: one 64-lane butterfly per row (steps 1,2,4,8,16,32; DPP and
+// permlane swaps, no LDS), the oracle's device order models this tree exactly.
+struct PairSum {
+    float a, b;
+};
+__device__ __forceinline__ PairSum reduce_pair(float acc_a, float acc_b) {
+    return {wave_sum(acc_a), wave_sum(acc_b)};
 }
 
 // ordered key of (logit, row): larger logit wins, ties -> smaller row (first max wins,
@@ -477,12 +584,12 @@ __device__ __forceinline__ unsigned long long argmax_key(float v, int row) {
     return ((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
 }
 
-// Epilogue of one finished pair; `v` holds row a in lane 0 and row b in lane 32.
+// Epilogue of one finished pair (every lane holds both row sums; lane 0 writes).
 template <int EPI>
-__device__ __forceinline__ void epilogue(const MVArgs& A, const PairRef& r, int p, float v, int pos,
+__device__ __forceinline__ void epilogue(const MVArgs& A, const PairRef& r, int p, PairSum v, int pos,
                                          unsigned long long& best) {
     const int lane = threadIdx.x & 63;
-    const float va = __shfl(v, 0), vb = __shfl(v, 32);
+    const float va = v.a, vb = v.b;
     if (lane != 0) return;
     if constexpr (EPI == EPI_STORE) {
         A.y[r.sa.row0 + r.ra] = va;
@@ -570,22 +677,28 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     PairRows<T> rows;
     bool pipe = false;
     PairRaw<T> cur;
+    ProRegs<NORM> R;
+    mv_prologue_issue<NORM>(A, R);  // activation loads first ...
     if (p < A.npairs) {
         r = pair_ref<EPI>(A, p);
         pipe = r.type == T;
         if (pipe) {
             rows = pair_rows<T>(r, A.cols);
-            cur = load_item<T>(rows, r.vb, lane, nch);  // issued before the prologue
+            cur = load_item<T>(rows, lane, nch);  // ... then the first weights, in flight during the prologue
         }
     }
-    mv_prologue<ACT, NORM>(A, L);
+#if !defined(LLMI_EXP_NOPRO)
+    mv_prologue_finish<ACT, NORM>(A, L, R);
+#else
+    if (R.x[0] == 1234.5f) L.d[0] = R.x[1];
+#endif
     __syncthreads();
 
     if (pipe) {
         int j = 0;
         float acc_a = 0.f, acc_b = 0.f;
         for (;;) {
-            // next work item: (p, j+1) or (p+G, 0)
+            // next work item: (p, j+1) or (p+G, 0); uniform control flow
             int pn = p, jn = j + 1;
             PairRef rn = r;
             PairRows<T> rowsn = rows;
@@ -598,14 +711,19 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
                 }
             }
             const bool has_next = pn < A.npairs && rn.type == T;
-            PairRaw<T> nxt;
-            if (has_next) nxt = load_item<T>(rowsn, rn.vb, lane + 64 * jn, nch);
+            // always issue the prefetch (a valid re-load of the current item if none)
+            const PairRaw<T> nxt = load_item<T>(has_next ? rowsn : rows, lane + 64 * (has_next ? jn : j), nch);
             const int ch = lane + 64 * j;
-            if (ch < nch) {
-                const Act act = load_act<ACT>(L, ch, nch);
-                acc_a += dot_chunk<T>(cur.a, act, ch);
-                if (r.vb) acc_b += dot_chunk<T>(cur.b, act, ch);
-            }
+            const int chc = ch < nch ? ch : nch - 1;
+            const Act act = load_act<ACT>(L, chc, nch);
+#if defined(LLMI_EXP_NODOT)
+            const float va = (float)(cur.a.q0.x ^ cur.a.q1.y ^ cur.a.hdr.x), vb = (float)(cur.b.q0.x ^ cur.b.q1.y ^ cur.b.hdr.x);
+            (void)act;
+#else
+            const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
+#endif
+            acc_a += ch < nch ? va : 0.f;
+            acc_b += ch < nch ? vb : 0.f;
             if (j == NJ - 1) {
                 epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
                 acc_a = acc_b = 0.f;
@@ -722,8 +840,7 @@ __global__ __launch_bounds__(256) void k_attn_pv(AttnArgs a) {
         const float* w = a.scores + (size_t)(g * G + hh) * a.n_ctx;
         float mx = -INFINITY;
         for (int t = tid; t < n_kv; t += 256) mx = fmaxf(mx, w[t]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        mx = wave_max(mx);
         if (lane == 0) redf[wave] = mx;
         __syncthreads();
         mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
@@ -813,8 +930,7 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
         sp_lds[t] = w;
         mx = fmaxf(mx, w);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    mx = wave_max(mx);
     if (lane == 0) redf[wave] = mx;
     __syncthreads();
     mx = redf[0];
@@ -844,8 +960,11 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
             if (t0 + 2 * j + 1 < n_kv) acc += (double)(h2f(vv[j] >> 16) * sp_lds[t0 + 2 * j + 1]);
         }
     }
-#pragma unroll
-    for (int o = 1; o < SL; o <<= 1) acc += __shfl_xor(acc, o);
+    acc += xor_partner_d<1>(acc);
+    acc += xor_partner_d<2>(acc);
+    acc += xor_partner_d<4>(acc);
+    if constexpr (SL >= 16) acc += xor_partner_d<8>(acc);
+    static_assert(SL == 8 || SL == 16, "head_dim 64 or 128");
     if (sl == 0) a.out[(size_t)h * D + d] = (float)acc;
 }
 

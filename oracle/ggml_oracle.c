@@ -350,7 +350,8 @@ static float vd_f32(int n, const float* x, const float* y) {
  * (DESIGN.md §Numerics): chunk ci contributes
  *   K-quants: (d*dA)*(float)isum - (dmin*dA)*(float)imin      (Q6_K: no min term)
  *   Q8_0    : (float)s0*(d0*dA0) + (float)s1*(d1*dA1)
- * lane L = ci % 64 accumulates its chunks in order, then a 64-lane xor butterfly.
+ * lane L = ci % 64 accumulates its chunks in order, then a 64-lane xor butterfly
+ * (steps 1,2,4,8,16,32 as in kernels.hip wave_sum).
  * Integer sums are ggml's exactly; only fp32 rounding order differs from the
  * generic loop (whose own order differs again from every SIMD variant upstream).
  * --------------------------------------------------------------------------- */
@@ -416,8 +417,12 @@ static float vd_device_order(int wtype, int n, const void* w, const void* act) {
         }
         acc[ci % 64] = acc[ci % 64] + v;
     }
-    for (int o = 32; o >= 1; o >>= 1)
-        for (int l = 0; l < o; ++l) acc[l] = acc[l] + acc[l + o];
+    /* xor butterfly, steps 1,2,4,8,16,32 (kernels.hip wave_sum: DPP + permlane swaps) */
+    for (int o = 1; o < 64; o <<= 1) {
+        float nxt[64];
+        for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
+        for (int l = 0; l < 64; ++l) acc[l] = nxt[l];
+    }
     return acc[0];
 }
 
