@@ -41,7 +41,7 @@ def parse(argv=None):
     ap.add_argument("--preset", default="llama3-8b-q4km")
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--model-dir", default=os.environ.get("LLMI_BENCH_DIR", "/tmp/llmi_bench"))
-    ap.add_argument("--profile-steps", type=int, default=8)
+    ap.add_argument("--profile-steps", type=int, default=20)
     ap.add_argument("--cpu-sample-tokens", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -172,9 +172,8 @@ class LlmiEngine:
         torch.cuda.synchronize()
 
     def profile(self, n):
-        prof = self.ctx.profile_kernels(self.next, self.pos, n)
-        self.pos += n
-        return prof
+        """Per-class kernel time at the current position (consumes no tokens)."""
+        return self.ctx.profile_kernels(self.next, self.pos, n)
 
 
 def log(msg):

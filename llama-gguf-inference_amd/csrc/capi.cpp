@@ -348,67 +348,68 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
     API_TRY
     if (!ctx || n_steps <= 0 || !us || !bytes || !launches) { set_err("llmi_profile_kernels: bad arguments"); return -1; }
     Context& c = ctx->c;
-    if (first < 0 || first >= c.m->hp.n_vocab || pos0 < 0 || pos0 + n_steps > c.n_ctx) {
+    if (first < 0 || first >= c.m->hp.n_vocab || pos0 < 0 || pos0 >= c.n_ctx) {
         set_err("llmi_profile_kernels: token/position out of range");
         return -1;
     }
     (void)hipSetDevice(c.m->device);
-    // The step is captured into a HIP graph WITH an event-record node pair around every
-    // kernel, then replayed step by step: kernels run exactly as in the timed graph
-    // replays (same grid, same back-to-back dependent launches), only the per-step host
-    // sync differs.
-    Prof prof;
-    if (!prof.reserve((size_t)(8 + 8 * c.m->hp.n_layer))) { set_err("hipEventCreate failed"); return -3; }
+    // Per kernel class: the class's launches of one step at position pos0 (all layers,
+    // the exact grids/arguments of the decode graph) are captured into a graph, and
+    // n_steps replays of it are timed between two events on the context stream.  The
+    // per-layer classes rotate through every layer's weights, so a replay streams them
+    // from HBM as the decode step does.  No tokens are consumed: the state is reset to
+    // (first, pos0) afterwards.
+    const int kv_bound = std::min(c.n_ctx, (pos0 / 256 + 1) * 256);
     std::string err;
-    if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
-    double t[K_NCLASS] = {0}, b[K_NCLASS] = {0};
-    int n[K_NCLASS] = {0};
-    hipGraphExec_t ex = nullptr;
-    int ex_bucket = -1;
-    for (int k = 0; k < n_steps; ++k) {
-        const int pos = pos0 + k, bucket = pos / 256;
-        if (bucket != ex_bucket) {
-            if (ex) (void)hipGraphExecDestroy(ex);
-            ex = nullptr;
-            prof.reset();
-            hipGraph_t g = nullptr;
-            if (hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-                set_err("capture begin failed");
-                return -3;
-            }
-            c.prof = &prof;
-            const bool ok = step_enqueue(c, std::min(c.n_ctx, (bucket + 1) * 256), err);
-            c.prof = nullptr;
-            const hipError_t ec = hipStreamEndCapture(c.stream, &g);
-            if (!ok || ec != hipSuccess || hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
-                if (g) (void)hipGraphDestroy(g);
-                set_err("llmi_profile_kernels: capture failed " + err);
-                return -3;
-            }
-            (void)hipGraphDestroy(g);
-            ex_bucket = bucket;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { set_err("hipEventCreate failed"); return -3; }
+    int rc = 0;
+    for (int k = 0; k < K_NCLASS && rc == 0; ++k) {
+        Prof pe;
+        pe.only = K_EMBED;
+        Prof pk;
+        pk.only = k;
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ex = nullptr;
+        if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); rc = -3; break; }
+        c.prof = &pe;  // sets pos/token of the step
+        bool ok = step_enqueue(c, kv_bound, err);
+        c.prof = nullptr;
+        if (!ok || hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            set_err("llmi_profile_kernels: " + err);
+            rc = -3;
+            break;
         }
-        if (hipGraphLaunch(ex, c.stream) != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess) {
-            (void)hipGraphExecDestroy(ex);
-            set_err("llmi_profile_kernels: replay failed");
-            return -4;
+        c.prof = &pk;
+        ok = step_enqueue(c, kv_bound, err);
+        c.prof = nullptr;
+        const hipError_t ec = hipStreamEndCapture(c.stream, &g);
+        if (!ok || ec != hipSuccess || hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+            set_err("llmi_profile_kernels: capture failed " + err);
+            if (g) (void)hipGraphDestroy(g);
+            rc = -3;
+            break;
         }
-        for (size_t i = 0; i < prof.used; ++i) {
-            float ms = 0.f;
-            hipEventElapsedTime(&ms, prof.ev[2 * i], prof.ev[2 * i + 1]);
-            t[prof.cls[i]] += ms * 1e3;
-            b[prof.cls[i]] += prof.bytes[i] + prof.per_kv[i] * (pos + 1);
-            n[prof.cls[i]] += 1;
-        }
+        (void)hipGraphDestroy(g);
+        float ms = 0.f;
+        bool run_ok = hipGraphLaunch(ex, c.stream) == hipSuccess && hipEventRecord(e0, c.stream) == hipSuccess;
+        for (int r = 0; run_ok && r < n_steps; ++r) run_ok = hipGraphLaunch(ex, c.stream) == hipSuccess;
+        run_ok = run_ok && hipEventRecord(e1, c.stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+                 hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+        (void)hipGraphExecDestroy(ex);
+        if (!run_ok) { set_err("llmi_profile_kernels: replay failed"); rc = -4; break; }
+        const int n = std::max(1, pk.launches);
+        us[k] = (double)ms * 1e3 / ((double)n_steps * n);
+        bytes[k] = (pk.bytes + pk.per_kv * (double)(pos0 + 1)) / n;
+        launches[k] = pk.launches;
     }
-    if (ex) (void)hipGraphExecDestroy(ex);
-    for (int k = 0; k < K_NCLASS; ++k) {
-        us[k] = n[k] ? t[k] / n[k] : 0.0;
-        bytes[k] = n[k] ? b[k] / n[k] : 0.0;
-        launches[k] = n[k] / n_steps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess) {
+        if (rc == 0) { set_err("llmi_profile_kernels: state reset failed"); rc = -4; }
     }
-    c.n_past = pos0 + n_steps;
-    return 0;
+    c.n_past = pos0;
+    return rc;
     API_CATCH(-5)
 }
 

@@ -311,29 +311,6 @@ void context_clear(Context& c) {
     c.n_past = 0;
 }
 
-bool Prof::reserve(size_t launches) {
-    while (ev.size() < 2 * launches) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return false;
-        ev.push_back(e);
-    }
-    return true;
-}
-bool Prof::begin(hipStream_t s) {
-    if (!reserve(used + 1)) return false;
-    return hipEventRecord(ev[2 * used], s) == hipSuccess;
-}
-void Prof::end(hipStream_t s, int k, double b, double b_per_kv) {
-    (void)hipEventRecord(ev[2 * used + 1], s);
-    cls.push_back(k);
-    bytes.push_back(b);
-    per_kv.push_back(b_per_kv);
-    ++used;
-}
-Prof::~Prof() {
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-}
-
 namespace {
 
 Seg seg_of(const Model& m, const DevMat& d, int row0) {
@@ -360,9 +337,9 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     ea.cols = E; ea.vocab = hp.n_vocab; ea.x = c.x; ea.st = c.st; ea.hist = c.hist; ea.n_ctx = c.n_ctx;
     Prof* P = c.prof;
     const double kvpos = (double)hp.n_head_kv * D * 2.0;  // bytes of K (or V) per layer per position
-    if (P) P->begin(c.stream);
-    HIPC(launch_embed(ea, c.stream));
-    if (P) P->end(c.stream, K_EMBED, (double)m.tok_embd.bytes / hp.n_vocab + E * 4.0);
+    auto want = [P](int k) { return !P || P->want(k); };
+    if (want(K_EMBED)) HIPC(launch_embed(ea, c.stream));
+    if (P) P->add(K_EMBED, (double)m.tok_embd.bytes / hp.n_vocab + E * 4.0);
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m.layers[(size_t)l];
         // --- QKV + RoPE + KV write (grouped by activation kind) ---
@@ -378,15 +355,14 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
             int rows = 0;
             while (j < 3 && act_kind(qkv[j].type) == act_kind(qkv[i].type)) { a.seg[a.nseg++] = qkv[j]; rows += qkv[j].rows; ++j; }
             a.npairs = rows / 2;
-            if (P) P->begin(c.stream);
-            HIPC(launch_matvec(a, EPI_QKV, c.max_blocks, c.stream));
+            if (want(K_QKV)) HIPC(launch_matvec(a, EPI_QKV, c.max_blocks, c.stream));
             if (P) {
                 double b = 8.0 * E;
                 for (int k = i; k < j; ++k) {
                     const DevMat& dm = k == 0 ? L.wq : k == 1 ? L.wk : L.wv;
                     b += (double)dm.bytes + (k == 0 ? 4.0 * nq : 2.0 * nk);
                 }
-                P->end(c.stream, K_QKV, b);
+                P->add(K_QKV, b);
             }
             i = j;
         }
@@ -394,37 +370,32 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         AttnArgs at;
         at.q = c.q; at.kc = a.kc; at.vc = a.vc; at.scores = c.scores; at.out = c.att; at.st = c.st;
         at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
-        if (P) P->begin(c.stream);
-        HIPC(launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
-        if (P) P->end(c.stream, K_ATTN, 8.0 * nq, 2.0 * kvpos);
+        if (want(K_ATTN)) HIPC(launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
+        if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---
         MVArgs o;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
-        if (P) P->begin(c.stream);
-        HIPC(launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
-        if (P) P->end(c.stream, K_ATTN_OUT, (double)L.wo.bytes + 4.0 * nq + 8.0 * E);
+        if (want(K_ATTN_OUT)) HIPC(launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
+        if (P) P->add(K_ATTN_OUT, (double)L.wo.bytes + 4.0 * nq + 8.0 * E);
         // --- gate/up + SwiGLU ---
         MVArgs gu;
         gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2;
         gu.cols = E; gu.x = c.x; gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps;
         gu.y = c.h; gu.npairs = hp.n_ff;
-        if (P) P->begin(c.stream);
-        HIPC(launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
-        if (P) P->end(c.stream, K_FFN_GATE_UP, (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff);
+        if (want(K_FFN_GATE_UP)) HIPC(launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
+        if (P) P->add(K_FFN_GATE_UP, (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff);
         // --- down + residual ---
         MVArgs dn;
         dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
-        if (P) P->begin(c.stream);
-        HIPC(launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
-        if (P) P->end(c.stream, K_FFN_DOWN, (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E);
+        if (want(K_FFN_DOWN)) HIPC(launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
+        if (P) P->add(K_FFN_DOWN, (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E);
     }
     MVArgs lo;
     lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
     lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
     lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = c.st->key; lo.st = c.st;
-    if (P) P->begin(c.stream);
-    HIPC(launch_matvec(lo, EPI_LOGITS, c.max_blocks, c.stream));
-    if (P) P->end(c.stream, K_OUTPUT, (double)m.output.bytes + 8.0 * E + 4.0 * hp.n_vocab);
+    if (want(K_OUTPUT)) HIPC(launch_matvec(lo, EPI_LOGITS, c.max_blocks, c.stream));
+    if (P) P->add(K_OUTPUT, (double)m.output.bytes + 8.0 * E + 4.0 * hp.n_vocab);
     return true;
 }
 

@@ -41,20 +41,21 @@ struct Model {
     ~Model();
 };
 
-// Per-launch device timing of one eager decode step (llmi_profile_kernels): an event
-// pair around every launch on the context stream, binned by kernel class.
+// Kernel-class timing (llmi_profile_kernels): step_enqueue with a Prof attached only
+// enqueues the launches of class `only` (all classes if -1) and records their
+// algorithmic bytes; the caller captures that subset into a graph and times replays
+// of it between two events on the context stream.
 enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_NCLASS };
 struct Prof {
-    std::vector<hipEvent_t> ev;  // pool, 2 per launch (pre-created: recorded inside a graph capture)
-    std::vector<int> cls;
-    std::vector<double> bytes;   // fixed algorithmic bytes of the launch
-    std::vector<double> per_kv;  // + per_kv * n_kv (attention: K and V rows read)
-    size_t used = 0;
-    bool reserve(size_t launches);
-    bool begin(hipStream_t s);
-    void end(hipStream_t s, int k, double b, double b_per_kv = 0.0);
-    void reset() { used = 0; cls.clear(); bytes.clear(); per_kv.clear(); }
-    ~Prof();
+    int only = -1;               // class filter
+    int launches = 0;            // launches of the filtered class enqueued
+    double bytes = 0;            // their fixed algorithmic bytes ...
+    double per_kv = 0;           // ... + per_kv * n_kv (attention: K and V rows read)
+    bool want(int k) const { return only < 0 || only == k; }
+    void add(int k, double b, double b_per_kv = 0.0) {
+        if (!want(k)) return;
+        ++launches; bytes += b; per_kv += b_per_kv;
+    }
 };
 
 struct Context {

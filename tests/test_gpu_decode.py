@@ -136,3 +136,28 @@ def test_decode_parity_real_widths(gpu, synth_dir, preset, n_layer, n_vocab):
     prompt = [1, 100, 2000, 31000]
     worst, g, o, margins, m, c = run_parity(path, prompt, 4, n_ctx=64, exact=True)
     assert g == o
+
+
+def test_profile_kernels_leaves_state(gpu, tiny_models):
+    """llmi_profile_kernels times every kernel class (positive times, launch counts of
+    the graph) and consumes no tokens: decoding after it is bit-identical."""
+    path = tiny_models["tiny-mixed-d128"]
+    m = llmi.Model(path)
+    ref = llmi.Context(m, n_ctx=64)
+    c = llmi.Context(m, n_ctx=64)
+    prompt = [1, 5, 9, 17]
+    assert ref.decode(prompt) == 0 and c.decode(prompt) == 0
+    nxt = c.greedy(-1)
+    prof = c.profile_kernels(nxt, len(prompt), 4)
+    n_layer = m.n_layer
+    for k, v in prof.items():
+        assert v["us"] > 0 and v["bytes"] > 0, (k, v)
+    assert prof["embed"]["launches_per_step"] == 1 and prof["output"]["launches_per_step"] == 1
+    assert prof["ffn_gate_up"]["launches_per_step"] == n_layer
+    assert prof["attention"]["launches_per_step"] == n_layer
+    a = ref.generate_greedy(nxt, len(prompt), 6)
+    b = c.generate_greedy(nxt, len(prompt), 6)
+    assert a == b
+    p = len(prompt) + 6
+    assert ref.decode([a[-1]], pos=[p]) == 0 and c.decode([b[-1]], pos=[p]) == 0
+    assert np.array_equal(ref.logits(-1), c.logits(-1))
