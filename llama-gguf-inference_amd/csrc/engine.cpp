@@ -256,6 +256,13 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string&
     const HParams& hp = m->hp;
     c.m = m;
     c.n_ctx = n_ctx > 0 ? n_ctx : std::min(hp.n_ctx_train > 0 ? hp.n_ctx_train : 4096, 4096);
+    // padded like upstream llama.cpp's KV cache (multiple of 256): the attention kernels
+    // read V rows in 16-B (8-position) pieces and K in 64-position tiles
+    c.n_ctx = (c.n_ctx + 255) / 256 * 256;
+    {
+        const char* e = getenv("LLMI_ATTN_MODE");
+        set_attn_mode(e ? atoi(e) : 0);
+    }
     c.use_graphs = use_graphs;
     HIPC(hipSetDevice(m->device));
     hipDeviceProp_t prop;

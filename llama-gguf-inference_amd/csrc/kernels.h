@@ -11,6 +11,7 @@ namespace llmi {
 
 constexpr int kMVThreads = 256;        // 4 waves of 64; each wave owns one row pair at a time
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
+constexpr size_t kSplitAttnMaxLds = 64 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
 
 enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
 
@@ -70,6 +71,10 @@ size_t mv_lds_bytes(int act, int cols);
 
 // All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t stream);
+// attention path for a KV bound: 1 fused (one WG per head), 2 split (scores + PV over
+// (group, 8-dim slice) workgroups), 3 two-kernel long-context path
+int attn_path(int n_head, int n_head_kv, int kv_bound);
+void set_attn_mode(int mode);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
 hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, int64_t cols,

@@ -894,6 +894,64 @@ __global__ __launch_bounds__(256) void k_attn_pv(AttnArgs a) {
         }
 }
 
+// Split attention, phase 2 (phase 1 = k_attn_scores): grid (HK, D/8), 256 threads.
+// Every workgroup recomputes the softmax statistics of its G heads from the scores
+// (one wave per head, so no barrier between heads; max, double exp-sum, f16-rounded
+// probabilities exactly as the fused kernel), keeps the probabilities in LDS and
+// accumulates 8 output dims: 32 lanes per dim, 8 positions (16 B of the transposed V
+// row) per lane per iteration, G double accumulators, 32-lane butterfly at the end.
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_attn_pv_split(AttnArgs a, int kvb) {
+    extern __shared__ __attribute__((aligned(16))) float spv[];  // [G][kvb]
+    const int g = blockIdx.x, dc = blockIdx.y;
+    const int n_kv = a.st->pos + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int hh = wave; hh < G; hh += 4) {
+        const float* w = a.scores + (size_t)(g * G + hh) * a.n_ctx;
+        float* sp = spv + hh * kvb;
+        float mx = -INFINITY;
+        for (int t = lane; t < n_kv; t += 64) {
+            const float v = w[t];
+            sp[t] = v;
+            mx = fmaxf(mx, v);
+        }
+        mx = wave_max(mx);
+        double sum = 0.0;
+        for (int t = lane; t < n_kv; t += 64) sum += (double)llmi_expf(sp[t] - mx);
+        sum = wave_sum_d(sum);
+        const float inv = (float)(1.0 / sum);
+        for (int t = lane; t < n_kv; t += 64) sp[t] = h2f(f2h(llmi_expf(sp[t] - mx) * inv));
+    }
+    __syncthreads();
+    const int d = dc * 8 + (tid >> 5), sl = tid & 31;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    double acc[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+    for (int t0 = 8 * sl; t0 < n_kv; t0 += 256) {
+        const u32x4 vv = *(const u32x4*)(vr + t0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = t0 + j;
+            const float v = h2f((uint16_t)(vv[j >> 1] >> (16 * (j & 1))));
+            if (t < n_kv) {
+#pragma unroll
+                for (int hh = 0; hh < G; ++hh) acc[hh] += (double)(v * spv[hh * kvb + t]);
+            }
+        }
+    }
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        double v = acc[hh];
+        v += xor_partner_d<1>(v);
+        v += xor_partner_d<2>(v);
+        v += xor_partner_d<4>(v);
+        v += xor_partner_d<8>(v);
+        v += xor_partner_d<16>(v);
+        if (sl == 0) a.out[(size_t)(g * G + hh) * D + d] = (float)v;
+    }
+}
+
 // Fused single-launch attention for KV lengths that fit in LDS (kv_bound <= 8192):
 // one 1024-thread workgroup per query head; scores, softmax statistics and the
 // f16-rounded probabilities stay in LDS, so the only global traffic is one K and one V
@@ -1192,10 +1250,45 @@ static hipError_t attn_dispatch_g(const AttnArgs& a, int g, int hk, int kv_bound
     return hipGetLastError();
 }
 
+template <int D>
+static hipError_t attn_split_g(const AttnArgs& a, int g, int hk, int kv_bound, hipStream_t s) {
+    const dim3 gs(hk, (kv_bound + 63) / 64), gp(hk, D / 8);
+    const size_t lds = (size_t)g * kv_bound * 4;
+    switch (g) {
+#define LLMI_ATT(G)                                                                      \
+    case G:                                                                              \
+        hipLaunchKernelGGL((k_attn_scores<D, G>), gs, dim3(256), 0, s, a);               \
+        hipLaunchKernelGGL((k_attn_pv_split<D, G>), gp, dim3(256), lds, s, a, kv_bound); \
+        break;
+        LLMI_ATT(1) LLMI_ATT(2) LLMI_ATT(4) LLMI_ATT(8)
+#undef LLMI_ATT
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel (experiments: LLMI_ATTN_MODE)
+void set_attn_mode(int mode) { g_attn_mode = mode; }
+int attn_path(int n_head, int n_head_kv, int kv_bound) {
+    const int g = n_head / n_head_kv;
+    const bool split_ok = (size_t)g * kv_bound * 4 <= kSplitAttnMaxLds;
+    const bool fused_ok = kv_bound <= kFusedAttnMaxKV;
+    if (g_attn_mode == 1 && fused_ok) return 1;
+    if (g_attn_mode == 2 && split_ok) return 2;
+    if (g_attn_mode == 3) return 3;
+    return split_ok ? 2 : fused_ok ? 1 : 3;
+}
+
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     const int g = n_head / n_head_kv;
-    if (kv_bound <= kFusedAttnMaxKV) {
+    const int path = attn_path(n_head, n_head_kv, kv_bound);
+    if (path == 2) {
+        if (head_dim == 128) return attn_split_g<128>(a, g, n_head_kv, kv_bound, s);
+        if (head_dim == 64) return attn_split_g<64>(a, g, n_head_kv, kv_bound, s);
+        return hipErrorInvalidValue;
+    }
+    if (path == 1) {
         const size_t lds = (size_t)kv_bound * 4;
         if (head_dim == 128) hipLaunchKernelGGL((k_attn_fused<128>), dim3(n_head), dim3(1024), lds, s, a, g, n_head_kv);
         else if (head_dim == 64) hipLaunchKernelGGL((k_attn_fused<64>), dim3(n_head), dim3(1024), lds, s, a, g, n_head_kv);

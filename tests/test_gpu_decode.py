@@ -161,3 +161,18 @@ def test_profile_kernels_leaves_state(gpu, tiny_models):
     p = len(prompt) + 6
     assert ref.decode([a[-1]], pos=[p]) == 0 and c.decode([b[-1]], pos=[p]) == 0
     assert np.array_equal(ref.logits(-1), c.logits(-1))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
+    """Each attention path (1 fused one-WG-per-head, 2 split scores+PV over 8-dim
+    slices, 3 long-context two-kernel) reproduces the oracle's logits bit for bit
+    (LLMI_ATTN_MODE is read when a context is created)."""
+    monkeypatch.setenv("LLMI_ATTN_MODE", str(mode))
+    rng = np.random.default_rng(5 + mode)
+    for preset in ("tiny-mixed", "tiny-mixed-d128"):
+        prompt = [1] + list(rng.integers(3, 700, 20))
+        worst, g, o, *_ = run_parity(tiny_models[preset], prompt, 8, n_ctx=64, exact=True)
+        assert g == o
+    monkeypatch.setenv("LLMI_ATTN_MODE", "0")
+    llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode

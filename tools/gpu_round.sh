@@ -30,6 +30,7 @@ cat "$OUT/prof_bench.json"
 step pmc_bench 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_bench" -o run --output-format csv -- \
     python3 bench.py --prompt 4 --steps 8 --warmup 2 --profile-steps 0 --no-cpu-baseline \
     > "$OUT/pmc_bench.json" 2> "$OUT/pmc_bench.err" || { tail -20 "$OUT/pmc_bench.err"; exit 1; }
-MV_SHAPES=12:28672x4096 MV_REPS=5 step pmc_cal 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_cal" -o run \
+export MV_SHAPES=12:28672x4096 MV_REPS=5
+step pmc_cal 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_cal" -o run \
     --output-format csv -- python3 tools/mvbench.py > "$OUT/pmc_cal.log" 2>&1 || { tail -20 "$OUT/pmc_cal.log"; exit 1; }
 echo "all steps done"
