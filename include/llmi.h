@@ -190,10 +190,18 @@ int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x_dev, const 
  * (to defeat the 256 MB Infinity Cache); returns average microseconds per matvec */
 double llmi_bench_matvec(int32_t type, const void* w_dev, int32_t n_mats, int64_t rows, int64_t cols,
                          const float* x_dev, float* y_dev, int32_t reps);
+/* the same with epilogue/prologue variants (mode bit 0: fused RMSNorm with unit weights,
+ * bit 1: logits epilogue with device argmax); launches graph-replayed */
+double llmi_bench_matvec_ex(int32_t type, const void* w_dev, int32_t n_mats, int64_t rows, int64_t cols,
+                            const float* x_dev, float* y_dev, int32_t reps, int32_t mode);
 
 /* streaming-read reference: average microseconds to read `bytes` from each of n_bufs
  * distinct buffers (stride `stride` bytes) with coalesced 16-B/lane loads */
 double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint64_t bytes, int32_t reps, int32_t blocks);
+/* Attention microbenchmark: n_kv positions, one launch per layer over >= 512 MB of
+ * distinct KV caches, graph-replayed `reps` times; microseconds per launch (< 0 error).
+ * mode: 0 auto, 1 fused, 2 split, 3 two-kernel. */
+double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps);
 
 #pragma GCC visibility pop
 

@@ -67,7 +67,7 @@ bool ensure_outs(llama_context* ctx, int n) {
     if (n > ctx->keys_cap) {
         if (ctx->keys_pinned) (void)hipHostFree(ctx->keys_pinned);
         ctx->keys_pinned = nullptr;
-        if (hipHostMalloc((void**)&ctx->keys_pinned, (size_t)n * 8, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc((void**)&ctx->keys_pinned, (size_t)n * 8 * kArgSlots, hipHostMallocDefault) != hipSuccess) {
             set_err("hipHostMalloc");
             return false;
         }
@@ -234,7 +234,8 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
         if (r >= 0) {
             (void)hipMemcpyAsync(ctx->outs + (size_t)r * hp.n_vocab * 4, c.logits, (size_t)hp.n_vocab * 4,
                                  hipMemcpyDeviceToDevice, c.stream);
-            (void)hipMemcpyAsync(ctx->keys_pinned + r, &c.st->key[pos & 1], 8, hipMemcpyDeviceToHost, c.stream);
+            (void)hipMemcpyAsync(ctx->keys_pinned + (size_t)r * kArgSlots, &c.st->key[pos & 1][0], 8 * kArgSlots,
+                                 hipMemcpyDeviceToHost, c.stream);
         }
         last_pos = std::max(last_pos, pos);
     }
@@ -303,8 +304,7 @@ llama_token llmi_greedy_ith(struct llama_context* ctx, int32_t i) {
     if (!ctx) return -1;
     const int r = out_row(ctx, i);
     if (r < 0) { set_err("llmi_greedy_ith: no logits for this batch index"); return -1; }
-    const unsigned long long k = ctx->keys_pinned[r];
-    return (llama_token)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+    return (llama_token)key_token(ctx->keys_pinned + (size_t)r * kArgSlots);
 }
 
 int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_gen, llama_token* out) {
@@ -325,14 +325,14 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
     }
     hipEventRecord(c.ev1, c.stream);
     std::vector<int32_t> h((size_t)n_gen);
-    unsigned long long key = 0;
+    unsigned long long keys[kArgSlots];
     if (n_gen > 1)
         (void)hipMemcpyAsync(h.data(), c.hist + pos0 + 1, (size_t)(n_gen - 1) * 4, hipMemcpyDeviceToHost, c.stream);
-    (void)hipMemcpyAsync(&key, &c.st->key[(pos0 + n_gen - 1) & 1], 8, hipMemcpyDeviceToHost, c.stream);
+    (void)hipMemcpyAsync(keys, &c.st->key[(pos0 + n_gen - 1) & 1][0], sizeof(keys), hipMemcpyDeviceToHost, c.stream);
     hipError_t e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess) { set_err("llmi_generate_greedy: " + hip_err(e)); return -4; }
     for (int k = 0; k + 1 < n_gen; ++k) out[k] = h[(size_t)k];
-    out[n_gen - 1] = (llama_token)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
+    out[n_gen - 1] = (llama_token)key_token(keys);
     float ms = 0.f;
     hipEventElapsedTime(&ms, c.ev0, c.ev1);
     c.last_us = ms * 1e3;
@@ -618,8 +618,8 @@ int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x, const floa
     return 0;
 }
 
-double llmi_bench_matvec(int32_t type, const void* w, int32_t n_mats, int64_t rows, int64_t cols, const float* x, float* y,
-                         int32_t reps) {
+double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t rows, int64_t cols, const float* x, float* y,
+                            int32_t reps, int32_t mode) {
     const int64_t lb = llmi_device_layout_bytes(type, rows, cols);
     if (lb <= 0 || n_mats <= 0 || reps <= 0) { set_err("bad arguments"); return -1.0; }
     const size_t stride = align_up((size_t)lb, 4096);
@@ -628,27 +628,63 @@ double llmi_bench_matvec(int32_t type, const void* w, int32_t n_mats, int64_t ro
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, dev);
     const int mb = std::max(64, prop.multiProcessorCount * wg_per_cu());
+    float* nw = nullptr;
+    StepState* st = nullptr;
+    const bool norm = mode & 1, logits = mode & 2;
+    if (norm) {
+        std::vector<float> ones((size_t)cols, 1.0f);
+        if (hipMalloc(&nw, (size_t)cols * 4) != hipSuccess) { set_err("out of device memory"); return -1.0; }
+        (void)hipMemcpy(nw, ones.data(), (size_t)cols * 4, hipMemcpyHostToDevice);
+    }
+    if (logits) {
+        if (hipMalloc(&st, sizeof(StepState)) != hipSuccess) { (void)hipFree(nw); set_err("out of device memory"); return -1.0; }
+        (void)hipMemset(st, 0, sizeof(StepState));
+    }
     MVArgs a;
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
-    for (int k = 0; k < n_mats; ++k) {  // warm-up (code, TLB)
+    a.nw = nw; a.eps = 1e-5f;
+    if (logits) { a.st = st; a.argmax = &st->key[0][0]; }
+    const int epi = logits ? EPI_LOGITS : EPI_STORE;
+    // one graph of n_mats launches (one per weight copy), replayed: no host launch cost
+    hipStream_t s = nullptr;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ex = nullptr;
+    bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    for (int k = 0; ok && k < n_mats; ++k) {
         a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows, cols);
-        if (launch_matvec(a, EPI_STORE, mb, nullptr) != hipSuccess) { set_err("launch failed"); return -1.0; }
+        ok = launch_matvec(a, epi, mb, s) == hipSuccess;
     }
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, nullptr);
-    for (int r = 0; r < reps; ++r) {
-        a.seg[0] = seg_at(type, (const uint8_t*)w + stride * (r % n_mats), rows, cols);
-        (void)launch_matvec(a, EPI_STORE, mb, nullptr);
+    ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
+    double res = -1.0;
+    const int nrep = std::max(1, reps / n_mats);
+    if (ok) {
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipGraphLaunch(ex, s);  // warm-up (code, TLB)
+        (void)hipEventRecord(e0, s);
+        for (int r = 0; r < nrep; ++r) (void)hipGraphLaunch(ex, s);
+        (void)hipEventRecord(e1, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+            res = (double)ms * 1e3 / ((double)nrep * n_mats);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } else {
+        set_err("llmi_bench_matvec: capture/launch failed");
     }
-    hipEventRecord(e1, nullptr);
-    hipEventSynchronize(e1);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, e0, e1);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    return (double)ms * 1e3 / reps;
+    if (ex) (void)hipGraphExecDestroy(ex);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipStreamDestroy(s);
+    (void)hipFree(nw);
+    (void)hipFree(st);
+    return res;
+}
+
+double llmi_bench_matvec(int32_t type, const void* w, int32_t n_mats, int64_t rows, int64_t cols, const float* x, float* y,
+                         int32_t reps) {
+    return llmi_bench_matvec_ex(type, w, n_mats, rows, cols, x, y, reps, 0);
 }
 
 double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint64_t bytes, int32_t reps, int32_t blocks) {
@@ -671,3 +707,76 @@ double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint6
 }
 
 }  // extern "C"
+
+// Attention microbenchmark (kernel level, no model): n_layers distinct KV caches of
+// n_ctx = round256(n_kv) positions (>= 512 MB in total, so replays stream them from HBM
+// like a decode step does), one launch per layer captured into a graph, `reps` graph
+// replays timed between two events.  Returns microseconds per launch (incl. the
+// dependent-launch gap), < 0 on error.  mode: attention path (0 auto, 1 fused, 2 split, 3 two-kernel).
+double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps) {
+    if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || (head_dim != 64 && head_dim != 128) || n_kv <= 0 || reps <= 0) {
+        set_err("llmi_bench_attention: bad arguments");
+        return -1.0;
+    }
+    const int n_ctx = (n_kv + 255) / 256 * 256;
+    const size_t kv_layer = (size_t)n_head_kv * n_ctx * head_dim;  // elements per layer, K or V
+    const int nl = (int)std::max<size_t>(2, (size_t)(512u << 20) / (kv_layer * 4) + 1);
+    uint16_t *kc = nullptr, *vc = nullptr;
+    float *q = nullptr, *scores = nullptr, *out = nullptr;
+    StepState* st = nullptr;
+    auto cleanup = [&] {
+        (void)hipFree(kc); (void)hipFree(vc); (void)hipFree(q); (void)hipFree(scores); (void)hipFree(out); (void)hipFree(st);
+    };
+    if (hipMalloc(&kc, kv_layer * nl * 2) != hipSuccess || hipMalloc(&vc, kv_layer * nl * 2) != hipSuccess ||
+        hipMalloc(&q, (size_t)n_head * head_dim * 4) != hipSuccess || hipMalloc(&scores, (size_t)n_head * n_ctx * 4) != hipSuccess ||
+        hipMalloc(&out, (size_t)n_head * head_dim * 4) != hipSuccess || hipMalloc(&st, sizeof(StepState)) != hipSuccess) {
+        cleanup();
+        set_err("llmi_bench_attention: out of device memory");
+        return -1.0;
+    }
+    (void)hipMemset(kc, 0x3c, kv_layer * nl * 2);  // f16 0x3c3c ~ 1.06
+    (void)hipMemset(vc, 0x3c, kv_layer * nl * 2);
+    (void)hipMemset(q, 0, (size_t)n_head * head_dim * 4);
+    StepState hs{};
+    hs.pos = n_kv - 1;
+    hs.pos_next = n_kv;
+    (void)hipMemcpy(st, &hs, sizeof(hs), hipMemcpyHostToDevice);
+    set_attn_mode(mode);
+    hipStream_t s = nullptr;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
+    AttnArgs a;
+    a.q = q; a.scores = scores; a.out = out; a.st = st; a.n_ctx = n_ctx; a.scale = 1.0f / sqrtf((float)head_dim);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ex = nullptr;
+    bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    for (int l = 0; ok && l < nl; ++l) {
+        a.kc = kc + (size_t)l * kv_layer;
+        a.vc = vc + (size_t)l * kv_layer;
+        ok = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s) == hipSuccess;
+    }
+    ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
+    double res = -1.0;
+    if (ok) {
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipGraphLaunch(ex, s);
+        (void)hipEventRecord(e0, s);
+        for (int r = 0; r < reps; ++r) (void)hipGraphLaunch(ex, s);
+        (void)hipEventRecord(e1, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+            res = (double)ms * 1e3 / ((double)reps * nl);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } else {
+        set_err("llmi_bench_attention: capture/launch failed");
+    }
+    if (ex) (void)hipGraphExecDestroy(ex);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipStreamDestroy(s);
+    set_attn_mode(0);
+    cleanup();
+    return res;
+}

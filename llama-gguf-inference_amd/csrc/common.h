@@ -99,7 +99,10 @@ inline bool needs_repack(int t) { return t == T_Q4_K || t == T_Q5_K || t == T_Q6
 //   k_embed (every workgroup): p = pos_next; token = (token_in_pos == p) ? token_in
 //           : argmax of key[(p-1)&1]; workgroup 0 publishes pos/token/hist[p] and
 //           clears key[p&1];
-//   logits kernel: atomicMax into key[p&1]; its workgroup 0 sets pos_next = p+1.
+//   logits kernel: each workgroup reduces its rows' argmax and atomicMax-es it into
+//           slot blockIdx % kArgSlots of key[p&1] (spreading the atomics over 64
+//           addresses: same-address atomics serialise at ~10 ns each); its workgroup 0
+//           sets pos_next = p+1.  Consumers take the max over the slots.
 // Every field is written by exactly one workgroup and never read by another workgroup
 // of the same launch, so no intra-kernel synchronisation is needed.
 struct StepState {
@@ -109,7 +112,13 @@ struct StepState {
     int32_t pos;             // position of the current step (written by k_embed)
     int32_t token;           // token of the current step
     int32_t pad;
-    unsigned long long key[2];  // per-parity argmax key: (ordered logit << 32) | (0xffffffff - row)
+    unsigned long long key[2][64];  // per-parity argmax key slots: (ordered logit << 32) | (0xffffffff - row)
 };
+constexpr int kArgSlots = 64;
+inline int key_token(const unsigned long long* slots) {  // host: token of a parity's slots
+    unsigned long long k = 0;
+    for (int i = 0; i < kArgSlots; ++i) k = slots[i] > k ? slots[i] : k;
+    return (int)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+}
 
 }  // namespace llmi

@@ -312,7 +312,9 @@ void context_clear(Context& c) {
     (void)hipMemsetAsync(c.kc, 0, kv_elems * 2, c.stream);
     (void)hipMemsetAsync(c.vc, 0, kv_elems * 2, c.stream);
     (void)hipMemsetAsync(c.hist, 0, (size_t)c.n_ctx * 4, c.stream);
-    StepState s0{-1, -1, 0, 0, 0, 0, {0ull, 0ull}};
+    StepState s0{};
+    s0.token_in = -1;
+    s0.token_in_pos = -1;
     (void)hipMemcpyAsync(c.st, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
     (void)hipStreamSynchronize(c.stream);
     c.n_past = 0;
@@ -400,7 +402,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     MVArgs lo;
     lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
     lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
-    lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = c.st->key; lo.st = c.st;
+    lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = &c.st->key[0][0]; lo.st = c.st;
     if (want(K_OUTPUT)) HIPC(launch_matvec(lo, EPI_LOGITS, c.max_blocks, c.stream));
     if (P) P->add(K_OUTPUT, (double)m.output.bytes + 8.0 * E + 4.0 * hp.n_vocab);
     return true;

@@ -9,9 +9,13 @@
 
 namespace llmi {
 
-constexpr int kMVThreads = 256;        // 4 waves of 64; each wave owns one row pair at a time
+#ifndef LLMI_MV_THREADS
+#define LLMI_MV_THREADS 256
+#endif
+constexpr int kMVThreads = LLMI_MV_THREADS;  // matvec workgroup; each wave owns one row pair at a time
+constexpr int kMVWaves = kMVThreads / 64;
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
-constexpr size_t kSplitAttnMaxLds = 64 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
+constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
 
 enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
 

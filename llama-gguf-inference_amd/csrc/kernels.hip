@@ -26,6 +26,10 @@
 //   k_repack_* one-time load-time layout transforms (common.h).
 #include "kernels.h"
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include <hip/hip_runtime.h>
 
 namespace llmi {
@@ -147,7 +151,7 @@ __host__ __device__ inline size_t lds_d_off(int act, int cols) { return a16((siz
 __host__ __device__ inline size_t lds_red_off(int act, int cols) {
     return a16(lds_d_off(act, cols) + (size_t)(act ? cols / 32 : cols / 256) * 4);
 }
-size_t mv_lds_bytes(int act, int cols) { return lds_red_off(act, cols) + 8 * sizeof(double); }
+size_t mv_lds_bytes(int act, int cols) { return lds_red_off(act, cols) + kMVWaves * sizeof(double); }
 
 __device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
     Lds l;
@@ -159,12 +163,20 @@ __device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
     return l;
 }
 
+// workgroup double sum of a matvec workgroup (kMVWaves waves; pairwise tree over waves)
 __device__ double block_sum_d(double v, double* red) {
     v = wave_sum_d(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    return (red[0] + red[1]) + (red[2] + red[3]);
+    double r[kMVWaves];
+#pragma unroll
+    for (int w = 0; w < kMVWaves; ++w) r[w] = red[w];
+#pragma unroll
+    for (int o = 1; o < kMVWaves; o <<= 1)
+#pragma unroll
+        for (int w = 0; w + o < kMVWaves; w += 2 * o) r[w] = r[w] + r[w + o];
+    return r[0];
 }
 
 // ----------------------------------------------------------------------------------
@@ -666,13 +678,13 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     const Lds L = carve(smem, ACT, A.cols);
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
-    const int G = gridDim.x * 4;
+    const int G = gridDim.x * kMVWaves;
     const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
 
-    int p = blockIdx.x * 4 + wave;
+    int p = blockIdx.x * kMVWaves + wave;
     PairRef r;
     PairRows<T> rows;
     bool pipe = false;
@@ -747,9 +759,19 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
     }
     if constexpr (EPI == EPI_LOGITS) {
+        // workgroup max of the waves' keys, then one atomic into this workgroup's slot
         const int cur_pos = A.st->pos;
-        if (lane == 0 && best) atomicMax(&A.argmax[cur_pos & 1], best);
-        if (blockIdx.x == 0 && threadIdx.x == 0) A.st->pos_next = cur_pos + 1;
+        unsigned long long* red = (unsigned long long*)L.red;
+        __syncthreads();
+        if (lane == 0) red[wave] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long b = red[0];
+#pragma unroll
+            for (int w = 1; w < kMVWaves; ++w) b = red[w] > b ? red[w] : b;
+            if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
+            if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
+        }
     }
 }
 
@@ -894,51 +916,135 @@ __global__ __launch_bounds__(256) void k_attn_pv(AttnArgs a) {
         }
 }
 
-// Split attention, phase 2 (phase 1 = k_attn_scores): grid (HK, D/8), 256 threads.
-// Every workgroup recomputes the softmax statistics of its G heads from the scores
-// (one wave per head, so no barrier between heads; max, double exp-sum, f16-rounded
-// probabilities exactly as the fused kernel), keeps the probabilities in LDS and
+// Split attention, phase 1: grid (HK, kv_bound/64), 256 threads; thread (t, qd) dots
+// quarter qd of K row t with the G f16-rounded query heads of its group (G independent
+// double chains of D/4), then a 4-lane butterfly; K rows are read straight from HBM,
+// 4 lanes x (D/2) B per row.  Rows < kv_bound are always inside the cache, so the K
+// loads are issued before the position is known (no dependent-load chain).
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_attn_scores4(AttnArgs a) {
+    const int g = blockIdx.x, t0 = blockIdx.y * 64;
+    const int tid = threadIdx.x;
+    constexpr int DQ = D / 4;
+    const int t = t0 + (tid >> 2), qd = tid & 3;
+    const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+    u32x4 kv[DQ / 8];
+#pragma unroll
+    for (int i = 0; i < DQ / 8; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
+    __shared__ __attribute__((aligned(16))) float qs[G][D];
+    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = h2f(f2h(a.q[(size_t)g * G * D + i]));
+    const int n_kv = a.st->pos + 1;
+    __syncthreads();
+    if (t0 >= n_kv) return;
+    double acc[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+#pragma unroll
+    for (int i = 0; i < DQ / 8; ++i) {
+        const int d = qd * DQ + 8 * i;
+        float k[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            k[2 * j] = h2f((uint16_t)kv[i][j]);
+            k[2 * j + 1] = h2f((uint16_t)(kv[i][j] >> 16));
+        }
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            const float4 qa = *(const float4*)&qs[hh][d], qb = *(const float4*)&qs[hh][d + 4];
+            acc[hh] += (double)(k[0] * qa.x); acc[hh] += (double)(k[1] * qa.y);
+            acc[hh] += (double)(k[2] * qa.z); acc[hh] += (double)(k[3] * qa.w);
+            acc[hh] += (double)(k[4] * qb.x); acc[hh] += (double)(k[5] * qb.y);
+            acc[hh] += (double)(k[6] * qb.z); acc[hh] += (double)(k[7] * qb.w);
+        }
+    }
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        acc[hh] += xor_partner_d<1>(acc[hh]);
+        acc[hh] += xor_partner_d<2>(acc[hh]);
+        if (t < n_kv && qd == (hh & 3)) a.scores[(size_t)(g * G + hh) * a.n_ctx + t] = (float)acc[hh] * a.scale;
+    }
+}
+
+// Split attention, phase 2: grid (HK, D/8), 256 threads.  Every workgroup recomputes
+// the softmax of its G heads from the scores (one wave per head: max, e = expf(s - max)
+// kept in LDS, double sum, p = f16(e / sum) exactly as the fused kernel), then
 // accumulates 8 output dims: 32 lanes per dim, 8 positions (16 B of the transposed V
-// row) per lane per iteration, G double accumulators, 32-lane butterfly at the end.
+// row) per lane and step, 4 steps of loads in flight, G double accumulators, 32-lane
+// butterfly.  Score and first V loads are issued before the position is known.
 template <int D, int G>
 __global__ __launch_bounds__(256) void k_attn_pv_split(AttnArgs a, int kvb) {
     extern __shared__ __attribute__((aligned(16))) float spv[];  // [G][kvb]
     const int g = blockIdx.x, dc = blockIdx.y;
-    const int n_kv = a.st->pos + 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int hh = wave; hh < G; hh += 4) {
-        const float* w = a.scores + (size_t)(g * G + hh) * a.n_ctx;
-        float* sp = spv + hh * kvb;
-        float mx = -INFINITY;
-        for (int t = lane; t < n_kv; t += 64) {
-            const float v = w[t];
-            sp[t] = v;
-            mx = fmaxf(mx, v);
-        }
-        mx = wave_max(mx);
-        double sum = 0.0;
-        for (int t = lane; t < n_kv; t += 64) sum += (double)llmi_expf(sp[t] - mx);
-        sum = wave_sum_d(sum);
-        const float inv = (float)(1.0 / sum);
-        for (int t = lane; t < n_kv; t += 64) sp[t] = h2f(f2h(llmi_expf(sp[t] - mx) * inv));
-    }
-    __syncthreads();
     const int d = dc * 8 + (tid >> 5), sl = tid & 31;
     const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    u32x4 vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) vv[u] = *(const u32x4*)(vr + min(8 * sl + 256 * u, kvb - 8));
+    // 1. stage the G score rows (all kv_bound positions; those past n_kv are never used)
+    const int n4 = kvb >> 2;
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        const float4* src = (const float4*)(a.scores + (size_t)(g * G + hh) * a.n_ctx);
+        float4* dst = (float4*)(spv + hh * kvb);
+        for (int j0 = tid; j0 < n4; j0 += 1024) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = src[min(j0 + 256 * u, n4 - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j0 + 256 * u < n4) dst[j0 + 256 * u] = v[u];
+        }
+    }
+    const int n_kv = a.st->pos + 1;
+    __syncthreads();
+    // 2. softmax, one wave per head; p = 0 past n_kv (up to the next multiple of 8)
+    for (int hh = wave; hh < G; hh += 4) {
+        float* sp = spv + hh * kvb;
+        float mx = -INFINITY;
+        for (int t = lane; t < n_kv; t += 64) mx = fmaxf(mx, sp[t]);
+        mx = wave_max(mx);
+        double sum = 0.0;
+        for (int t = lane; t < n_kv; t += 64) {
+            const float e = llmi_expf(sp[t] - mx);
+            sp[t] = e;
+            sum += (double)e;
+        }
+        sum = wave_sum_d(sum);
+        const float inv = (float)(1.0 / sum);
+        for (int t = lane; t < n_kv; t += 64) sp[t] = h2f(f2h(sp[t] * inv));
+        for (int t = n_kv + lane; t < ((n_kv + 7) & ~7); t += 64) sp[t] = 0.f;
+    }
+    __syncthreads();
+    // 3. PV (V past n_kv may be anything: masked to 0 so 0 * NaN never happens)
     double acc[G];
 #pragma unroll
     for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
-    for (int t0 = 8 * sl; t0 < n_kv; t0 += 256) {
-        const u32x4 vv = *(const u32x4*)(vr + t0);
+    for (int t0 = 8 * sl;;) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int t = t0 + j;
-            const float v = h2f((uint16_t)(vv[j >> 1] >> (16 * (j & 1))));
-            if (t < n_kv) {
+        for (int u = 0; u < 4; ++u) {
+            const int tb = t0 + 256 * u;
+            if (tb < n_kv) {
+                float v[8];
 #pragma unroll
-                for (int hh = 0; hh < G; ++hh) acc[hh] += (double)(v * spv[hh * kvb + t]);
+                for (int j = 0; j < 8; ++j) {
+                    const float f = h2f((uint16_t)(vv[u][j >> 1] >> (16 * (j & 1))));
+                    v[j] = tb + j < n_kv ? f : 0.f;
+                }
+#pragma unroll
+                for (int hh = 0; hh < G; ++hh) {
+                    const float4 pa = *(const float4*)&spv[hh * kvb + tb], pb = *(const float4*)&spv[hh * kvb + tb + 4];
+                    acc[hh] += (double)(v[0] * pa.x); acc[hh] += (double)(v[1] * pa.y);
+                    acc[hh] += (double)(v[2] * pa.z); acc[hh] += (double)(v[3] * pa.w);
+                    acc[hh] += (double)(v[4] * pb.x); acc[hh] += (double)(v[5] * pb.y);
+                    acc[hh] += (double)(v[6] * pb.z); acc[hh] += (double)(v[7] * pb.w);
+                }
             }
         }
+        t0 += 1024;
+        if (t0 >= n_kv) break;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) vv[u] = *(const u32x4*)(vr + min(t0 + 256 * u, kvb - 8));
     }
 #pragma unroll
     for (int hh = 0; hh < G; ++hh) {
@@ -1010,13 +1116,18 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
     const int d = tid / SL, sl = tid % SL;
     const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
     double acc = 0.0;
-    for (int t0 = 8 * sl; t0 < n_kv; t0 += 8 * SL) {
-        const u32x4 vv = *(const u32x4*)(vr + t0);
+    for (int t0 = 8 * sl; t0 < n_kv; t0 += 32 * SL) {  // 4 loads in flight, addresses clamped into the row
+        u32x4 vv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (t0 + 2 * j < n_kv) acc += (double)(h2f(vv[j]) * sp_lds[t0 + 2 * j]);
-            if (t0 + 2 * j + 1 < n_kv) acc += (double)(h2f(vv[j] >> 16) * sp_lds[t0 + 2 * j + 1]);
-        }
+        for (int u = 0; u < 4; ++u) vv[u] = *(const u32x4*)(vr + min(t0 + 8 * SL * u, a.n_ctx - 8));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = t0 + 8 * SL * u + 2 * j;
+                if (t < n_kv) acc += (double)(h2f(vv[u][j]) * sp_lds[t]);
+                if (t + 1 < n_kv) acc += (double)(h2f(vv[u][j] >> 16) * sp_lds[t + 1]);
+            }
     }
     acc += xor_partner_d<1>(acc);
     acc += xor_partner_d<2>(acc);
@@ -1067,17 +1178,40 @@ __device__ float dequant_elem(const Seg& w, int row, int e, int cols) {
     }
 }
 
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#define LLMI_MAX64_STEP(O)                                                                        \
+    {                                                                                             \
+        const uint32_t lo = xor_partner_u32<O>((uint32_t)v), hi = xor_partner_u32<O>((uint32_t)(v >> 32)); \
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;                         \
+        v = o > v ? o : v;                                                                        \
+    }
+    LLMI_MAX64_STEP(1) LLMI_MAX64_STEP(2) LLMI_MAX64_STEP(4) LLMI_MAX64_STEP(8) LLMI_MAX64_STEP(16) LLMI_MAX64_STEP(32)
+#undef LLMI_MAX64_STEP
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_embed(EmbArgs a) {
-    const StepState* st = a.st;
+    StepState* st = a.st;
     const int pos = st->pos_next;
-    int tok = st->token_in_pos == pos ? st->token_in
-                                      : (int)(0xffffffffu - (uint32_t)(st->key[(pos + 1) & 1] & 0xffffffffull));
-    if (tok < 0 || tok >= a.vocab) tok = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.st->pos = pos;
-        a.st->token = tok;
-        a.st->key[pos & 1] = 0;
-        if (pos >= 0 && pos < a.n_ctx) a.hist[pos] = tok;
+    __shared__ int s_tok;
+    if (threadIdx.x < 64) {  // wave 0: max over the previous step's argmax slots
+        static_assert(kArgSlots == 64, "one slot per lane");
+        const unsigned long long k = wave_max_u64(st->key[(pos + 1) & 1][threadIdx.x]);
+        if (threadIdx.x == 0) {
+            int tok = st->token_in_pos == pos ? st->token_in : (int)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+            if (tok < 0 || tok >= a.vocab) tok = 0;
+            s_tok = tok;
+        }
+    }
+    __syncthreads();
+    const int tok = s_tok;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < kArgSlots) st->key[pos & 1][threadIdx.x] = 0;
+        if (threadIdx.x == 0) {
+            st->pos = pos;
+            st->token = tok;
+            if (pos >= 0 && pos < a.n_ctx) a.hist[pos] = tok;
+        }
     }
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e < a.cols) a.x[e] = dequant_elem(a.w, tok, e, a.cols);
@@ -1182,17 +1316,52 @@ hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int bl
 // ----------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------
+// Grid of a matvec launch: never more workgroups than can be resident at once (the
+// kernel is grid-strided over row pairs; a second dispatch round would be a tail of
+// idle CUs).  Residency per CU comes from the occupancy query for the instantiation
+// and its LDS, cached per (kernel, LDS bytes, device).
+template <typename K>
+static dim3 resident_grid(K kernel, dim3 grid, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, size_t, int>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple((const void*)kernel, lds, dev);
+    int cap = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) {
+            cap = it->second;
+        } else {
+            int occ = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kMVThreads, lds) != hipSuccess || occ <= 0) occ = 1;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
+            cap = occ * cus;
+            cache.emplace(key, cap);
+        }
+    }
+    if ((int)grid.x > cap) grid.x = cap;
+    return grid;
+}
+
+template <int ACT, bool NORM, int T, int EPI>
+static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    auto k = k_matvec<ACT, NORM, EPI, T>;
+    hipLaunchKernelGGL(k, resident_grid(k, grid, lds), dim3(kMVThreads), lds, s, a);
+    return hipGetLastError();
+}
+
 template <int ACT, bool NORM, int T>
 static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
     switch (epi) {
-        case EPI_STORE: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_STORE, T>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_ADD: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_ADD, T>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_QKV: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_QKV, T>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_SWIGLU: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_SWIGLU, T>), grid, dim3(kMVThreads), lds, s, a); break;
-        case EPI_LOGITS: hipLaunchKernelGGL((k_matvec<ACT, NORM, EPI_LOGITS, T>), grid, dim3(kMVThreads), lds, s, a); break;
+        case EPI_STORE: return mv_launch<ACT, NORM, T, EPI_STORE>(a, grid, lds, s);
+        case EPI_ADD: return mv_launch<ACT, NORM, T, EPI_ADD>(a, grid, lds, s);
+        case EPI_QKV: return mv_launch<ACT, NORM, T, EPI_QKV>(a, grid, lds, s);
+        case EPI_SWIGLU: return mv_launch<ACT, NORM, T, EPI_SWIGLU>(a, grid, lds, s);
+        case EPI_LOGITS: return mv_launch<ACT, NORM, T, EPI_LOGITS>(a, grid, lds, s);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 template <bool NORM>
@@ -1220,7 +1389,7 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
     for (int i = 1; i < a.nseg; ++i)
         if (act_kind(a.seg[i].type) != act) return hipErrorInvalidValue;
     const size_t lds = mv_lds_bytes(act, a.cols);
-    int blocks = (a.npairs + 3) / 4;
+    int blocks = (a.npairs + kMVWaves - 1) / kMVWaves;
     if (blocks > max_blocks) blocks = max_blocks;
     const dim3 grid(blocks);
     return a.nw ? mv_dispatch_type<true>(a, epi, grid, lds, s) : mv_dispatch_type<false>(a, epi, grid, lds, s);
@@ -1257,7 +1426,7 @@ static hipError_t attn_split_g(const AttnArgs& a, int g, int hk, int kv_bound, h
     switch (g) {
 #define LLMI_ATT(G)                                                                      \
     case G:                                                                              \
-        hipLaunchKernelGGL((k_attn_scores<D, G>), gs, dim3(256), 0, s, a);               \
+        hipLaunchKernelGGL((k_attn_scores4<D, G>), gs, dim3(256), 0, s, a);              \
         hipLaunchKernelGGL((k_attn_pv_split<D, G>), gp, dim3(256), lds, s, a, kv_bound); \
         break;
         LLMI_ATT(1) LLMI_ATT(2) LLMI_ATT(4) LLMI_ATT(8)

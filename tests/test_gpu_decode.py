@@ -117,7 +117,8 @@ def test_batch_decode_equals_single(gpu, tiny_models):
 def test_decode_error_codes(gpu, tiny_models):
     m = llmi.Model(tiny_models["tiny-mixed"])
     c = llmi.Context(m, n_ctx=32)
-    assert c.decode([1], pos=[32]) == 1          # no KV slot
+    assert c.n_ctx == 256                        # padded to 256 like upstream's KV cache
+    assert c.decode([1], pos=[c.n_ctx]) == 1     # no KV slot
     assert c.decode([m.n_vocab]) == -1            # invalid token
     assert c.decode([1, 2, 3]) == 0
     assert c.eval([4, 5], 3) == 0

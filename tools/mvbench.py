@@ -19,6 +19,7 @@ if os.environ.get("MV_SHAPES"):  # e.g. "12:28672x4096,14:128256x4096"
         t, rc = tok.split(":"); r, c = rc.split("x")
         shapes.append((int(t), int(r), int(c)))
 REPS = int(os.environ.get("MV_REPS", "200"))
+MODE = int(os.environ.get("MV_MODE", "0"))  # bit0 fused RMSNorm, bit1 logits epilogue
 rng = np.random.default_rng(0)
 for qt, rows, cols in shapes:
     lb = L.llmi_device_layout_bytes(qt, rows, cols)
@@ -30,7 +31,7 @@ for qt, rows, cols in shapes:
         assert L.llmi_repack(qt, P(raw), C.c_void_p(w.data_ptr() + stride * k), rows, cols) == 0
     x = torch.randn(cols, device="cuda"); y = torch.empty(rows, device="cuda")
     torch.cuda.synchronize()
-    us = L.llmi_bench_matvec(qt, P(w), n, rows, cols, P(x), P(y), REPS)
+    us = L.llmi_bench_matvec_ex(qt, P(w), n, rows, cols, P(x), P(y), REPS, MODE)
     alg = raw.numel()
     us_s = L.llmi_bench_stream(P(w), n, stride, alg, REPS, 2048)
     key = f"{qt}:{rows}x{cols}"
