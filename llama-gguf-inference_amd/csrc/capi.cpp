@@ -780,3 +780,25 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     cleanup();
     return res;
 }
+
+// Experiment hook (LLMI_EXP_TRACE builds): one STORE matvec launch with per-wave
+// s_memrealtime stamps {entry, after prologue, first pair done, exit, HW_ID, XCC<<32|pairs}
+// written to trace_dev[grid*waves*6]; returns the grid size, < 0 on error.
+int32_t llmi_trace_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, const float* x, float* y, int32_t mode,
+                          uint64_t* trace_dev) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev);
+    const int mb = std::max(64, prop.multiProcessorCount * wg_per_cu());
+    MVArgs a;
+    a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
+    a.seg[0] = seg_at(type, w, rows, cols);
+    a.trace = (unsigned long long*)trace_dev;
+    (void)mode;
+    if (launch_matvec(a, EPI_STORE, mb, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        set_err("llmi_trace_matvec: launch failed");
+        return -1;
+    }
+    return std::min(mb, (a.npairs + kMVWaves - 1) / kMVWaves);
+}

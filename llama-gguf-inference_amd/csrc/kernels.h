@@ -46,6 +46,7 @@ struct MVArgs {
     StepState* st = nullptr;     // QKV reads pos; LOGITS reads pos and advances pos_next
     int head_dim = 0, n_rot = 0, n_ctx = 0, nq = 0, nk = 0;
     unsigned long long* argmax = nullptr;  // LOGITS
+    unsigned long long* trace = nullptr;   // LLMI_EXP_TRACE builds: per-wave s_memrealtime stamps
 };
 
 struct AttnArgs {

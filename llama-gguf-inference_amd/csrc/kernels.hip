@@ -257,41 +257,40 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
 }
 
 // Prologue in two halves so a caller can put the weight prefetch between them:
-// issue() loads this thread's sub-blocks of x (and norm w) into registers (up to
-// NPRE of them: 4 without norm = cols <= 16384, 2 with norm = cols <= 8192);
-// finish() computes the norm, quantizes and writes LDS.  Sub-blocks beyond NPRE are
-// loaded inside finish() (correct, just not overlapped).
-template <bool NORM>
+// issue() loads this thread's first NP sub-blocks of x (and norm w) into registers —
+// UNCONDITIONALLY (indices clamped), so the load count is static and the first use
+// waits with vmcnt(#weight loads issued after them) instead of vmcnt(0), i.e. the
+// prologue never waits for the weight prefetch; finish() computes the norm,
+// quantizes and writes LDS.  NP = ceil(cols / (16 * kMVThreads)) rounded up to 1/2/4
+// (chosen at launch); sub-blocks beyond NP are loaded inside finish().
+template <bool NORM, int NP>
 struct ProRegs {
-    static constexpr int NPRE = NORM ? 2 : 4;
-    float x[NPRE][16];
-    float w[NORM ? NPRE : 1][16];
+    float x[NP][16];
+    float w[NORM ? NP : 1][16];
 };
-template <bool NORM>
-__device__ __forceinline__ void mv_prologue_issue(const MVArgs& A, ProRegs<NORM>& R) {
+template <bool NORM, int NP>
+__device__ __forceinline__ void mv_prologue_issue(const MVArgs& A, ProRegs<NORM, NP>& R) {
     const int nsub = A.cols / 16;
 #pragma unroll
-    for (int i = 0; i < ProRegs<NORM>::NPRE; ++i) {
-        const int sb = threadIdx.x + i * kMVThreads;
-        if (sb < nsub) {
+    for (int i = 0; i < NP; ++i) {
+        const int sb = min((int)threadIdx.x + i * kMVThreads, nsub - 1);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
-                R.x[i][4 * k + 0] = xv.x; R.x[i][4 * k + 1] = xv.y; R.x[i][4 * k + 2] = xv.z; R.x[i][4 * k + 3] = xv.w;
-                if constexpr (NORM) {
-                    const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
-                    R.w[i][4 * k + 0] = wv.x; R.w[i][4 * k + 1] = wv.y; R.w[i][4 * k + 2] = wv.z; R.w[i][4 * k + 3] = wv.w;
-                }
+        for (int k = 0; k < 4; ++k) {
+            const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
+            R.x[i][4 * k + 0] = xv.x; R.x[i][4 * k + 1] = xv.y; R.x[i][4 * k + 2] = xv.z; R.x[i][4 * k + 3] = xv.w;
+            if constexpr (NORM) {
+                const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                R.w[i][4 * k + 0] = wv.x; R.w[i][4 * k + 1] = wv.y; R.w[i][4 * k + 2] = wv.z; R.w[i][4 * k + 3] = wv.w;
             }
         }
     }
 }
-template <bool NORM>
-__device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM>& R, int i, int sb, float (&v)[16],
+template <bool NORM, int NP>
+__device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM, NP>& R, int i, int sb, float (&v)[16],
                                          float (&w)[16]) {
-    if (i < ProRegs<NORM>::NPRE) {
+    if (i < NP) {
 #pragma unroll
-        for (int ii = 0; ii < ProRegs<NORM>::NPRE; ++ii)
+        for (int ii = 0; ii < NP; ++ii)
             if (ii == i) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
@@ -311,16 +310,22 @@ __device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM>& R
         }
     }
 }
-template <int ACT, bool NORM>
-__device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM>& R) {
+template <int ACT, bool NORM, int NP>
+__device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
     const int tid = threadIdx.x, cols = A.cols;
     const int nsub = cols / 16;
     float scale = 1.0f;
     if constexpr (NORM) {
         double s = 0.0;
-        for (int i = 0, sb = tid; sb < nsub; ++i, sb += kMVThreads) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i)  // register-held sub-blocks (static indices)
+            if (tid + i * kMVThreads < nsub) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) s += (double)(R.x[i][j] * R.x[i][j]);
+            }
+        for (int sb = tid + NP * kMVThreads; sb < nsub; sb += kMVThreads) {  // rest (cols > NP*16*threads)
             float v[16], w[16];
-            load_sub<NORM>(A, R, i, sb, v, w);
+            load_sub<NORM, NP>(A, R, NP, sb, v, w);
 #pragma unroll
             for (int j = 0; j < 16; ++j) s += (double)(v[j] * v[j]);
         }
@@ -328,9 +333,22 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
         const float mean = (float)(s / (double)cols);
         scale = 1.0f / sqrtf(mean + A.eps);
     }
-    for (int i = 0, sb = tid; sb < nsub; ++i, sb += kMVThreads) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int sb = tid + i * kMVThreads;
+        if (sb < nsub) {
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                v[j] = R.x[i][j];
+                if constexpr (NORM) v[j] = (v[j] * scale) * R.w[i][j];
+            }
+            quant_sub<ACT>(L, cols, sb, v);
+        }
+    }
+    for (int sb = tid + NP * kMVThreads; sb < nsub; sb += kMVThreads) {
         float v[16], w[16];
-        load_sub<NORM>(A, R, i, sb, v, w);
+        load_sub<NORM, NP>(A, R, NP, sb, v, w);
         if constexpr (NORM) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) v[j] = (v[j] * scale) * w[j];
@@ -340,9 +358,9 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
 }
 template <int ACT, bool NORM>
 __device__ __forceinline__ void mv_prologue(const MVArgs& A, const Lds& L) {
-    ProRegs<NORM> R;
-    mv_prologue_issue<NORM>(A, R);
-    mv_prologue_finish<ACT, NORM>(A, L, R);
+    ProRegs<NORM, 1> R;
+    mv_prologue_issue<NORM, 1>(A, R);
+    mv_prologue_finish<ACT, NORM, 1>(A, L, R);
 }
 
 // ----------------------------------------------------------------------------------
@@ -672,7 +690,7 @@ __device__ __forceinline__ float generic_row_any(int type, const Seg& s, int row
     }
 }
 
-template <int ACT, bool NORM, int EPI, int T>
+template <int ACT, bool NORM, int EPI, int T, int NP>
 __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Lds L = carve(smem, ACT, A.cols);
@@ -684,27 +702,39 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
 
+#if defined(LLMI_EXP_TRACE)
+    const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long tr1 = 0, tr2 = 0;
+    int tr_items = 0;
+#endif
     int p = blockIdx.x * kMVWaves + wave;
     PairRef r;
     PairRows<T> rows;
     bool pipe = false;
-    PairRaw<T> cur;
-    ProRegs<NORM> R;
-    mv_prologue_issue<NORM>(A, R);  // activation loads first ...
-    if (p < A.npairs) {
-        r = pair_ref<EPI>(A, p);
-        pipe = r.type == T;
-        if (pipe) {
-            rows = pair_rows<T>(r, A.cols);
-            cur = load_item<T>(rows, lane, nch);  // ... then the first weights, in flight during the prologue
-        }
+    ProRegs<NORM, NP> R;
+    mv_prologue_issue<NORM, NP>(A, R);  // activation loads first ...
+    r = pair_ref<EPI>(A, p < A.npairs ? p : A.npairs - 1);
+    pipe = p < A.npairs && r.type == T;
+    rows = pair_rows<T>(r, A.cols);
+    // ... then the first weights, in flight during the prologue.  Issued on every path
+    // (a wave without a pipelined pair reads a dummy chunk inside x: every plane offset
+    // of one chunk stays below cols*4 bytes) so the prologue's first wait counts only
+    // the activation loads.
+    {
+        const uint8_t* xb = (const uint8_t*)A.x;
+        const RowPtr dummy{xb, xb, xb, xb};
+        if (!pipe) rows.a = rows.b = dummy;
     }
+    PairRaw<T> cur = load_item<T>(rows, lane, nch);
 #if !defined(LLMI_EXP_NOPRO)
-    mv_prologue_finish<ACT, NORM>(A, L, R);
+    mv_prologue_finish<ACT, NORM, NP>(A, L, R);
 #else
-    if (R.x[0] == 1234.5f) L.d[0] = R.x[1];
+    if (R.x[0][0] == 1234.5f) L.d[0] = R.x[0][1];
 #endif
     __syncthreads();
+#if defined(LLMI_EXP_TRACE)
+    tr1 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     if (pipe) {
         int j = 0;
@@ -739,6 +769,9 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             if (j == NJ - 1) {
                 epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
                 acc_a = acc_b = 0.f;
+#if defined(LLMI_EXP_TRACE)
+                if (tr_items++ == 0) tr2 = __builtin_amdgcn_s_memrealtime();
+#endif
             }
             if (!has_next) {
                 p = pn;
@@ -758,6 +791,17 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         const float acc_b = r.vb ? generic_row_any<ACT>(r.sb.type, r.sb, r.rb, A.cols, L) : 0.f;
         epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
     }
+#if defined(LLMI_EXP_TRACE)
+    if (A.trace && lane == 0) {
+        unsigned hw = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned long long* t = A.trace + ((size_t)blockIdx.x * kMVWaves + wave) * 6;
+        t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = __builtin_amdgcn_s_memrealtime();
+        t[4] = hw; t[5] = ((unsigned long long)xcc << 32) | (unsigned)tr_items;
+    }
+#endif
     if constexpr (EPI == EPI_LOGITS) {
         // workgroup max of the waves' keys, then one atomic into this workgroup's slot
         const int cur_pos = A.st->pos;
@@ -1345,23 +1389,46 @@ static dim3 resident_grid(K kernel, dim3 grid, size_t lds) {
     return grid;
 }
 
-template <int ACT, bool NORM, int T, int EPI>
+template <int ACT, bool NORM, int T, int EPI, int NP>
 static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    auto k = k_matvec<ACT, NORM, EPI, T>;
+    auto k = k_matvec<ACT, NORM, EPI, T, NP>;
     hipLaunchKernelGGL(k, resident_grid(k, grid, lds), dim3(kMVThreads), lds, s, a);
     return hipGetLastError();
 }
 
+// prologue sub-blocks per thread held in registers: 1, 2 or 4
+static int prologue_np(int cols) {
+    const int per = (cols / 16 + kMVThreads - 1) / kMVThreads;
+    return per <= 1 ? 1 : per <= 2 ? 2 : 4;
+}
+
+template <int ACT, bool NORM, int T, int EPI>
+static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    switch (prologue_np(a.cols)) {
+        case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
+        case 2: return mv_launch<ACT, NORM, T, EPI, 2>(a, grid, lds, s);
+        default: return mv_launch<ACT, NORM, T, EPI, 4>(a, grid, lds, s);
+    }
+}
+
+// Instantiated (ACT, NORM, EPI) combinations: STORE and ADD with or without the fused
+// RMSNorm; QKV, SWIGLU and LOGITS always take a normalised input.
 template <int ACT, bool NORM, int T>
 static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
     switch (epi) {
-        case EPI_STORE: return mv_launch<ACT, NORM, T, EPI_STORE>(a, grid, lds, s);
-        case EPI_ADD: return mv_launch<ACT, NORM, T, EPI_ADD>(a, grid, lds, s);
-        case EPI_QKV: return mv_launch<ACT, NORM, T, EPI_QKV>(a, grid, lds, s);
-        case EPI_SWIGLU: return mv_launch<ACT, NORM, T, EPI_SWIGLU>(a, grid, lds, s);
-        case EPI_LOGITS: return mv_launch<ACT, NORM, T, EPI_LOGITS>(a, grid, lds, s);
-        default: return hipErrorInvalidValue;
+        case EPI_STORE: return mv_launch_np<ACT, NORM, T, EPI_STORE>(a, grid, lds, s);
+        case EPI_ADD: return mv_launch_np<ACT, NORM, T, EPI_ADD>(a, grid, lds, s);
+        default: break;
     }
+    if constexpr (NORM) {
+        switch (epi) {
+            case EPI_QKV: return mv_launch_np<ACT, NORM, T, EPI_QKV>(a, grid, lds, s);
+            case EPI_SWIGLU: return mv_launch_np<ACT, NORM, T, EPI_SWIGLU>(a, grid, lds, s);
+            case EPI_LOGITS: return mv_launch_np<ACT, NORM, T, EPI_LOGITS>(a, grid, lds, s);
+            default: break;
+        }
+    }
+    return hipErrorInvalidValue;
 }
 
 template <bool NORM>
@@ -1391,6 +1458,12 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
     const size_t lds = mv_lds_bytes(act, a.cols);
     int blocks = (a.npairs + kMVWaves - 1) / kMVWaves;
     if (blocks > max_blocks) blocks = max_blocks;
+#if defined(LLMI_EXP_BALANCE)
+    {  // experiment: equal pairs per wave (fewer workgroups when that divides better)
+        const int waves = blocks * kMVWaves, per = (a.npairs + waves - 1) / waves;
+        blocks = ((a.npairs + per - 1) / per + kMVWaves - 1) / kMVWaves;
+    }
+#endif
     const dim3 grid(blocks);
     return a.nw ? mv_dispatch_type<true>(a, epi, grid, lds, s) : mv_dispatch_type<false>(a, epi, grid, lds, s);
 }
