@@ -353,58 +353,38 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
         return -1;
     }
     (void)hipSetDevice(c.m->device);
-    // Per kernel class: the class's launches of one step at position pos0 (all layers,
-    // the exact grids/arguments of the decode graph) are captured into a graph, and
-    // n_steps replays of it are timed between two events on the context stream.  The
-    // per-layer classes rotate through every layer's weights, so a replay streams them
-    // from HBM as the decode step does.  No tokens are consumed: the state is reset to
-    // (first, pos0) afterwards.
+    // Per kernel class: the class's launches of n_steps steps at position pos0 (every
+    // layer, the decode graph's exact grids and arguments) are launched back to back,
+    // each armed with an event pair that the runtime records when the kernel starts
+    // and ends (hipExtLaunchKernelGGL): kernel execution time without launch gaps.
+    // The per-layer classes rotate through every layer's weights, so each launch
+    // streams its matrix from HBM as in decode.  No tokens are consumed: the state is
+    // reset to (first, pos0) afterwards.
     const int kv_bound = std::min(c.n_ctx, (pos0 / 256 + 1) * 256);
     std::string err;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { set_err("hipEventCreate failed"); return -3; }
     int rc = 0;
     for (int k = 0; k < K_NCLASS && rc == 0; ++k) {
         Prof pe;
         pe.only = K_EMBED;
         Prof pk;
         pk.only = k;
-        hipGraph_t g = nullptr;
-        hipGraphExec_t ex = nullptr;
+        pk.timed = true;
         if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); rc = -3; break; }
         c.prof = &pe;  // sets pos/token of the step
         bool ok = step_enqueue(c, kv_bound, err);
-        c.prof = nullptr;
-        if (!ok || hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-            set_err("llmi_profile_kernels: " + err);
-            rc = -3;
-            break;
-        }
         c.prof = &pk;
-        ok = step_enqueue(c, kv_bound, err);
+        for (int r = 0; ok && r < n_steps; ++r) ok = step_enqueue(c, kv_bound, err);
         c.prof = nullptr;
-        const hipError_t ec = hipStreamEndCapture(c.stream, &g);
-        if (!ok || ec != hipSuccess || hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
-            set_err("llmi_profile_kernels: capture failed " + err);
-            if (g) (void)hipGraphDestroy(g);
-            rc = -3;
+        if (!ok || hipStreamSynchronize(c.stream) != hipSuccess) {
+            set_err("llmi_profile_kernels: " + (err.empty() ? std::string("launch failed") : err));
+            rc = -4;
             break;
         }
-        (void)hipGraphDestroy(g);
-        float ms = 0.f;
-        bool run_ok = hipGraphLaunch(ex, c.stream) == hipSuccess && hipEventRecord(e0, c.stream) == hipSuccess;
-        for (int r = 0; run_ok && r < n_steps; ++r) run_ok = hipGraphLaunch(ex, c.stream) == hipSuccess;
-        run_ok = run_ok && hipEventRecord(e1, c.stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
-                 hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
-        (void)hipGraphExecDestroy(ex);
-        if (!run_ok) { set_err("llmi_profile_kernels: replay failed"); rc = -4; break; }
         const int n = std::max(1, pk.launches);
-        us[k] = (double)ms * 1e3 / ((double)n_steps * n);
+        us[k] = pk.used ? pk.elapsed_us() / (double)pk.used : 0.0;
         bytes[k] = (pk.bytes + pk.per_kv * (double)(pos0 + 1)) / n;
-        launches[k] = pk.launches;
+        launches[k] = pk.launches / n_steps;
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess) {
         if (rc == 0) { set_err("llmi_profile_kernels: state reset failed"); rc = -4; }
     }

@@ -48,14 +48,21 @@ struct Model {
 enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_NCLASS };
 struct Prof {
     int only = -1;               // class filter
+    bool timed = false;          // arm an event pair around every filtered launch
     int launches = 0;            // launches of the filtered class enqueued
     double bytes = 0;            // their fixed algorithmic bytes ...
     double per_kv = 0;           // ... + per_kv * n_kv (attention: K and V rows read)
+    std::vector<hipEvent_t> ev;  // 2 per timed launch
+    size_t used = 0;
     bool want(int k) const { return only < 0 || only == k; }
     void add(int k, double b, double b_per_kv = 0.0) {
         if (!want(k)) return;
         ++launches; bytes += b; per_kv += b_per_kv;
     }
+    bool arm();                  // next event pair -> set_launch_events
+    static void disarm();
+    double elapsed_us() const;   // sum over the recorded pairs (after a sync)
+    ~Prof();
 };
 
 struct Context {

@@ -79,6 +79,8 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
 // attention path for a KV bound: 1 fused (one WG per head), 2 split (scores + PV over
 // (group, 8-dim slice) workgroups), 3 two-kernel long-context path
 int attn_path(int n_head, int n_head_kv, int kv_bound);
+// arm (or with nullptrs disarm) per-op kernel timing events for this thread's launches
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);

@@ -30,9 +30,26 @@
 #include <mutex>
 #include <tuple>
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 namespace llmi {
+
+// Launch-event hook (llmi_profile_kernels): while armed, the timed launches record
+// `start` when the first kernel of the op begins and `stop` when the last one ends
+// (hipExtLaunchKernelGGL), i.e. kernel execution time without dependent-launch gaps.
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+    t_ev_start = start;
+    t_ev_stop = stop;
+}
+template <typename K, typename... Args>
+static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool first, bool last, Args... args) {
+    hipEvent_t e0 = first ? t_ev_start : nullptr, e1 = last ? t_ev_stop : nullptr;
+    if (e0 || e1) hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, e0, e1, 0, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+}
+
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1392,7 +1409,7 @@ static dim3 resident_grid(K kernel, dim3 grid, size_t lds) {
 template <int ACT, bool NORM, int T, int EPI, int NP>
 static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     auto k = k_matvec<ACT, NORM, EPI, T, NP>;
-    hipLaunchKernelGGL(k, resident_grid(k, grid, lds), dim3(kMVThreads), lds, s, a);
+    launch_k(k, resident_grid(k, grid, lds), dim3(kMVThreads), lds, s, true, true, a);
     return hipGetLastError();
 }
 
@@ -1482,8 +1499,8 @@ static hipError_t attn_dispatch_g(const AttnArgs& a, int g, int hk, int kv_bound
     switch (g) {
 #define LLMI_ATT(G)                                                                   \
     case G:                                                                           \
-        hipLaunchKernelGGL((k_attn_scores<D, G>), gs, dim3(256), 0, s, a);            \
-        hipLaunchKernelGGL((k_attn_pv<D, G>), gp, dim3(256), 0, s, a);                \
+        launch_k(k_attn_scores<D, G>, gs, dim3(256), 0, s, true, false, a);          \
+        launch_k(k_attn_pv<D, G>, gp, dim3(256), 0, s, false, true, a);              \
         break;
         LLMI_ATT(1) LLMI_ATT(2) LLMI_ATT(4) LLMI_ATT(8)
 #undef LLMI_ATT
@@ -1499,8 +1516,8 @@ static hipError_t attn_split_g(const AttnArgs& a, int g, int hk, int kv_bound, h
     switch (g) {
 #define LLMI_ATT(G)                                                                      \
     case G:                                                                              \
-        hipLaunchKernelGGL((k_attn_scores4<D, G>), gs, dim3(256), 0, s, a);              \
-        hipLaunchKernelGGL((k_attn_pv_split<D, G>), gp, dim3(256), lds, s, a, kv_bound); \
+        launch_k(k_attn_scores4<D, G>, gs, dim3(256), 0, s, true, false, a);            \
+        launch_k(k_attn_pv_split<D, G>, gp, dim3(256), lds, s, false, true, a, kv_bound); \
         break;
         LLMI_ATT(1) LLMI_ATT(2) LLMI_ATT(4) LLMI_ATT(8)
 #undef LLMI_ATT
@@ -1532,8 +1549,8 @@ hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int he
     }
     if (path == 1) {
         const size_t lds = (size_t)kv_bound * 4;
-        if (head_dim == 128) hipLaunchKernelGGL((k_attn_fused<128>), dim3(n_head), dim3(1024), lds, s, a, g, n_head_kv);
-        else if (head_dim == 64) hipLaunchKernelGGL((k_attn_fused<64>), dim3(n_head), dim3(1024), lds, s, a, g, n_head_kv);
+        if (head_dim == 128) launch_k(k_attn_fused<128>, dim3(n_head), dim3(1024), lds, s, true, true, a, g, n_head_kv);
+        else if (head_dim == 64) launch_k(k_attn_fused<64>, dim3(n_head), dim3(1024), lds, s, true, true, a, g, n_head_kv);
         else return hipErrorInvalidValue;
         return hipGetLastError();
     }
@@ -1543,7 +1560,7 @@ hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int he
 }
 
 hipError_t launch_embed(const EmbArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_embed, dim3((a.cols + 255) / 256), dim3(256), 0, s, a);
+    launch_k(k_embed, dim3((a.cols + 255) / 256), dim3(256), 0, s, true, true, a);
     return hipGetLastError();
 }
 

@@ -198,9 +198,9 @@ class Context:
     KERNEL_CLASSES = ("embed", "qkv", "attention", "attn_output", "ffn_gate_up", "ffn_down", "output")
 
     def profile_kernels(self, first: int, pos0: int, n_steps: int) -> dict:
-        """Per-kernel-class mean device time / algorithmic bytes per launch: each class's
-        launches of one step at pos0 replayed n_steps times from a graph between two HIP
-        events (llmi_profile_kernels).  Consumes no tokens."""
+        """Per-kernel-class mean kernel execution time / algorithmic bytes per launch:
+        each class's launches of n_steps steps at pos0, every launch bracketed by HIP
+        events recorded at kernel start/end (llmi_profile_kernels).  Consumes no tokens."""
         us, by, nl = (C.c_double * 7)(), (C.c_double * 7)(), (C.c_int32 * 7)()
         if lib().llmi_profile_kernels(self._h, int(first), int(pos0), int(n_steps), us, by, nl) != 0:
             raise LlmiError(last_error())

@@ -13,10 +13,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name, seconds, command...
     local name=$1 secs=$2; shift 2
-    echo "== $name"
+    echo "== $name" >&2
     timeout -k 10 "$secs" "$@"
     local rc=$?
-    echo "== $name exit=$rc"
+    echo "== $name exit=$rc" >&2
     return $rc
 }
 step tests 900 python -m pytest tests -m gpu -q -rf > "$OUT/gpu_tests.log" 2>&1
