@@ -177,3 +177,28 @@ def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
         assert g == o
     monkeypatch.setenv("LLMI_ATTN_MODE", "0")
     llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode
+
+
+def test_golden_greedy16_on_gpu(gpu):
+    """The committed 16-step greedy fixture (tests/golden/, oracle device order):
+    GPU logits bit-identical at every step, same ids."""
+    import os
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(here, "greedy16.npz"))
+    prompt = [int(t) for t in z["prompt"]]
+    want = z["logits_device"]
+    m = llmi.Model(os.path.join(here, "tiny-mixed.gguf"))
+    c = llmi.Context(m, n_ctx=64)
+    cur, pos, ids = prompt[0], 0, []
+    for step in range(want.shape[0]):
+        assert c.decode([cur], pos=[pos]) == 0
+        lg = c.logits(-1)
+        assert np.array_equal(lg, want[step]), f"step {step}: max |d| {np.abs(lg - want[step]).max()}"
+        pos += 1
+        if pos < len(prompt):
+            cur = prompt[pos]
+        else:
+            cur = c.greedy(-1)
+            ids.append(cur)
+    assert ids == [int(i) for i in z["ids_device"]]
