@@ -205,7 +205,7 @@ def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
 
 def main(argv=None):
     args = parse(argv)
-    dist = Dist("nccl")
+    dist = Dist(os.environ.get("LLMI_DIST_BACKEND", "nccl"))
     if dist.world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={dist.world}; using WORLD_SIZE")
     n = dist.world

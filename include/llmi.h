@@ -6,9 +6,9 @@
  * proxies HTTP to it (scripts/gateway.py:699-804).  Inside that binary the decode
  * loop is driven through llama.cpp's C API (llama.h, upstream, not vendored).  This
  * header restates that llama.h surface — same names, argument meaning, return codes
- * and ownership rules — for the functions on the decode path, so a
- * llama-server-compatible HTTP shim (llmi/server.py) or any ctypes/cgo caller can
- * bind it the way it would bind libllama.  Structs are llmi's own (llama.h's
+ * and ownership rules — for the functions on the decode path, so the
+ * ctypes binding (llmi/), a llama-server-compatible HTTP front end or any cgo caller
+ * can bind it the way it would bind libllama.  Structs are llmi's own (llama.h's
  * carry many more fields), so this is API-shape compatible, not ABI compatible.
  *
  * Each entry point names the upstream function it replaces and the reference call

@@ -1,0 +1,72 @@
+"""Multi-process (world_size 2, gloo on CPU) coverage of bench.py's N>1 harness: the
+barrier-bracketed timed region, the max-over-ranks time, whole-job aggregation and
+the rank-0 broadcast used for the RCCL unique id.  Replicas only: no data-path
+collective exists to test."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class FakeEngine:
+    """Stands in for LlmiEngine: rank r takes (r+1)*10 ms per run()."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.runs = []
+
+    def warmup(self, n):
+        self.runs.append(("warmup", n))
+
+    def run(self, n):
+        self.runs.append(("run", n))
+        time.sleep(0.01 * (self.rank + 1))
+
+    def sync(self):
+        pass
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import bench
+
+    d = bench.Dist("gloo")
+    eng = FakeEngine(rank)
+    dt, dt_max = bench.timed_decode(eng, d, steps=7, warmup=3)
+    uid = d.bcast_bytes(b"unique-id-from-rank0" if rank == 0 else None)
+    q.put((rank, dt, dt_max, eng.runs, uid))
+    d.close()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_timed_region_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (r0, dt0, max0, runs0, uid0), (r1, dt1, max1, runs1, uid1) = res
+    assert max0 == max1 == pytest.approx(max(dt0, dt1))
+    assert max0 >= 0.02  # the slower rank's 20 ms dominates the job time
+    assert runs0 == runs1 == [("warmup", 3), ("run", 7)]
+    assert uid0 == uid1 == b"unique-id-from-rank0"
