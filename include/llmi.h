@@ -205,7 +205,8 @@ double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint6
 double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps);
 /* Experiment hook: one STORE matvec launch; builds with -DLLMI_EXP_TRACE write per-wave
  * s_memrealtime stamps {entry, after prologue, first pair done, exit, HW_ID,
- * XCC_ID<<32 | pairs} to trace_dev (6 x uint64 per wave, zero-initialised by the caller).
+ * XCC_ID<<32 | pairs, activation arrived, quantized} to trace_dev (8 x uint64 per wave,
+ * zero-initialised by the caller).
  * Returns the requested grid size, < 0 on error. */
 int32_t llmi_trace_matvec(int32_t type, const void* w_dev, int64_t rows, int64_t cols, const float* x_dev, float* y_dev,
                           int32_t mode, uint64_t* trace_dev);

@@ -180,19 +180,20 @@ __device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
     return l;
 }
 
-// workgroup double sum of a matvec workgroup (kMVWaves waves; pairwise tree over waves)
+// workgroup double sum of a matvec workgroup (NW waves; pairwise tree over waves)
+template <int NW = kMVWaves>
 __device__ double block_sum_d(double v, double* red) {
     v = wave_sum_d(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    double r[kMVWaves];
+    double r[NW];
 #pragma unroll
-    for (int w = 0; w < kMVWaves; ++w) r[w] = red[w];
+    for (int w = 0; w < NW; ++w) r[w] = red[w];
 #pragma unroll
-    for (int o = 1; o < kMVWaves; o <<= 1)
+    for (int o = 1; o < NW; o <<= 1)
 #pragma unroll
-        for (int w = 0; w + o < kMVWaves; w += 2 * o) r[w] = r[w] + r[w + o];
+        for (int w = 0; w + o < NW; w += 2 * o) r[w] = r[w] + r[w + o];
     return r[0];
 }
 
@@ -285,12 +286,12 @@ struct ProRegs {
     float x[NP][16];
     float w[NORM ? NP : 1][16];
 };
-template <bool NORM, int NP>
+template <bool NORM, int NP, int NT = kMVThreads>
 __device__ __forceinline__ void mv_prologue_issue(const MVArgs& A, ProRegs<NORM, NP>& R) {
     const int nsub = A.cols / 16;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-        const int sb = min((int)threadIdx.x + i * kMVThreads, nsub - 1);
+        const int sb = min((int)threadIdx.x + i * NT, nsub - 1);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
@@ -327,7 +328,7 @@ __device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM, NP
         }
     }
 }
-template <int ACT, bool NORM, int NP>
+template <int ACT, bool NORM, int NP, int NT = kMVThreads>
 __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
     const int tid = threadIdx.x, cols = A.cols;
     const int nsub = cols / 16;
@@ -336,23 +337,23 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
         double s = 0.0;
 #pragma unroll
         for (int i = 0; i < NP; ++i)  // register-held sub-blocks (static indices)
-            if (tid + i * kMVThreads < nsub) {
+            if (tid + i * NT < nsub) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) s += (double)(R.x[i][j] * R.x[i][j]);
             }
-        for (int sb = tid + NP * kMVThreads; sb < nsub; sb += kMVThreads) {  // rest (cols > NP*16*threads)
+        for (int sb = tid + NP * NT; sb < nsub; sb += NT) {  // rest (cols > NP*16*threads)
             float v[16], w[16];
             load_sub<NORM, NP>(A, R, NP, sb, v, w);
 #pragma unroll
             for (int j = 0; j < 16; ++j) s += (double)(v[j] * v[j]);
         }
-        s = block_sum_d(s, L.red);
+        s = block_sum_d<NT / 64>(s, L.red);
         const float mean = (float)(s / (double)cols);
         scale = 1.0f / sqrtf(mean + A.eps);
     }
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-        const int sb = tid + i * kMVThreads;
+        const int sb = tid + i * NT;
         if (sb < nsub) {
             float v[16];
 #pragma unroll
@@ -363,7 +364,7 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
             quant_sub<ACT>(L, cols, sb, v);
         }
     }
-    for (int sb = tid + NP * kMVThreads; sb < nsub; sb += kMVThreads) {
+    for (int sb = tid + NP * NT; sb < nsub; sb += NT) {
         float v[16], w[16];
         load_sub<NORM, NP>(A, R, NP, sb, v, w);
         if constexpr (NORM) {
@@ -721,7 +722,7 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
 
 #if defined(LLMI_EXP_TRACE)
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long tr1 = 0, tr2 = 0;
+    unsigned long long tr1 = 0, tr2 = 0, tr_x = 0, tr_q = 0;
     int tr_items = 0;
 #endif
     int p = blockIdx.x * kMVWaves + wave;
@@ -730,6 +731,9 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     bool pipe = false;
     ProRegs<NORM, NP> R;
     mv_prologue_issue<NORM, NP>(A, R);  // activation loads first ...
+#if defined(LLMI_EXP_XFIRST)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // experiment: weights only after x arrived
+#endif
     r = pair_ref<EPI>(A, p < A.npairs ? p : A.npairs - 1);
     pipe = p < A.npairs && r.type == T;
     rows = pair_rows<T>(r, A.cols);
@@ -743,8 +747,16 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         if (!pipe) rows.a = rows.b = dummy;
     }
     PairRaw<T> cur = load_item<T>(rows, lane, nch);
+#if defined(LLMI_EXP_TRACE)
+    // stamp once this wave's activation registers have arrived (forces the wait here)
+    asm volatile("" ::"v"(R.x[0][0]), "v"(R.x[0][15]));
+    tr_x = __builtin_amdgcn_s_memrealtime();
+#endif
 #if !defined(LLMI_EXP_NOPRO)
     mv_prologue_finish<ACT, NORM, NP>(A, L, R);
+#if defined(LLMI_EXP_TRACE)
+    tr_q = __builtin_amdgcn_s_memrealtime();
+#endif
 #else
     if (R.x[0][0] == 1234.5f) L.d[0] = R.x[0][1];
 #endif
@@ -814,9 +826,10 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         unsigned xcc = 0;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        unsigned long long* t = A.trace + ((size_t)blockIdx.x * kMVWaves + wave) * 6;
+        unsigned long long* t = A.trace + ((size_t)blockIdx.x * kMVWaves + wave) * 8;
         t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = __builtin_amdgcn_s_memrealtime();
         t[4] = hw; t[5] = ((unsigned long long)xcc << 32) | (unsigned)tr_items;
+        t[6] = tr_x; t[7] = tr_q;
     }
 #endif
     if constexpr (EPI == EPI_LOGITS) {
@@ -830,6 +843,103 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             unsigned long long b = red[0];
 #pragma unroll
             for (int w = 1; w < kMVWaves; ++w) b = red[w] > b ? red[w] : b;
+            if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
+            if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
+        }
+    }
+}
+
+// K-split matvec for rows longer than one 64-chunk item (NJ = ceil(cols/4096) >= 2:
+// ffn_down, 70B-wide inputs).  A workgroup's 4 waves form 4/KS pair slots of KS waves;
+// the waves of a slot split the pair's items (wave sub takes items sub, sub+KS, ...),
+// so every item of the first pair is in flight during the prologue, instead of one
+// item per wave with the rest fetched serially after it.  Per-lane item values go to
+// LDS; the slot's wave 0 adds them in item order starting from 0.f — exactly the
+// single-wave loop's `acc += item value` sequence, so the fp32 association (the
+// oracle's device order) is unchanged — then runs the butterfly and the epilogue.
+// LDS part buffer double-buffered by round: one barrier per round.
+constexpr int kKSThreads = 1024, kKSWaves = kKSThreads / 64;  // one workgroup per CU
+template <int KS>
+__host__ __device__ inline size_t ks_part_bytes(int cols) {
+    const int nj = ((cols >> 6) + 63) >> 6;
+    return (size_t)2 * (kKSWaves / KS) * nj * 128 * sizeof(float);
+}
+__host__ __device__ inline size_t ks_part_off(int act, int cols) { return a16(lds_red_off(act, cols) + kKSWaves * sizeof(double)); }
+
+template <int ACT, bool NORM, int EPI, int T, int NP, int KS>
+__global__ __launch_bounds__(kKSThreads) void k_matvec_ks(MVArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Lds L = carve(smem, ACT, A.cols);
+    float* part = (float*)(smem + ks_part_off(ACT, A.cols));  // [2][PPW][NJ][2][64]
+    constexpr int PPW = kKSWaves / KS;
+    const int wave = uniform((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int slot = wave / KS, sub = wave % KS;
+    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+    const int stride = gridDim.x * PPW;
+    const int rounds = (A.npairs + stride - 1) / stride;
+    int pos = 0;
+    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
+    unsigned long long best = 0;
+    const uint8_t* xb = (const uint8_t*)A.x;
+    const RowPtr dummy{xb, xb, xb, xb};
+
+    ProRegs<NORM, NP> R;
+    mv_prologue_issue<NORM, NP, kKSThreads>(A, R);  // activation loads first, then this wave's first item
+    int pr = blockIdx.x * PPW + slot;   // this slot's pair in the current round
+    PairRows<T> rows = pair_rows<T>(pair_ref<EPI>(A, pr < A.npairs ? pr : A.npairs - 1), A.cols);
+    if (!(pr < A.npairs && sub < NJ)) rows.a = rows.b = dummy;
+    PairRaw<T> cur = load_item<T>(rows, lane + 64 * (sub < NJ ? sub : 0), nch);
+    mv_prologue_finish<ACT, NORM, NP, kKSThreads>(A, L, R);
+    __syncthreads();
+
+    int buf = 0;
+    for (int rd = 0; rd < rounds; ++rd, pr += stride) {
+        const bool have = pr < A.npairs;
+        float* pb = part + (size_t)(buf * PPW + slot) * NJ * 128;
+        for (int j = sub; j < NJ; j += KS) {
+            // the wave's next item: (pr, j+KS) or (pr+stride, sub); loads always issued
+            int jn = j + KS, prn = pr;
+            PairRows<T> rowsn = rows;
+            if (jn >= NJ) {
+                jn = sub;
+                prn = pr + stride;
+                rowsn = pair_rows<T>(pair_ref<EPI>(A, prn < A.npairs ? prn : A.npairs - 1), A.cols);
+                if (prn >= A.npairs) rowsn.a = rowsn.b = dummy;
+            }
+            const PairRaw<T> nxt = load_item<T>(rowsn, lane + 64 * jn, nch);
+            if (have) {
+                const int ch = lane + 64 * j;
+                const int chc = ch < nch ? ch : nch - 1;
+                const Act act = load_act<ACT>(L, chc, nch);
+                const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
+                pb[j * 128 + lane] = ch < nch ? va : 0.f;
+                pb[j * 128 + 64 + lane] = ch < nch ? vb : 0.f;
+            }
+            cur = nxt;
+            rows = rowsn;
+        }
+        __syncthreads();
+        if (sub == 0 && have) {
+            float acc_a = 0.f, acc_b = 0.f;
+            for (int j = 0; j < NJ; ++j) {
+                acc_a += pb[j * 128 + lane];
+                acc_b += pb[j * 128 + 64 + lane];
+            }
+            epilogue<EPI>(A, pair_ref<EPI>(A, pr), pr, reduce_pair(acc_a, acc_b), pos, best);
+        }
+        buf ^= 1;
+    }
+    if constexpr (EPI == EPI_LOGITS) {
+        const int cur_pos = A.st->pos;
+        unsigned long long* red = (unsigned long long*)L.red;
+        __syncthreads();
+        if (lane == 0) red[wave] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long b = red[0];
+#pragma unroll
+            for (int w = 1; w < kKSWaves; ++w) b = red[w] > b ? red[w] : b;
             if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
             if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
         }
@@ -1382,12 +1492,12 @@ hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int bl
 // idle CUs).  Residency per CU comes from the occupancy query for the instantiation
 // and its LDS, cached per (kernel, LDS bytes, device).
 template <typename K>
-static dim3 resident_grid(K kernel, dim3 grid, size_t lds) {
+static dim3 resident_grid(K kernel, dim3 grid, size_t lds, int threads = kMVThreads) {
     static std::mutex mu;
     static std::map<std::tuple<const void*, size_t, int>, int> cache;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const auto key = std::make_tuple((const void*)kernel, lds, dev);
+    const auto key = std::make_tuple((const void*)kernel, lds, dev * 4096 + threads);
     int cap = 0;
     {
         std::lock_guard<std::mutex> lk(mu);
@@ -1396,7 +1506,7 @@ static dim3 resident_grid(K kernel, dim3 grid, size_t lds) {
             cap = it->second;
         } else {
             int occ = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kMVThreads, lds) != hipSuccess || occ <= 0) occ = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, lds) != hipSuccess || occ <= 0) occ = 1;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
             cap = occ * cus;
             cache.emplace(key, cap);
@@ -1419,8 +1529,37 @@ static int prologue_np(int cols) {
     return per <= 1 ? 1 : per <= 2 ? 2 : 4;
 }
 
+template <int ACT, bool NORM, int T, int EPI, int NP, int KS>
+static hipError_t mv_launch_ks(const MVArgs& a, int max_blocks, hipStream_t s) {
+    auto k = k_matvec_ks<ACT, NORM, EPI, T, NP, KS>;
+    const size_t lds = ks_part_off(ACT, a.cols) + ks_part_bytes<KS>(a.cols);
+    constexpr int PPW = kKSWaves / KS;
+    int blocks = (a.npairs + PPW - 1) / PPW;
+    if (blocks > max_blocks) blocks = max_blocks;
+    launch_k(k, resident_grid(k, dim3(blocks), lds, kKSThreads), dim3(kKSThreads), lds, s, true, true, a);
+    return hipGetLastError();
+}
+
+static thread_local int g_mv_max_blocks = 1024;  // set by launch_matvec
+
+// K-split is taken for rows of >= 2 items when every segment has the pipelined type
+static bool use_ks(const MVArgs& a, int T) {
+    if (((a.cols >> 6) + 63) >> 6 < 2) return false;
+    for (int i = 0; i < a.nseg; ++i)
+        if (a.seg[i].type != T) return false;
+    return true;
+}
+
 template <int ACT, bool NORM, int T, int EPI>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (use_ks(a, T)) {  // one 1024-thread workgroup per CU: NP from 1024 threads
+        const int nj = ((a.cols >> 6) + 63) >> 6;
+        const int per = (a.cols / 16 + kKSThreads - 1) / kKSThreads;
+        const int mb = g_mv_max_blocks;
+        if (per <= 1) return nj >= 4 ? mv_launch_ks<ACT, NORM, T, EPI, 1, 4>(a, mb, s)
+                                     : mv_launch_ks<ACT, NORM, T, EPI, 1, 2>(a, mb, s);
+        return nj >= 4 ? mv_launch_ks<ACT, NORM, T, EPI, 2, 4>(a, mb, s) : mv_launch_ks<ACT, NORM, T, EPI, 2, 2>(a, mb, s);
+    }
     switch (prologue_np(a.cols)) {
         case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
         case 2: return mv_launch<ACT, NORM, T, EPI, 2>(a, grid, lds, s);
@@ -1468,6 +1607,7 @@ static hipError_t mv_dispatch_type(const MVArgs& a, int epi, dim3 grid, size_t l
 }
 
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s) {
+    g_mv_max_blocks = max_blocks;
     if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0) return hipErrorInvalidValue;
     const int act = act_kind(a.seg[0].type);
     for (int i = 1; i < a.nseg; ++i)

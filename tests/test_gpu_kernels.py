@@ -108,7 +108,10 @@ def gpu_matvec(qtype, raw, rows, cols, x, nw=None, eps=1e-5):
     return yd.cpu().numpy()
 
 
-SHAPES = [(2, 256), (7, 512), (130, 1024), (1024, 4096), (333, 14336), (4096, 4096)]
+# cols > 4096 take the K-split kernel (KS=2 for 2-3 items per row, KS=4 for >= 4;
+# 28672 also exercises the prologue's tail loop beyond the register-held sub-blocks)
+SHAPES = [(2, 256), (7, 512), (130, 1024), (1024, 4096), (333, 14336), (4096, 4096), (64, 8192), (130, 5632),
+          (5, 28672), (2048, 14336)]
 
 
 @pytest.mark.parametrize("qtype", QTYPES, ids=[TNAME[t] for t in QTYPES])
@@ -132,8 +135,8 @@ def test_matvec_vs_oracle(gpu, qtype, rows, cols):
 
 
 @pytest.mark.parametrize("qtype", QTYPES, ids=[TNAME[t] for t in QTYPES])
-def test_matvec_fused_rmsnorm(gpu, qtype):
-    rows, cols = 96, 2048
+@pytest.mark.parametrize("rows,cols", [(96, 2048), (70, 8192)])
+def test_matvec_fused_rmsnorm(gpu, qtype, rows, cols):
     rng = np.random.default_rng(11 + qtype)
     raw = random_blocks(qtype, rows, cols, rng)
     x = (rng.standard_normal(cols) * 4).astype(np.float32)

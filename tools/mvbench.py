@@ -24,7 +24,7 @@ rng = np.random.default_rng(0)
 for qt, rows, cols in shapes:
     lb = L.llmi_device_layout_bytes(qt, rows, cols)
     stride = (lb + 4095) // 4096 * 4096
-    n = max(2, int(np.ceil(1.2e9 / stride)))
+    n = int(os.environ.get("MV_NCOPIES", "0")) or max(2, int(np.ceil(1.2e9 / stride)))
     raw = torch.from_numpy(random_blocks(qt, rows, cols, rng)).cuda()
     w = torch.empty(stride * n, dtype=torch.uint8, device="cuda")
     for k in range(n):

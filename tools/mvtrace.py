@@ -39,11 +39,13 @@ for qt, rows, cols in shapes:
         assert L.llmi_repack(qt, P(raw), C.c_void_p(w.data_ptr() + stride * k), rows, cols) == 0
     x = torch.randn(cols, device="cuda")
     y = torch.empty(rows, device="cuda")
+    hot = os.environ.get("MV_HOT") == "1"  # trace a copy just read by the previous launch
     for k in range(n - 1):  # warm code / TLB, leave copy n-1 cold
         L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * k), rows, cols, P(x), P(y), 0, None)
-    tr = torch.zeros(2048 * 16 * 6, dtype=torch.int64, device="cuda")
-    g = L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * (n - 1)), rows, cols, P(x), P(y), 0, P(tr))
-    t = tr.cpu().numpy().reshape(-1, 6)
+    tgt = (n - 2) if hot else (n - 1)
+    tr = torch.zeros(2048 * 16 * 8, dtype=torch.int64, device="cuda")
+    g = L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * tgt), rows, cols, P(x), P(y), 0, P(tr))
+    t = tr.cpu().numpy().reshape(-1, 8)
     t = t[t[:, 0] != 0].astype(np.int64)
     t0 = t[:, 0].min()
     start, pro, first, end = t[:, 0] - t0, t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t0
@@ -52,6 +54,10 @@ for qt, rows, cols in shapes:
           f"({lb / (end.max() * 10e-9) / 1e9:.0f} GB/s over the wave span)")
     print("  start offset us :", pct(start))
     print("  prologue us     :", pct(pro))
+    if (t[:, 6] != 0).any():
+        print("    x arrived     :", pct(t[:, 6] - t[:, 0]))
+        print("    quantized     :", pct(t[:, 7] - t[:, 6]))
+        print("    barrier wait  :", pct(t[:, 1] - t[:, 7]))
     print("  first pair us   :", pct(first[items > 0]))
     print("  exit offset us  :", pct(end))
     print("  pairs per wave  :", np.bincount(items).tolist())
