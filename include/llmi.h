@@ -201,8 +201,11 @@ double llmi_bench_matvec_ex(int32_t type, const void* w_dev, int32_t n_mats, int
 double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint64_t bytes, int32_t reps, int32_t blocks);
 /* Attention microbenchmark: n_kv positions, one launch per layer over >= 512 MB of
  * distinct KV caches, graph-replayed `reps` times; microseconds per launch (< 0 error).
- * mode: 0 auto, 1 fused, 2 split, 3 two-kernel. */
-double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps);
+ * mode: 0 auto, 1 fused, 2 split, 3 two-kernel.  trace_dev != NULL (LLMI_EXP_TRACE
+ * builds): one eager launch on a cold layer writing per-wave s_memrealtime stamps
+ * [kernel][block][wave < 16][4] (zero-initialised, 2*4096*64 uint64); returns 0. */
+double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps,
+                            uint64_t* trace_dev);
 /* Experiment hook: one STORE matvec launch; builds with -DLLMI_EXP_TRACE write per-wave
  * s_memrealtime stamps {entry, after prologue, first pair done, exit, HW_ID,
  * XCC_ID<<32 | pairs, activation arrived, quantized} to trace_dev (8 x uint64 per wave,

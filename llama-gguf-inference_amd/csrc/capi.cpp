@@ -693,7 +693,8 @@ double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint6
 // like a decode step does), one launch per layer captured into a graph, `reps` graph
 // replays timed between two events.  Returns microseconds per launch (incl. the
 // dependent-launch gap), < 0 on error.  mode: attention path (0 auto, 1 fused, 2 split, 3 two-kernel).
-double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps) {
+double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps,
+                            uint64_t* trace_dev) {
     if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || (head_dim != 64 && head_dim != 128) || n_kv <= 0 || reps <= 0) {
         set_err("llmi_bench_attention: bad arguments");
         return -1.0;
@@ -708,7 +709,8 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
         (void)hipFree(kc); (void)hipFree(vc); (void)hipFree(q); (void)hipFree(scores); (void)hipFree(out); (void)hipFree(st);
     };
     if (hipMalloc(&kc, kv_layer * nl * 2) != hipSuccess || hipMalloc(&vc, kv_layer * nl * 2) != hipSuccess ||
-        hipMalloc(&q, (size_t)n_head * head_dim * 4) != hipSuccess || hipMalloc(&scores, (size_t)n_head * n_ctx * 4) != hipSuccess ||
+        hipMalloc(&q, (size_t)n_head * head_dim * 4) != hipSuccess ||
+        hipMalloc(&scores, attn_scratch_floats(n_head, n_ctx) * 4) != hipSuccess ||
         hipMalloc(&out, (size_t)n_head * head_dim * 4) != hipSuccess || hipMalloc(&st, sizeof(StepState)) != hipSuccess) {
         cleanup();
         set_err("llmi_bench_attention: out of device memory");
@@ -727,6 +729,23 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
     AttnArgs a;
     a.q = q; a.scores = scores; a.out = out; a.st = st; a.n_ctx = n_ctx; a.scale = 1.0f / sqrtf((float)head_dim);
+    a.tmax = scores + (size_t)n_head * n_ctx;
+    if (trace_dev) {  // one traced eager launch on a cold layer (LLMI_EXP_TRACE builds)
+        for (int l = 0; l + 1 < nl; ++l) {
+            a.kc = kc + (size_t)l * kv_layer;
+            a.vc = vc + (size_t)l * kv_layer;
+            (void)launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s);
+        }
+        a.kc = kc + (size_t)(nl - 1) * kv_layer;
+        a.vc = vc + (size_t)(nl - 1) * kv_layer;
+        a.trace = (unsigned long long*)trace_dev;
+        const bool okt = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s) == hipSuccess &&
+                         hipStreamSynchronize(s) == hipSuccess;
+        (void)hipStreamDestroy(s);
+        set_attn_mode(0);
+        cleanup();
+        return okt ? 0.0 : -1.0;
+    }
     hipGraph_t g = nullptr;
     hipGraphExec_t ex = nullptr;
     bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;

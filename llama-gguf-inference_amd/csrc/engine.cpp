@@ -278,7 +278,7 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string&
     HIPC(hipMalloc(&c.att, QD * 4));
     HIPC(hipMalloc(&c.h, (size_t)hp.n_ff * 4));
     HIPC(hipMalloc(&c.logits, (size_t)hp.n_vocab * 4));
-    HIPC(hipMalloc(&c.scores, (size_t)hp.n_head * c.n_ctx * 4));
+    HIPC(hipMalloc(&c.scores, attn_scratch_floats(hp.n_head, c.n_ctx) * 4));
     HIPC(hipMalloc(&c.kc, kv_elems * 2));
     HIPC(hipMalloc(&c.vc, kv_elems * 2));
     HIPC(hipMalloc(&c.st, sizeof(StepState)));
@@ -419,6 +419,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         // --- attention ---
         AttnArgs at;
         at.q = c.q; at.kc = a.kc; at.vc = a.vc; at.scores = c.scores; at.out = c.att; at.st = c.st;
+        at.tmax = c.scores + (size_t)hp.n_head * c.n_ctx;
         at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
         LLMI_RUN(K_ATTN, launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);

@@ -16,6 +16,8 @@ constexpr int kMVThreads = LLMI_MV_THREADS;  // matvec workgroup; each wave owns
 constexpr int kMVWaves = kMVThreads / 64;
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
 constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
+// scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
+inline size_t attn_scratch_floats(int n_head, int n_ctx) { return (size_t)n_head * n_ctx + (size_t)n_head * (n_ctx / 32 + 1); }
 
 enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
 
@@ -54,10 +56,12 @@ struct AttnArgs {
     const uint16_t* kc = nullptr;  // layer base
     const uint16_t* vc = nullptr;
     float* scores = nullptr;       // f32[H][n_ctx]
+    float* tmax = nullptr;         // f32[H][n_ctx/32]: per-32-position tile max of the scores
     float* out = nullptr;          // f32[H*D]
     const StepState* st = nullptr;
     int n_ctx = 0;
     float scale = 0.f;
+    unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [kernel][block][wave][4] stamps
 };
 
 struct EmbArgs {

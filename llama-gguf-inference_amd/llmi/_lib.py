@@ -104,7 +104,7 @@ SIGNATURES = {
     "llmi_bench_matvec": (C.c_double, [C.c_int32, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, C.c_int32]),
     "llmi_bench_matvec_ex": (C.c_double, [C.c_int32, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, C.c_int32, C.c_int32]),
     "llmi_trace_matvec": (C.c_int32, [C.c_int32, _P, C.c_int64, C.c_int64, _P, _P, C.c_int32, _P]),
-    "llmi_bench_attention": (C.c_double, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "llmi_bench_attention": (C.c_double, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
 }
 
 _lib = None

@@ -20,7 +20,7 @@ res = {}
 for n in kvs:
     row = {}
     for m in modes:
-        us = L.llmi_bench_attention(H, HK, D, n, m, reps)
+        us = L.llmi_bench_attention(H, HK, D, n, m, reps, None)
         row[m] = round(us, 2)
     kv_bytes = 2 * HK * n * D * 2
     res[n] = row
