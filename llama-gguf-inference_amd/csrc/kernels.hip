@@ -55,11 +55,13 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// Weight loads use the default cache policy: a wave reads each header line from
-// several lanes/instructions, and measured nontemporal loads were 5-25% slower
-// (profiles/r01/mvbench_nt.md).
+// Weight loads are nontemporal (nt): every weight byte is read once per token by one
+// CU, so keeping it in L2/MALL only evicts the activations and KV.  Measured with the
+// statically counted prologue (tools/mvbench.py, graph-replayed): 2-10 % faster on
+// every shape (output 128256x4096 Q6_K: 78.8 -> 70.8 us); end to end 555 -> 581 tok/s.
+// (Before the prologue stopped waiting on vmcnt(0), nt measured slower.)
 #ifndef LLMI_NT
-#define LLMI_NT 0
+#define LLMI_NT 1
 #endif
 constexpr bool kNontemporalWeights = LLMI_NT != 0;
 
@@ -848,6 +850,44 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         }
     }
 }
+
+// Experiment (LLMI_EXP_R1): single-row work items for one-item rows (cols <= 4096),
+// 2 items prefetched per wave.  STORE epilogue only; rows of segment 0.
+#if defined(LLMI_EXP_R1)
+template <int ACT, int T, int NP>
+__global__ __launch_bounds__(kMVThreads) void k_matvec_r1(MVArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Lds L = carve(smem, ACT, A.cols);
+    const int wave = uniform((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int G = gridDim.x * kMVWaves;
+    const int nch = A.cols >> 6;
+    const int rows = A.seg[0].rows;
+    const uint8_t* xb = (const uint8_t*)A.x;
+    const RowPtr dummy{xb, xb, xb, xb};
+    ProRegs<false, NP> R;
+    mv_prologue_issue<false, NP>(A, R);
+    int u = blockIdx.x * kMVWaves + wave;
+    RowPtr r0 = u < rows ? row_ptr<T>(A.seg[0], u, A.cols) : dummy;
+    RowPtr r1 = u + G < rows ? row_ptr<T>(A.seg[0], u + G, A.cols) : dummy;
+    const int c = lane < nch ? lane : nch - 1;
+    Raw w0 = load_chunk<T>(r0, c, nch);
+    Raw w1 = load_chunk<T>(r1, c, nch);
+    mv_prologue_finish<ACT, false, NP>(A, L, R);
+    __syncthreads();
+    const Act act = load_act<ACT>(L, c, nch);
+    for (; u < rows; u += G) {
+        const int u2 = u + 2 * G;
+        const RowPtr r2 = u2 < rows ? row_ptr<T>(A.seg[0], u2, A.cols) : dummy;
+        const Raw w2 = load_chunk<T>(r2, c, nch);
+        const float v = dot_chunk<T>(w0, act, c);
+        const float s = wave_sum(lane < nch ? v : 0.f);
+        if (lane == 0) A.y[u] = s;
+        w0 = w1;
+        w1 = w2;
+    }
+}
+#endif
 
 // K-split matvec for rows longer than one 64-chunk item (NJ = ceil(cols/4096) >= 2:
 // ffn_down, 70B-wide inputs).  A workgroup's 4 waves form 4/KS pair slots of KS waves;
@@ -1754,6 +1794,17 @@ static bool use_ks(const MVArgs& a, int T) {
 
 template <int ACT, bool NORM, int T, int EPI>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+#if defined(LLMI_EXP_R1)
+    if constexpr (EPI == EPI_STORE && !NORM) {
+        if (a.nseg == 1 && a.cols <= 4096 && a.seg[0].type == T) {
+            auto k = k_matvec_r1<ACT, T, 1>;
+            int blocks = (a.seg[0].rows + kMVWaves - 1) / kMVWaves;
+            if (blocks > g_mv_max_blocks) blocks = g_mv_max_blocks;
+            launch_k(k, resident_grid(k, dim3(blocks), lds), dim3(kMVThreads), lds, s, true, true, a);
+            return hipGetLastError();
+        }
+    }
+#endif
     if (use_ks(a, T)) {  // one 1024-thread workgroup per CU: NP from 1024 threads
         const int nj = ((a.cols >> 6) + 63) >> 6;
         const int per = (a.cols / 16 + kKSThreads - 1) / kKSThreads;
