@@ -74,8 +74,14 @@ __device__ __forceinline__ u32x4 ldw(const uint8_t* p) {
     if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x4*)p);
     else return *(const u32x4*)p;
 }
-__device__ __forceinline__ u32x2 ldw8(const uint8_t* p) { return *(const u32x2*)p; }
-__device__ __forceinline__ uint32_t ldw4(const uint8_t* p) { return *(const uint32_t*)p; }
+__device__ __forceinline__ u32x2 ldw8(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x2*)p);
+    else return *(const u32x2*)p;
+}
+__device__ __forceinline__ uint32_t ldw4(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const uint32_t*)p);
+    else return *(const uint32_t*)p;
+}
 __device__ __forceinline__ int dot4(uint32_t a, int b, int c) {
     return __builtin_amdgcn_sdot4((int)a, b, c, false);
 }
@@ -767,6 +773,58 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     tr1 = __builtin_amdgcn_s_memrealtime();
 #endif
 
+#if defined(LLMI_EXP_PF2)
+    if (pipe) {
+        // two items in flight ahead of the one being reduced
+        struct Cur {
+            int p, j;
+            PairRef r;
+            PairRows<T> rows;
+            bool ok;
+        };
+        auto advance = [&](const Cur& c) {
+            Cur n = c;
+            n.j = c.j + 1;
+            if (n.j == NJ) {
+                n.j = 0;
+                n.p = c.p + G;
+                if (n.p < A.npairs) {
+                    n.r = pair_ref<EPI>(A, n.p);
+                    n.rows = pair_rows<T>(n.r, A.cols);
+                }
+            }
+            n.ok = c.ok && n.p < A.npairs && n.r.type == T;
+            return n;
+        };
+        Cur c0{p, 0, r, rows, true};
+        Cur c1 = advance(c0);
+        PairRaw<T> n1 = load_item<T>(c1.ok ? c1.rows : c0.rows, lane + 64 * (c1.ok ? c1.j : c0.j), nch);
+        Cur c2 = advance(c1);
+        float acc_a = 0.f, acc_b = 0.f;
+        for (;;) {
+            const PairRaw<T> n2 = load_item<T>(c2.ok ? c2.rows : c0.rows, lane + 64 * (c2.ok ? c2.j : c0.j), nch);
+            const int ch = lane + 64 * c0.j;
+            const int chc = ch < nch ? ch : nch - 1;
+            const Act act = load_act<ACT>(L, chc, nch);
+            const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
+            acc_a += ch < nch ? va : 0.f;
+            acc_b += ch < nch ? vb : 0.f;
+            if (c0.j == NJ - 1) {
+                epilogue<EPI>(A, c0.r, c0.p, reduce_pair(acc_a, acc_b), pos, best);
+                acc_a = acc_b = 0.f;
+            }
+            if (!c1.ok) {
+                p = c1.p;
+                break;
+            }
+            cur = n1;
+            n1 = n2;
+            c0 = c1;
+            c1 = c2;
+            c2 = advance(c2);
+        }
+    }
+#else
     if (pipe) {
         int j = 0;
         float acc_a = 0.f, acc_b = 0.f;
@@ -815,6 +873,7 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             rows = rowsn;
         }
     }
+#endif
     // remaining pairs of other types (or all pairs if the first was not of type T)
     for (; p < A.npairs; p += G) {
         r = pair_ref<EPI>(A, p);
@@ -1305,7 +1364,7 @@ __global__ __launch_bounds__(256) void k_attn_scores8(AttnArgs a) {
     const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
     u32x4 kv[DQ / 8];
 #pragma unroll
-    for (int i = 0; i < DQ / 8; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
+    for (int i = 0; i < DQ / 8; ++i) kv[i] = __builtin_nontemporal_load((const u32x4*)(kr + 8 * i));  // K read once
     // q rounded to f16 as upstream's KQ mul_mat does, held as double: every k*q product
     // of two f16 values is exact, so fma(k, q, acc) == acc + (double)(k * q)
     __shared__ __attribute__((aligned(16))) double qs[G][D];
@@ -1383,9 +1442,9 @@ __global__ __launch_bounds__(512) void k_attn_pv16(AttnArgs a, int kvb) {
     // V window issued after the score staging (loads return in order: the staging
     // must not queue behind it), in flight during the softmax
     constexpr int NV = 8;  // 8-B V loads in flight per lane: a 1024-position window
-    uint2 vv[NV];
+    u32x2 vv[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) vv[k] = *(const uint2*)(vr + min(4 * sl + 128 * k, kvb - 4));
+    for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(4 * sl + 128 * k, kvb - 4)));
     const int n_kv = a.st->pos + 1;
     const int hh = wave / WPH, wi = wave % WPH;
     {   // row max from the tile maxima (all kv_bound/32 tiles loaded without waiting for
@@ -1456,7 +1515,7 @@ __global__ __launch_bounds__(512) void k_attn_pv16(AttnArgs a, int kvb) {
         t0 += 128 * NV;
         if (t0 >= n_kv) break;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) vv[k] = *(const uint2*)(vr + min(t0 + 128 * k, kvb - 4));
+        for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(t0 + 128 * k, kvb - 4)));
     }
 #pragma unroll
     for (int h = 0; h < G; ++h) {

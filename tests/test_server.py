@@ -190,3 +190,36 @@ def test_version_and_argv():
                            "--api-key-file", "/k", "-t", "8", "--flash-attn"])
     assert (a.model, a.port, a.ctx_size, a.ngl, a.api_key_file, a.threads) == ("/m.gguf", 18080, 16384, 99, "/k", 8)
     assert extra == ["--flash-attn"]
+
+
+def test_gateway_forwarded_bytes(server):
+    """The exact request shape the reference gateway forwards (SURVEY.md §8b capture of
+    scripts/gateway.py:721-745: lowercase client headers, backend Bearer key, Connection:
+    close) sent as raw bytes; the response is status line + headers + body and the
+    server closes the socket (the gateway copies until EOF, gateway.py:776-783)."""
+    import socket
+
+    eng, port = server
+    eng.ready = True
+    body = json.dumps({"messages": [{"role": "user", "content": "Write a short poem about the sea"}],
+                       "max_tokens": 4, "stream": True}).encode()
+    head = (f"POST /v1/chat/completions HTTP/1.1\r\nHost: 127.0.0.1:{port}\r\n"
+            f"content-type: application/json\r\ncontent-length: {len(body)}\r\n"
+            f"Authorization: Bearer {KEY}\r\nConnection: close\r\n\r\n").encode()
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(head + body)
+    chunks = []
+    while True:
+        b = s.recv(65536)
+        if not b:
+            break  # server closed: EOF delimits the response
+        chunks.append(b)
+    s.close()
+    raw = b"".join(chunks).decode()
+    status, rest = raw.split("\r\n", 1)
+    assert status == "HTTP/1.1 200 OK"
+    hdr, payload = rest.split("\r\n\r\n", 1)
+    assert len(hdr) < 64 * 1024  # gateway header-block limit (gateway.py:123)
+    assert "Content-Type: text/event-stream" in hdr and "Connection: close" in hdr
+    events = [e for e in payload.split("\n\n") if e]
+    assert events[-1] == "data: [DONE]" and all(e.startswith("data: ") for e in events)
