@@ -739,9 +739,12 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     bool pipe = false;
     ProRegs<NORM, NP> R;
     mv_prologue_issue<NORM, NP>(A, R);  // activation loads first ...
-#if defined(LLMI_EXP_XFIRST)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // experiment: weights only after x arrived
-#endif
+    // Single-round launches (every wave owns at most one pair: QKV, attn_output) issue
+    // their weights only once the activation has arrived: the activation loads then do
+    // not queue behind the chip-wide weight burst, and the weight latency overlaps the
+    // quantization instead (4096x4096: 5.2 -> 4.7 us).  Multi-round launches keep the
+    // weights in flight from the start.
+    if (A.npairs <= (int)gridDim.x * kMVWaves) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     r = pair_ref<EPI>(A, p < A.npairs ? p : A.npairs - 1);
     pipe = p < A.npairs && r.type == T;
     rows = pair_rows<T>(r, A.cols);
@@ -773,58 +776,6 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     tr1 = __builtin_amdgcn_s_memrealtime();
 #endif
 
-#if defined(LLMI_EXP_PF2)
-    if (pipe) {
-        // two items in flight ahead of the one being reduced
-        struct Cur {
-            int p, j;
-            PairRef r;
-            PairRows<T> rows;
-            bool ok;
-        };
-        auto advance = [&](const Cur& c) {
-            Cur n = c;
-            n.j = c.j + 1;
-            if (n.j == NJ) {
-                n.j = 0;
-                n.p = c.p + G;
-                if (n.p < A.npairs) {
-                    n.r = pair_ref<EPI>(A, n.p);
-                    n.rows = pair_rows<T>(n.r, A.cols);
-                }
-            }
-            n.ok = c.ok && n.p < A.npairs && n.r.type == T;
-            return n;
-        };
-        Cur c0{p, 0, r, rows, true};
-        Cur c1 = advance(c0);
-        PairRaw<T> n1 = load_item<T>(c1.ok ? c1.rows : c0.rows, lane + 64 * (c1.ok ? c1.j : c0.j), nch);
-        Cur c2 = advance(c1);
-        float acc_a = 0.f, acc_b = 0.f;
-        for (;;) {
-            const PairRaw<T> n2 = load_item<T>(c2.ok ? c2.rows : c0.rows, lane + 64 * (c2.ok ? c2.j : c0.j), nch);
-            const int ch = lane + 64 * c0.j;
-            const int chc = ch < nch ? ch : nch - 1;
-            const Act act = load_act<ACT>(L, chc, nch);
-            const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
-            acc_a += ch < nch ? va : 0.f;
-            acc_b += ch < nch ? vb : 0.f;
-            if (c0.j == NJ - 1) {
-                epilogue<EPI>(A, c0.r, c0.p, reduce_pair(acc_a, acc_b), pos, best);
-                acc_a = acc_b = 0.f;
-            }
-            if (!c1.ok) {
-                p = c1.p;
-                break;
-            }
-            cur = n1;
-            n1 = n2;
-            c0 = c1;
-            c1 = c2;
-            c2 = advance(c2);
-        }
-    }
-#else
     if (pipe) {
         int j = 0;
         float acc_a = 0.f, acc_b = 0.f;
@@ -873,7 +824,6 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             rows = rowsn;
         }
     }
-#endif
     // remaining pairs of other types (or all pairs if the first was not of type T)
     for (; p < A.npairs; p += G) {
         r = pair_ref<EPI>(A, p);
@@ -909,44 +859,6 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         }
     }
 }
-
-// Experiment (LLMI_EXP_R1): single-row work items for one-item rows (cols <= 4096),
-// 2 items prefetched per wave.  STORE epilogue only; rows of segment 0.
-#if defined(LLMI_EXP_R1)
-template <int ACT, int T, int NP>
-__global__ __launch_bounds__(kMVThreads) void k_matvec_r1(MVArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Lds L = carve(smem, ACT, A.cols);
-    const int wave = uniform((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    const int G = gridDim.x * kMVWaves;
-    const int nch = A.cols >> 6;
-    const int rows = A.seg[0].rows;
-    const uint8_t* xb = (const uint8_t*)A.x;
-    const RowPtr dummy{xb, xb, xb, xb};
-    ProRegs<false, NP> R;
-    mv_prologue_issue<false, NP>(A, R);
-    int u = blockIdx.x * kMVWaves + wave;
-    RowPtr r0 = u < rows ? row_ptr<T>(A.seg[0], u, A.cols) : dummy;
-    RowPtr r1 = u + G < rows ? row_ptr<T>(A.seg[0], u + G, A.cols) : dummy;
-    const int c = lane < nch ? lane : nch - 1;
-    Raw w0 = load_chunk<T>(r0, c, nch);
-    Raw w1 = load_chunk<T>(r1, c, nch);
-    mv_prologue_finish<ACT, false, NP>(A, L, R);
-    __syncthreads();
-    const Act act = load_act<ACT>(L, c, nch);
-    for (; u < rows; u += G) {
-        const int u2 = u + 2 * G;
-        const RowPtr r2 = u2 < rows ? row_ptr<T>(A.seg[0], u2, A.cols) : dummy;
-        const Raw w2 = load_chunk<T>(r2, c, nch);
-        const float v = dot_chunk<T>(w0, act, c);
-        const float s = wave_sum(lane < nch ? v : 0.f);
-        if (lane == 0) A.y[u] = s;
-        w0 = w1;
-        w1 = w2;
-    }
-}
-#endif
 
 // K-split matvec for rows longer than one 64-chunk item (NJ = ceil(cols/4096) >= 2:
 // ffn_down, 70B-wide inputs).  A workgroup's 4 waves form 4/KS pair slots of KS waves;
@@ -1853,17 +1765,6 @@ static bool use_ks(const MVArgs& a, int T) {
 
 template <int ACT, bool NORM, int T, int EPI>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-#if defined(LLMI_EXP_R1)
-    if constexpr (EPI == EPI_STORE && !NORM) {
-        if (a.nseg == 1 && a.cols <= 4096 && a.seg[0].type == T) {
-            auto k = k_matvec_r1<ACT, T, 1>;
-            int blocks = (a.seg[0].rows + kMVWaves - 1) / kMVWaves;
-            if (blocks > g_mv_max_blocks) blocks = g_mv_max_blocks;
-            launch_k(k, resident_grid(k, dim3(blocks), lds), dim3(kMVThreads), lds, s, true, true, a);
-            return hipGetLastError();
-        }
-    }
-#endif
     if (use_ks(a, T)) {  // one 1024-thread workgroup per CU: NP from 1024 threads
         const int nj = ((a.cols >> 6) + 63) >> 6;
         const int per = (a.cols / 16 + kKSThreads - 1) / kKSThreads;
