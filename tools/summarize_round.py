@@ -74,10 +74,12 @@ with open(os.path.join(out, "SUMMARY.md"), "w") as f:
         f.write(f"| `{n[:90]}` | {c} | {a:.2f} | {mi:.2f} | {ma:.2f} | {p:.1f} |\n")
     if dom_rows:
         n, c, a, *_ = dom_rows[0]
-        f.write(f"\nDominant kernel `{n}`: rocprof average {a:.2f} us -> {alg / (a * 1e-6) / 1e9:.0f} GB/s "
-                f"algorithmic; bench.py live HIP-event figure {bench['roofline']['us_per_launch']} us "
-                f"({bench['roofline']['achieved']} GB/s; the event figure includes the dependent-launch gap "
-                f"between graph-replayed launches).\n")
+        f.write(f"\nDominant kernel `{n}`: rocprof average {a:.2f} us (in-graph decode launches) -> "
+                f"{alg / (a * 1e-6) / 1e9:.0f} GB/s algorithmic.  bench.py's live figure (start/stop events "
+                f"on each launch, llmi_profile_kernels) in the unprofiled run: {plain['roofline']['us_per_launch']} us "
+                f"({plain['roofline']['achieved']} GB/s, {100 * (plain['roofline']['us_per_launch'] / a - 1):+.1f} % vs "
+                f"rocprof); under rocprofv3 the same event figure reads {bench['roofline']['us_per_launch']} us "
+                f"(the profiler's per-launch interception inflates eager event timing).\n")
     if hbm:
         f.write(f"\nHBM traffic (separate `--pmc FETCH_SIZE` pass, {len(dom)} launches): "
                 f"{hbm / 1e6:.2f} MB per launch vs {alg / 1e6:.2f} MB algorithmic "
