@@ -444,7 +444,9 @@ __device__ __forceinline__ Raw load_chunk(const RowPtr& rp, int ch, int nch) {
     r.q0 = ldw(rp.qa + o);
     r.q1 = ldw(rp.qa + o + step);
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
-        r.hdr = ldw(rp.sb + (uint32_t)(ch >> 2) * 16);
+        // the block header is shared by the 4 lanes of a block: default policy (nt loads
+        // of duplicated addresses were fetched once per lane: +24 % FETCH_SIZE)
+        r.hdr = *(const u32x4*)(rp.sb + (uint32_t)(ch >> 2) * 16);
         if constexpr (T == T_Q5_K) r.qh = ldw8(rp.hb + (uint32_t)ch * 8);
     } else if constexpr (T == T_Q6_K) {
         r.hdr = ldw(rp.hb + (uint32_t)ch * 16);
