@@ -49,6 +49,8 @@ struct MVArgs {
     int head_dim = 0, n_rot = 0, n_ctx = 0, nq = 0, nk = 0;
     unsigned long long* argmax = nullptr;  // LOGITS
     unsigned long long* trace = nullptr;   // LLMI_EXP_TRACE builds: per-wave s_memrealtime stamps
+    int split_pairs = 0;                   // two-type launches: pairs of the first type group ...
+    int split_wgs = 0;                     // ... and the workgroups that run them (set by launch_matvec)
 };
 
 struct AttnArgs {

@@ -26,6 +26,7 @@
 //   k_repack_* one-time load-time layout transforms (common.h).
 #include "kernels.h"
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -718,24 +719,23 @@ __device__ __forceinline__ float generic_row_any(int type, const Seg& s, int row
     }
 }
 
+// The matvec of the pair range [pbeg, pend) by waves starting at pair p0 with stride G
+// (one type group of a launch); returns the wave's LOGITS argmax key.
 template <int ACT, bool NORM, int EPI, int T, int NP>
-__global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Lds L = carve(smem, ACT, A.cols);
-    const int wave = uniform((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    const int G = gridDim.x * kMVWaves;
-    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+__device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, int p0, int G, int pbeg, int pend) {
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
+    const int lane = threadIdx.x & 63;
+    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
 
 #if defined(LLMI_EXP_TRACE)
+    const int wave = threadIdx.x >> 6;
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long tr1 = 0, tr2 = 0, tr_x = 0, tr_q = 0;
     int tr_items = 0;
 #endif
-    int p = blockIdx.x * kMVWaves + wave;
+    int p = p0;
     PairRef r;
     PairRows<T> rows;
     bool pipe = false;
@@ -746,9 +746,9 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     // not queue behind the chip-wide weight burst, and the weight latency overlaps the
     // quantization instead (4096x4096: 5.2 -> 4.7 us).  Multi-round launches keep the
     // weights in flight from the start.
-    if (A.npairs <= (int)gridDim.x * kMVWaves) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    r = pair_ref<EPI>(A, p < A.npairs ? p : A.npairs - 1);
-    pipe = p < A.npairs && r.type == T;
+    if (pend - pbeg <= G) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    r = pair_ref<EPI>(A, p < pend ? p : pend - 1);
+    pipe = p < pend && r.type == T;
     rows = pair_rows<T>(r, A.cols);
     // ... then the first weights, in flight during the prologue.  Issued on every path
     // (a wave without a pipelined pair reads a dummy chunk inside x: every plane offset
@@ -789,12 +789,12 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             if (jn == NJ) {
                 jn = 0;
                 pn = p + G;
-                if (pn < A.npairs) {
+                if (pn < pend) {
                     rn = pair_ref<EPI>(A, pn);
                     rowsn = pair_rows<T>(rn, A.cols);
                 }
             }
-            const bool has_next = pn < A.npairs && rn.type == T;
+            const bool has_next = pn < pend && rn.type == T;
             // always issue the prefetch (a valid re-load of the current item if none)
             const PairRaw<T> nxt = load_item<T>(has_next ? rowsn : rows, lane + 64 * (has_next ? jn : j), nch);
             const int ch = lane + 64 * j;
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         }
     }
     // remaining pairs of other types (or all pairs if the first was not of type T)
-    for (; p < A.npairs; p += G) {
+    for (; p < pend; p += G) {
         r = pair_ref<EPI>(A, p);
         const float acc_a = generic_row_any<ACT>(r.sa.type, r.sa, r.ra, A.cols, L);
         const float acc_b = r.vb ? generic_row_any<ACT>(r.sb.type, r.sb, r.rb, A.cols, L) : 0.f;
@@ -845,6 +845,29 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         t[6] = tr_x; t[7] = tr_q;
     }
 #endif
+    return best;
+}
+
+// A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
+// split by workgroup: workgroups [0, split_wgs) run the pairs of type T, the rest the
+// pairs of type T2, each group pipelined in its own type (no divergence in a workgroup).
+template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T>
+__global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Lds L = carve(smem, ACT, A.cols);
+    const int wave = uniform((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    unsigned long long best;
+    if constexpr (T2 == T) {
+        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.npairs);
+    } else {
+        if ((int)blockIdx.x < A.split_wgs)
+            best = mv_body<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
+                                                  A.split_pairs);
+        else
+            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, A.split_pairs + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
+                                                   (gridDim.x - A.split_wgs) * kMVWaves, A.split_pairs, A.npairs);
+    }
     if constexpr (EPI == EPI_LOGITS) {
         // workgroup max of the waves' keys, then one atomic into this workgroup's slot
         const int cur_pos = A.st->pos;
@@ -1738,6 +1761,21 @@ static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t 
     return hipGetLastError();
 }
 
+// Two type groups (pairs [0, split) of type T, [split, npairs) of type T2): the
+// resident grid is dealt to the groups in proportion to their pairs (>= 1 each).
+template <int ACT, bool NORM, int T, int T2, int EPI, int NP>
+static hipError_t mv_launch2(const MVArgs& a0, int split_pairs, dim3 grid, size_t lds, hipStream_t s) {
+    auto k = k_matvec<ACT, NORM, EPI, T, NP, T2>;
+    const dim3 g = resident_grid(k, grid, lds);
+    MVArgs a = a0;
+    a.split_pairs = split_pairs;
+    int w1 = (int)(((long long)g.x * split_pairs + a.npairs / 2) / a.npairs);
+    w1 = w1 < 1 ? 1 : w1 > (int)g.x - 1 ? (int)g.x - 1 : w1;
+    a.split_wgs = w1;
+    launch_k(k, g, dim3(kMVThreads), lds, s, true, true, a);
+    return hipGetLastError();
+}
+
 // prologue sub-blocks per thread held in registers: 1, 2 or 4
 static int prologue_np(int cols) {
     const int per = (cols / 16 + kMVThreads - 1) / kMVThreads;
@@ -1802,8 +1840,36 @@ static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t ld
     return hipErrorInvalidValue;
 }
 
+// QKV whose segments form two contiguous type groups split at an even row: both groups
+// pipelined (k_matvec's T2 path).  Returns hipErrorNotSupported when not applicable.
+template <bool NORM>
+static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (a.nseg < 2 || grid.x < 2) return hipErrorNotSupported;
+    int t1 = a.seg[0].type, t2 = -1, split_row = -1;
+    for (int i = 1; i < a.nseg; ++i) {
+        if (a.seg[i].type == (t2 < 0 ? t1 : t2)) continue;
+        if (t2 >= 0) return hipErrorNotSupported;  // a third group
+        t2 = a.seg[i].type;
+        split_row = a.seg[i].row0 - a.seg[0].row0;
+    }
+    if (t2 < 0 || (split_row & 1) || prologue_np(a.cols) != 1) return hipErrorNotSupported;
+    const int sp = split_row / 2;
+#define LLMI_QKV2(A_, B_)                                                                            \
+    if (t1 == A_ && t2 == B_) return mv_launch2<0, NORM, A_, B_, EPI_QKV, 1>(a, sp, grid, lds, s);
+    if constexpr (NORM) {
+        LLMI_QKV2(T_Q4_K, T_Q6_K) LLMI_QKV2(T_Q4_K, T_Q5_K) LLMI_QKV2(T_Q5_K, T_Q6_K)
+    }
+#undef LLMI_QKV2
+    return hipErrorNotSupported;
+}
+
 template <bool NORM>
 static hipError_t mv_dispatch_type(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
+    static const bool qkv2 = !getenv("LLMI_NO_QKV2");  // A/B switch for measurements
+    if (epi == EPI_QKV && qkv2) {
+        const hipError_t e = mv_dispatch_qkv2<NORM>(a, grid, lds, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     // primary (pipelined) type = the type owning the most rows of the launch
     int best = a.seg[0].type, best_rows = 0;
     for (int i = 0; i < a.nseg; ++i) {
