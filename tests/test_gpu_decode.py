@@ -129,9 +129,10 @@ def test_decode_error_codes(gpu, tiny_models):
 
 
 @pytest.mark.parametrize("preset,n_layer,n_vocab", [("llama3-8b-q4km", 2, 0), ("tinyllama-q8_0", 2, 0),
-                                                    ("mistral7b-q5km", 2, 0)])
+                                                    ("mistral7b-q5km", 2, 0), ("llama3-70b-q4km", 2, 32000)])
 def test_decode_parity_real_widths(gpu, synth_dir, preset, n_layer, n_vocab):
-    """Exact Llama-3-8B / TinyLlama / Mistral widths (E, FF, heads, vocab), 2 layers."""
+    """Exact Llama-3-8B / TinyLlama / Mistral / Llama-3-70B widths (E, FF, heads; 70B:
+    E 8192 -> the K-split path on every matvec, GQA 8, Q5_K and Q6_K attn_v), 2 layers."""
     path = str(synth_dir / f"{preset}-L{n_layer}.gguf")
     llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=n_layer, n_vocab=n_vocab)
     prompt = [1, 100, 2000, 31000]
