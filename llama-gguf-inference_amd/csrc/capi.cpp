@@ -730,14 +730,19 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     AttnArgs a;
     a.q = q; a.scores = scores; a.out = out; a.st = st; a.n_ctx = n_ctx; a.scale = 1.0f / sqrtf((float)head_dim);
     a.tmax = scores + (size_t)n_head * n_ctx;
+    a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
+    a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);
+    (void)hipMemset(scores, 0, attn_scratch_floats(n_head, n_ctx) * 4);
     if (trace_dev) {  // one traced eager launch on a cold layer (LLMI_EXP_TRACE builds)
         for (int l = 0; l + 1 < nl; ++l) {
             a.kc = kc + (size_t)l * kv_layer;
             a.vc = vc + (size_t)l * kv_layer;
+            a.layer = l % 255;
             (void)launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s);
         }
         a.kc = kc + (size_t)(nl - 1) * kv_layer;
         a.vc = vc + (size_t)(nl - 1) * kv_layer;
+        a.layer = (nl - 1) % 255;
         a.trace = (unsigned long long*)trace_dev;
         const bool okt = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s) == hipSuccess &&
                          hipStreamSynchronize(s) == hipSuccess;
@@ -749,9 +754,12 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     hipGraph_t g = nullptr;
     hipGraphExec_t ex = nullptr;
     bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    // a new step sequence number per replay: k_attn_x's hand-off tags never repeat
+    ok = ok && launch_state_tick(st, s) == hipSuccess;
     for (int l = 0; ok && l < nl; ++l) {
         a.kc = kc + (size_t)l * kv_layer;
         a.vc = vc + (size_t)l * kv_layer;
+        a.layer = l % 255;
         ok = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s) == hipSuccess;
     }
     ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;

@@ -111,7 +111,7 @@ struct StepState {
     int32_t pos_next;        // position of the next step
     int32_t pos;             // position of the current step (written by k_embed)
     int32_t token;           // token of the current step
-    int32_t pad;
+    uint32_t seq;            // step sequence number (k_embed increments; in-launch hand-off tags)
     unsigned long long key[2][64];  // per-parity argmax key slots: (ordered logit << 32) | (0xffffffff - row)
 };
 constexpr int kArgSlots = 64;

@@ -312,6 +312,9 @@ void context_clear(Context& c) {
     (void)hipMemsetAsync(c.kc, 0, kv_elems * 2, c.stream);
     (void)hipMemsetAsync(c.vc, 0, kv_elems * 2, c.stream);
     (void)hipMemsetAsync(c.hist, 0, (size_t)c.n_ctx * 4, c.stream);
+    // attention scratch incl. k_attn_x's granules: the step sequence restarts at 0 below,
+    // so no granule of an earlier sequence may keep a tag the new one will use
+    (void)hipMemsetAsync(c.scores, 0, attn_scratch_floats(hp.n_head, c.n_ctx) * 4, c.stream);
     StepState s0{};
     s0.token_in = -1;
     s0.token_in_pos = -1;
@@ -371,7 +374,17 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     ea.cols = E; ea.vocab = hp.n_vocab; ea.x = c.x; ea.st = c.st; ea.hist = c.hist; ea.n_ctx = c.n_ctx;
     Prof* P = c.prof;
     const double kvpos = (double)hp.n_head_kv * D * 2.0;  // bytes of K (or V) per layer per position
-    auto want = [P](int k) { return !P || P->want(k); };
+    // experiment hook (timing only, results garbage): LLMI_EXP_SKIP = bitmask of kernel
+    // classes left out of the step, to measure each class's marginal cost in the pipeline
+    static const int exp_skip = [] {
+        const char* e = getenv("LLMI_EXP_SKIP");
+        return e ? atoi(e) : 0;
+    }();
+    static const int exp_xfirst = [] {
+        const char* e = getenv("LLMI_EXP_XFIRST");
+        return e ? atoi(e) : 0;
+    }();
+    auto want = [P](int k) { return !(exp_skip >> k & 1) && (!P || P->want(k)); };
     // a filtered launch, armed with an event pair when the profiler asks for timing
 #define LLMI_RUN(K, EXPR)                                  \
     do {                                                   \
@@ -393,7 +406,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m.layers[(size_t)l];
         // --- QKV + RoPE + KV write (grouped by activation kind) ---
-        MVArgs a;
+        MVArgs a; a.xfirst = exp_xfirst >> 0 & 1;
         a.cols = E; a.x = c.x; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps; a.y = c.q;
         a.kc = c.kc + l * kv_layer; a.vc = c.vc + l * kv_layer; a.rope = c.rope; a.st = c.st;
         a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = nq; a.nk = nk;
@@ -421,22 +434,25 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         at.q = c.q; at.kc = a.kc; at.vc = a.vc; at.scores = c.scores; at.out = c.att; at.st = c.st;
         at.tmax = c.scores + (size_t)hp.n_head * c.n_ctx;
         at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
+        at.layer = l;
+        at.gran = (unsigned long long*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx));
+        at.fault = (unsigned*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx) + 2 * (size_t)hp.n_head * kXAttnMaxKV);
         LLMI_RUN(K_ATTN, launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---
-        MVArgs o;
+        MVArgs o; o.xfirst = exp_xfirst >> 1 & 1;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
         LLMI_RUN(K_ATTN_OUT, launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
         if (P) P->add(K_ATTN_OUT, (double)L.wo.bytes + 4.0 * nq + 8.0 * E);
         // --- gate/up + SwiGLU ---
-        MVArgs gu;
+        MVArgs gu; gu.xfirst = exp_xfirst >> 2 & 1;
         gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2;
         gu.cols = E; gu.x = c.x; gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps;
         gu.y = c.h; gu.npairs = hp.n_ff;
         LLMI_RUN(K_FFN_GATE_UP, launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
         if (P) P->add(K_FFN_GATE_UP, (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff);
         // --- down + residual ---
-        MVArgs dn;
+        MVArgs dn; dn.xfirst = exp_xfirst >> 3 & 1;
         dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
         LLMI_RUN(K_FFN_DOWN, launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
         if (P) P->add(K_FFN_DOWN, (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E);

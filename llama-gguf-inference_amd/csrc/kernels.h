@@ -16,8 +16,13 @@ constexpr int kMVThreads = LLMI_MV_THREADS;  // matvec workgroup; each wave owns
 constexpr int kMVWaves = kMVThreads / 64;
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
 constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
+constexpr int kXAttnMaxKV = 1024;  // one-launch exchange attention (k_attn_x) up to this KV bound
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
-inline size_t attn_scratch_floats(int n_head, int n_ctx) { return (size_t)n_head * n_ctx + (size_t)n_head * (n_ctx / 32 + 1); }
+// + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
+inline size_t attn_gran_off(int n_head, int n_ctx) {
+    return ((size_t)n_head * n_ctx + (size_t)n_head * (n_ctx / 32 + 1) + 3) & ~(size_t)3;
+}
+inline size_t attn_scratch_floats(int n_head, int n_ctx) { return attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV + 4; }
 
 enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
 
@@ -51,6 +56,7 @@ struct MVArgs {
     unsigned long long* trace = nullptr;   // LLMI_EXP_TRACE builds: per-wave s_memrealtime stamps
     int split_pairs = 0;                   // two-type launches: pairs of the first type group ...
     int split_wgs = 0;                     // ... and the workgroups that run them (set by launch_matvec)
+    int xfirst = 0;                        // experiment: multi-round launches also wait for x before weights
 };
 
 struct AttnArgs {
@@ -63,6 +69,9 @@ struct AttnArgs {
     const StepState* st = nullptr;
     int n_ctx = 0;
     float scale = 0.f;
+    int layer = 0;                        // k_attn_x: hand-off tag = step seq * 256 + layer + 1
+    unsigned long long* gran = nullptr;   // k_attn_x: [H][kXAttnMaxKV] {tag, score} granules
+    unsigned* fault = nullptr;            // k_attn_x: set when a bounded wait timed out
     unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [kernel][block][wave][4] stamps
 };
 
@@ -83,7 +92,8 @@ size_t mv_lds_bytes(int act, int cols);
 // All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t stream);
 // attention path for a KV bound: 1 fused (one WG per head), 2 split (scores + PV over
-// (group, 8-dim slice) workgroups), 3 two-kernel long-context path
+// (group, 16-dim slice) workgroups), 3 two-kernel long-context path, 4 one-launch
+// exchange (k_attn_x: scores tiles + granule hand-off + PV, kv_bound <= kXAttnMaxKV)
 int attn_path(int n_head, int n_head_kv, int kv_bound);
 // arm (or with nullptrs disarm) per-op kernel timing events for this thread's launches
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
@@ -96,5 +106,6 @@ hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);
 hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int blocks, hipStream_t stream);
 hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream_t stream);
+hipError_t launch_state_tick(StepState* st, hipStream_t stream);  // seq += 1 (microbenchmarks)
 
 }  // namespace llmi

@@ -224,23 +224,25 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
     int q[16];
     uint8_t* dst;
     if constexpr (ACT == 0) {
-        float am = 0.f, mv = 0.f;
-        int gi = sb * 16;
+        // max |y| of the Q8_K block (order-free), then the SIGNED value ggml keeps: the
+        // first element (lowest index) whose |y| equals it ('if (ax > amax)' scan).  Key =
+        // (index within the block) * 2 + sign, minimised over the 16 lanes of the block.
+        float am = 0.f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float ax = fabsf(v[j]);
-            if (ax > am) { am = ax; mv = v[j]; gi = sb * 16 + j; }
-        }
-        // 16-lane (one Q8_K block) arg-max of |y|, first index wins; each step compares
-        // with the (uniform-so-far) partner group, so mirror partners are exact
-#define LLMI_AMAX_STEP(O)                                                                  \
-        {                                                                                  \
-            const float am2 = xor_partner<O>(am), mv2 = xor_partner<O>(mv);                \
-            const int gi2 = xor_partner_i<O>(gi);                                          \
-            if (am2 > am || (am2 == am && gi2 < gi)) { am = am2; mv = mv2; gi = gi2; }     \
-        }
-        LLMI_AMAX_STEP(1) LLMI_AMAX_STEP(2) LLMI_AMAX_STEP(4) LLMI_AMAX_STEP(8)
-#undef LLMI_AMAX_STEP
+        for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+        am = fmaxf(am, xor_partner<1>(am));
+        am = fmaxf(am, xor_partner<2>(am));
+        am = fmaxf(am, xor_partner<4>(am));
+        am = fmaxf(am, xor_partner<8>(am));
+        int key = 0x7fffffff;
+#pragma unroll
+        for (int j = 15; j >= 0; --j)
+            key = fabsf(v[j]) == am ? (((sb & 15) * 16 + j) << 1) | (v[j] < 0.f ? 1 : 0) : key;
+        key = min(key, xor_partner_i<1>(key));
+        key = min(key, xor_partner_i<2>(key));
+        key = min(key, xor_partner_i<4>(key));
+        key = min(key, xor_partner_i<8>(key));
+        const float mv = (key & 1) ? -am : am;
         float dval = 0.f;
         int bsum = 0;
         if (am == 0.f) {
@@ -746,7 +748,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     // not queue behind the chip-wide weight burst, and the weight latency overlaps the
     // quantization instead (4096x4096: 5.2 -> 4.7 us).  Multi-round launches keep the
     // weights in flight from the start.
-    if (pend - pbeg <= G) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pend - pbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     r = pair_ref<EPI>(A, p < pend ? p : pend - 1);
     pipe = p < pend && r.type == T;
     rows = pair_rows<T>(r, A.cols);
@@ -922,6 +924,7 @@ __global__ __launch_bounds__(kKSThreads) void k_matvec_ks(MVArgs A) {
 
     ProRegs<NORM, NP> R;
     mv_prologue_issue<NORM, NP, kKSThreads>(A, R);  // activation loads first, then this wave's first item
+    if (A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int pr = blockIdx.x * PPW + slot;   // this slot's pair in the current round
     PairRows<T> rows = pair_rows<T>(pair_ref<EPI>(A, pr < A.npairs ? pr : A.npairs - 1), A.cols);
     if (!(pr < A.npairs && sub < NJ)) rows.a = rows.b = dummy;
@@ -1467,6 +1470,219 @@ __global__ __launch_bounds__(512) void k_attn_pv16(AttnArgs a, int kvb) {
     LLMI_ATT_STAMP(1, 3)
 }
 
+// One-launch exchange attention for short contexts (kv_bound <= kXAttnMaxKV): grid
+// (HK, D/16), 512 threads.  Workgroup (g, j) computes the scores of position tile j
+// (64*NP positions; 8 lanes x D/8 dims per position, exact f16 products in double as
+// k_attn_scores8) and publishes them as 8-byte {tag, score} granules (one relaxed
+// agent-scope store each: the data is the flag, no fence; MI355X_MICROARCH.md
+// "R2 granules").  Every workgroup of the group then sweeps all G x n_kv granules of
+// its group until their tags match this step's (tag = step seq * 256 + layer + 1, read
+// from device state at run time, so graph replays never see a previous step's
+// granules), and runs k_attn_pv16's softmax and PV for its 16 output dims.  One
+// launch and one hand-off replace the scores -> PV kernel boundary; K and V loads are
+// issued before the position is known.  Every spin is bounded: a timed-out wait writes
+// NaN outputs and sets *a.fault instead of hanging the GPU.
+constexpr int kXSpinLimit = 1 << 22;
+typedef unsigned long long __attribute__((address_space(1))) gu64;
+template <int D, int G, int NP>
+__global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
+    LLMI_ATT_STAMP(0, 0)
+    extern __shared__ __attribute__((aligned(16))) float spx[];  // [G][kvb] probabilities
+    __shared__ __attribute__((aligned(16))) double qs[G][D];
+    __shared__ float redm[8];
+    __shared__ double reds[8];
+    __shared__ int s_fault;
+    constexpr int WPH = 8 / G;             // waves per head (softmax)
+    constexpr int DQ = D / 8;              // dims per lane in the scores
+    constexpr int NS = kXAttnMaxKV / (WPH * 64);  // max positions per lane in the softmax
+    const int g = blockIdx.x, j = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // 1. step state and q first (they gate everything), then this tile's K rows (NP
+    // passes of 64 positions), then this workgroup's V window: loads complete in issue
+    // order, so nothing early waits behind the K/V stream
+    const int pos = a.st->pos;
+    const uint32_t seq = a.st->seq;
+    float qv[(G * D + 511) / 512];
+#pragma unroll
+    for (int k = 0; k < (G * D + 511) / 512; ++k) qv[k] = a.q[(size_t)g * G * D + min(tid + 512 * k, G * D - 1)];
+    const int qd = tid & 7;
+    const int tile0 = j * 64 * NP;
+    u32x4 kv[NP][DQ / 8];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int t = min(tile0 + p * 64 + (tid >> 3), kvb - 1);
+        const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = __builtin_nontemporal_load((const u32x4*)(kr + 8 * i));
+    }
+    const int d = j * 16 + (tid >> 5), sl = tid & 31;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    constexpr int NV = 8;  // 8-B V loads in flight per lane: a 1024-position window
+    u32x2 vv[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(4 * sl + 128 * k, kvb - 4)));
+#pragma unroll
+    for (int k = 0; k < (G * D + 511) / 512; ++k)
+        if (tid + 512 * k < G * D) qs[(tid + 512 * k) / D][(tid + 512 * k) % D] = (double)(float)(_Float16)qv[k];
+    if (tid == 0) s_fault = 0;
+    const int n_kv = pos + 1;
+    const uint32_t tag = seq * 256u + (uint32_t)a.layer + 1u;
+    __syncthreads();
+    LLMI_ATT_STAMP(0, 1)
+    // 2. scores of the tile -> granules
+    gu64* gr = (gu64*)a.gran + (size_t)g * G * kXAttnMaxKV;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int t = tile0 + p * 64 + (tid >> 3);
+        if (tile0 + p * 64 >= n_kv) break;  // uniform
+        double acc[G];
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) {
+            const int d0 = qd * DQ + 8 * i;
+            double k[8];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                k[2 * jj] = (double)h2f((uint16_t)kv[p][i][jj]);
+                k[2 * jj + 1] = (double)h2f((uint16_t)(kv[p][i][jj] >> 16));
+            }
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh)
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) acc[hh] = __builtin_fma(k[jj], qs[hh][d0 + jj], acc[hh]);
+        }
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            acc[hh] += xor_partner_d<1>(acc[hh]);
+            acc[hh] += xor_partner_d<2>(acc[hh]);
+            acc[hh] += xor_partner_d<4>(acc[hh]);
+            if (t < n_kv && qd == (hh & 7)) {
+                const float sc = (float)acc[hh] * a.scale;
+                __hip_atomic_store(gr + (size_t)hh * kXAttnMaxKV + t,
+                                   ((unsigned long long)tag << 32) | __float_as_uint(sc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    LLMI_ATT_STAMP(0, 2)
+    // 3. sweep: lane (head hh, wave wi of the head) owns positions wi*64 + lane + k*WPH*64,
+    // the softmax's own mapping, so the scores stay in registers.  All of a lane's
+    // granule loads are issued together; only stragglers are re-read (bounded spin).
+    const int hh = wave / WPH, wi = wave % WPH;
+    const gu64* gh = gr + (size_t)hh * kXAttnMaxKV;
+    float sv[NS];
+    {
+        unsigned long long x[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const int t = wi * 64 + lane + k * WPH * 64;
+            x[k] = t < n_kv ? __hip_atomic_load(gh + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : ((unsigned long long)tag << 32);
+        }
+        for (int spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) ok &= (uint32_t)(x[k] >> 32) == tag;
+            if (__all(ok)) break;
+            if (spins > kXSpinLimit) {
+                s_fault = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                const int t = wi * 64 + lane + k * WPH * 64;
+                if ((uint32_t)(x[k] >> 32) != tag && t < n_kv)
+                    x[k] = __hip_atomic_load(gh + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k) sv[k] = __uint_as_float((uint32_t)x[k]);
+    }
+    LLMI_ATT_STAMP(0, 3)
+    // 4. softmax as k_attn_pv16: row max (exact in any order), e = expf(s - max) with a
+    // double sum (waves combined in fixed order), p = f16(e / sum) into LDS
+    {
+        float m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (wi * 64 + lane + k * WPH * 64 < n_kv) m = fmaxf(m, sv[k]);
+        m = wave_max(m);
+        if (lane == 0) redm[wave] = m;
+    }
+    __syncthreads();
+    float mx = redm[hh * WPH];
+#pragma unroll
+    for (int i = 1; i < WPH; ++i) mx = fmaxf(mx, redm[hh * WPH + i]);
+    double sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+        if (wi * 64 + lane + k * WPH * 64 < n_kv) {
+            sv[k] = llmi_expf(sv[k] - mx);
+            sum += (double)sv[k];
+        }
+    sum = wave_sum_d(sum);
+    if (lane == 0) reds[wave] = sum;
+    __syncthreads();
+    double tot = reds[hh * WPH];
+#pragma unroll
+    for (int i = 1; i < WPH; ++i) tot += reds[hh * WPH + i];
+    const float inv = (float)(1.0 / tot);
+    float* sp = spx + hh * kvb;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const int t = wi * 64 + lane + k * WPH * 64;
+        if (t < n_kv) sp[t] = (float)(_Float16)(sv[k] * inv);
+        else if (t < ((n_kv + 3) & ~3)) sp[t] = 0.f;
+    }
+    __syncthreads();
+    LLMI_ATT_STAMP(1, 0)
+    // 5. PV for dims [16j, 16j+16): as k_attn_pv16
+    double acc[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) acc[h] = 0.0;
+    for (int t0 = 4 * sl;;) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int tb = t0 + 128 * k;
+            if (tb < n_kv) {
+                double v[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float f = h2f((uint16_t)((jj < 2 ? vv[k].x : vv[k].y) >> (16 * (jj & 1))));
+                    v[jj] = tb + jj < n_kv ? (double)f : 0.0;
+                }
+#pragma unroll
+                for (int h = 0; h < G; ++h) {
+                    const float4 p = *(const float4*)(spx + h * kvb + tb);
+                    acc[h] = __builtin_fma(v[0], (double)p.x, acc[h]);
+                    acc[h] = __builtin_fma(v[1], (double)p.y, acc[h]);
+                    acc[h] = __builtin_fma(v[2], (double)p.z, acc[h]);
+                    acc[h] = __builtin_fma(v[3], (double)p.w, acc[h]);
+                }
+            }
+        }
+        t0 += 128 * NV;
+        if (t0 >= n_kv) break;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(t0 + 128 * k, kvb - 4)));
+    }
+    LLMI_ATT_STAMP(1, 1)
+    const bool fault = s_fault != 0;
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        double v = acc[h];
+        v += xor_partner_d<1>(v);
+        v += xor_partner_d<2>(v);
+        v += xor_partner_d<4>(v);
+        v += xor_partner_d<8>(v);
+        v += xor_partner_d<16>(v);
+        if (sl == 0) a.out[(size_t)(g * G + h) * D + d] = fault ? __uint_as_float(0x7fc00000u) : (float)v;
+    }
+    if (fault && tid == 0) atomicOr(a.fault, 1u);
+}
+
 // Fused single-launch attention for KV lengths that fit in LDS (kv_bound <= 8192):
 // one 1024-thread workgroup per query head; scores, softmax statistics and the
 // f16-rounded probabilities stay in LDS, so the only global traffic is one K and one V
@@ -1619,11 +1835,19 @@ __global__ __launch_bounds__(256) void k_embed(EmbArgs a) {
         if (threadIdx.x == 0) {
             st->pos = pos;
             st->token = tok;
+            st->seq = st->seq + 1u;  // tags of this step's in-launch hand-offs (k_attn_x)
             if (pos >= 0 && pos < a.n_ctx) a.hist[pos] = tok;
         }
     }
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e < a.cols) a.x[e] = dequant_elem(a.w, tok, e, a.cols);
+}
+
+__global__ void k_state_tick(StepState* st) { st->seq = st->seq + 1u; }
+
+hipError_t launch_state_tick(StepState* st, hipStream_t s) {
+    hipLaunchKernelGGL(k_state_tick, dim3(1), dim3(1), 0, s, st);
+    return hipGetLastError();
 }
 
 __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
@@ -1947,22 +2171,56 @@ static hipError_t attn_split_g(const AttnArgs& a, int g, int hk, int kv_bound, h
     return hipGetLastError();
 }
 
-static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel (experiments: LLMI_ATTN_MODE)
+// exchange attention: K tile passes for a KV bound (tiles of 64*NP positions cover
+// kv_bound with D/16 workgroups per group); 0 = not applicable
+static int attn_x_np(int head_dim, int kv_bound) {
+    const int nw = head_dim / 16;
+    const int np = (kv_bound + nw * 64 - 1) / (nw * 64);
+    if (kv_bound > kXAttnMaxKV) return 0;
+    return np <= 1 ? 1 : np <= 2 ? 2 : np <= 4 ? 4 : 0;
+}
+
+template <int D>
+static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipStream_t s) {
+    const int np = attn_x_np(D, kv_bound);
+    const dim3 grid(hk, D / 16);
+    const size_t lds = (size_t)g * kv_bound * 4;
+#define LLMI_ATTX(G, NPV) \
+    if (g == G && np == NPV) { launch_k(k_attn_x<D, G, NPV>, grid, dim3(512), lds, s, true, true, a, kv_bound); return hipGetLastError(); }
+#define LLMI_ATTX_G(G) LLMI_ATTX(G, 1) LLMI_ATTX(G, 2) LLMI_ATTX(G, 4)
+    LLMI_ATTX_G(1) LLMI_ATTX_G(2) LLMI_ATTX_G(4) LLMI_ATTX_G(8)
+#undef LLMI_ATTX_G
+#undef LLMI_ATTX
+    return hipErrorInvalidValue;
+}
+
+static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel, 4 exchange (experiments: LLMI_ATTN_MODE)
 void set_attn_mode(int mode) { g_attn_mode = mode; }
 int attn_path(int n_head, int n_head_kv, int kv_bound) {
     const int g = n_head / n_head_kv;
     const bool split_ok = (size_t)g * kv_bound * 4 <= kSplitAttnMaxLds;
     const bool fused_ok = kv_bound <= kFusedAttnMaxKV;
+    (void)n_head;
+    if (g_attn_mode == 4 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
     if (g_attn_mode == 1 && fused_ok) return 1;
     if (g_attn_mode == 2 && split_ok) return 2;
     if (g_attn_mode == 3) return 3;
+    // auto: the one-launch exchange path up to kXAttnMaxKV (decode step 1.76 -> 1.71 ms at
+    // 8B, ctx 128..640: one boundary fewer; the split path's two launches beyond)
+    if (g_attn_mode == 0 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
     return split_ok ? 2 : fused_ok ? 1 : 3;
 }
 
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     const int g = n_head / n_head_kv;
-    const int path = attn_path(n_head, n_head_kv, kv_bound);
+    int path = attn_path(n_head, n_head_kv, kv_bound);
+    if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254)) path = attn_path(n_head, n_head_kv, kXAttnMaxKV + 256);
+    if (path == 4) {
+        if (head_dim == 128 && attn_x_np(128, kv_bound)) return attn_x_g<128>(a, g, n_head_kv, kv_bound, s);
+        if (head_dim == 64 && attn_x_np(64, kv_bound)) return attn_x_g<64>(a, g, n_head_kv, kv_bound, s);
+        return hipErrorInvalidValue;
+    }
     if (path == 2) {
         if (head_dim == 128) return attn_split_g<128>(a, g, n_head_kv, kv_bound, s);
         if (head_dim == 64) return attn_split_g<64>(a, g, n_head_kv, kv_bound, s);

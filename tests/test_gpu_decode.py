@@ -165,10 +165,11 @@ def test_profile_kernels_leaves_state(gpu, tiny_models):
     assert np.array_equal(ref.logits(-1), c.logits(-1))
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
-    """Each attention path (1 fused one-WG-per-head, 2 split scores+PV over 8-dim
-    slices, 3 long-context two-kernel) reproduces the oracle's logits bit for bit
+    """Each attention path (1 fused one-WG-per-head, 2 split scores+PV over 16-dim
+    slices, 3 long-context two-kernel, 4 one-launch exchange: score tiles handed off
+    as tagged granules) reproduces the oracle's logits bit for bit
     (LLMI_ATTN_MODE is read when a context is created)."""
     monkeypatch.setenv("LLMI_ATTN_MODE", str(mode))
     rng = np.random.default_rng(5 + mode)
