@@ -152,6 +152,12 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
 /* Algorithmic bytes of one decode step at KV length n_kv (weights + one embedding row
  * + norms + KV read/write), the numerator of achieved GB/s. */
 double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv);
+/* 1 when llama_decode runs a prompt (a leading run of >= 2 tokens at consecutive
+ * positions that need no logits) through the batched MFMA prefill path (one launch per
+ * op over all its tokens; bit-identical to decode steps), 0 when every token of such a
+ * batch is a decode step (shapes the prefill kernels do not take).  LLMI_NO_PREFILL=1
+ * in the environment forces decode steps. */
+int32_t llmi_prefill_supported(const struct llama_model* model);
 /* Device weight arena (for RCCL broadcast by a caller that owns the communicator). */
 int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64_t* bytes);
 /* In-process replica fan-out: copies model's arena to devices[0..n) with an RCCL
@@ -183,6 +189,11 @@ int32_t llmi_repack(int32_t type, const void* raw_dev, void* w_dev, int64_t rows
 /* y = W . quantize(norm_w ? rmsnorm(x)*norm_w : x); mode 0 store, 1 accumulate (y += .) */
 int32_t llmi_matvec(int32_t type, const void* w_dev, int64_t rows, int64_t cols, const float* x_dev,
                     const float* norm_w_dev, float eps, float* y_dev, int32_t mode);
+/* batched prefill GEMM (prefill.hip.inc): Y[t] = W . quantize(norm_w ? rmsnorm(x[t])*norm_w
+ * : x[t]) for n_tok rows x[t] of `cols` floats (row-major), Y [n_tok][rows]; must equal
+ * n_tok llmi_matvec calls bit for bit.  usec (optional): device time of the GEMM launch. */
+int32_t llmi_pf_gemm(int32_t type, const void* w_dev, int64_t rows, int64_t cols, const float* x_dev,
+                     const float* norm_w_dev, float eps, int32_t n_tok, float* y_dev, double* usec);
 /* the activation quantization the matvec prologue performs, written out in ggml block
  * form (block_q8_K for K-quant weight types, block_q8_0 for Q8_0) for bit-exact checks */
 int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x_dev, const float* norm_w_dev,

@@ -194,6 +194,9 @@ void llama_batch_free(struct llama_batch b) {
     free(b.logits);
 }
 
+// shortest prompt run taken by the batched prefill path (shorter runs: decode steps)
+static constexpr int kPrefillMin = 2;
+
 int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
     API_TRY
     if (!ctx) { set_err("null context"); return -1; }
@@ -223,7 +226,27 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
     double bytes = 0;
     hipEventRecord(c.ev0, c.stream);
     int last_pos = c.n_past - 1;
-    for (int i = 0; i < n; ++i) {
+    // Batched prefill of the longest leading run of tokens that need no logits and sit at
+    // consecutive positions (the prompt), leaving at least the last token to the decode
+    // step.  LLMI_NO_PREFILL=1 runs every token as a decode step.
+    int i0 = 0;
+    {
+        const char* no_pf_env = getenv("LLMI_NO_PREFILL");
+        const bool no_pf = no_pf_env && atoi(no_pf_env) != 0;
+        const int p0 = batch.pos ? batch.pos[0] : c.n_past;
+        int run = 0;
+        while (run < n - 1 && rows[(size_t)run] < 0 && (batch.pos ? batch.pos[run] : c.n_past + run) == p0 + run) ++run;
+        if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
+            if (!prefill_enqueue(c, batch.token, run, p0, err)) {
+                set_err("llama_decode: " + err);
+                return -3;
+            }
+            for (int i = 0; i < run; ++i) bytes += bytes_per_token(*c.m, p0 + i + 1);
+            last_pos = std::max(last_pos, p0 + run - 1);
+            i0 = run;
+        }
+    }
+    for (int i = i0; i < n; ++i) {
         const int pos = batch.pos ? batch.pos[i] : c.n_past + i;
         if (launch_state_set(c.st, batch.token[i], pos, c.stream) != hipSuccess || !step_run(c, pos, err)) {
             set_err("llama_decode: " + (err.empty() ? std::string("launch failed") : err));
@@ -397,6 +420,10 @@ void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec
     if (!ctx) return;
     if (bytes) *bytes = ctx->c.last_bytes;
     if (usec) *usec = ctx->c.last_us;
+}
+
+int32_t llmi_prefill_supported(const struct llama_model* model) {
+    return model && prefill_supported(model->m) ? 1 : 0;
 }
 
 double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv) {
@@ -584,6 +611,41 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
     (void)hipGetDeviceProperties(&prop, dev);
     hipError_t e = launch_matvec(a, mode == 1 ? EPI_ADD : EPI_STORE, std::max(64, prop.multiProcessorCount * wg_per_cu()), nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+    return 0;
+}
+
+int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, const float* x, const float* nw, float eps,
+                     int32_t n_tok, float* y, double* usec) {
+    if (!pf_gemm_ok(type, (int)rows, (int)cols) || n_tok <= 0) { set_err("llmi_pf_gemm: unsupported type/shape"); return -1; }
+    const int tpad = (n_tok + 31) / 32 * 32;
+    int8_t* aq = nullptr;
+    int16_t* abs = nullptr;
+    float* ad = nullptr;
+    hipError_t e = hipMalloc(&aq, (size_t)tpad * cols);
+    if (e == hipSuccess) e = hipMalloc(&abs, (size_t)tpad * (cols / 16) * 2);
+    if (e == hipSuccess) e = hipMalloc(&ad, (size_t)tpad * (cols / 32) * 4);
+    if (e == hipSuccess) e = hipMemset(aq, 0, (size_t)tpad * cols);
+    if (e == hipSuccess) e = hipMemset(abs, 0, (size_t)tpad * (cols / 16) * 2);
+    if (e == hipSuccess) e = hipMemset(ad, 0, (size_t)tpad * (cols / 32) * 4);
+    if (e == hipSuccess) e = launch_pf_quant(x, (int)cols, nw, eps, (int)cols, act_kind(type), n_tok, aq, abs, ad, nullptr);
+    PfGemm g;
+    g.w = seg_at(type, w, rows, cols); g.rows = (int)rows; g.cols = (int)cols; g.T = n_tok;
+    g.aq = aq; g.abs = abs; g.ad = ad; g.y = y; g.ldy = (int)rows;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e == hipSuccess && usec) { (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventRecord(e0, nullptr); }
+    if (e == hipSuccess) e = launch_pf_gemm(g, EPI_STORE, nullptr);
+    if (e == hipSuccess && usec) {
+        (void)hipEventRecord(e1, nullptr);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        *usec = ms * 1e3;
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(aq); (void)hipFree(abs); (void)hipFree(ad);
     if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
     return 0;
 }

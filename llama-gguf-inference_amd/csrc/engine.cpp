@@ -49,7 +49,7 @@ Context::~Context() {
     (void)hipGetDevice(&cur);
     if (m) (void)hipSetDevice(m->device);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
-    void* bufs[] = {x, q, att, h, logits, scores, rope, kc, vc, st, hist};
+    void* bufs[] = {x, q, att, h, logits, scores, rope, kc, vc, st, hist, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -487,6 +487,121 @@ bool step_run(Context& c, int pos, std::string& err) {
         it = c.graphs.emplace(bucket, ex).first;
     }
     HIPC(hipGraphLaunch(it->second, c.stream));
+    return true;
+}
+
+// ---------------------------------------------------------------------------------
+// Batched prefill: the prompt's tokens go through every layer as
+// one launch per op over all of them (prefill.hip.inc): embed -> per layer [norm+quant,
+// q/k/v GEMMs (RoPE, KV write), causal attention, quant, attn_output GEMM (+residual),
+// norm+quant, gate/up GEMM (SwiGLU), quant, down GEMM (+residual)].  Results equal T
+// decode steps bit for bit (the GEMM keeps the matvec's device order); the caller runs
+// the prompt's last token as an ordinary decode step for its logits.
+// ---------------------------------------------------------------------------------
+bool prefill_supported(const Model& m) {
+    const HParams& hp = m.hp;
+    if (hp.head_dim != 128 && hp.head_dim != 64) return false;
+    if (hp.n_rot % 2 || hp.n_rot > hp.head_dim) return false;
+    for (const Layer& L : m.layers) {
+        const DevMat* ms[] = {&L.wq, &L.wk, &L.wv, &L.wo, &L.wg, &L.wu, &L.wd};
+        for (const DevMat* d : ms)
+            if (!pf_gemm_ok(d->type, (int)d->rows, (int)d->cols)) return false;
+        if (act_kind(L.wg.type) != act_kind(L.wu.type)) return false;
+    }
+    return true;
+}
+
+static bool prefill_alloc(Context& c, std::string& err) {
+    if (c.pf_cap) return true;
+    const HParams& hp = c.m->hp;
+    const int cap = 512;  // ubatch (llama.cpp's default n_ubatch), a multiple of 32
+    const size_t E = hp.n_embd, QD = (size_t)hp.n_head * hp.head_dim, F = hp.n_ff;
+    const size_t maxc = std::max({E, QD, F});
+    HIPC(hipMalloc(&c.pf_tok, cap * 4));
+    HIPC(hipMalloc(&c.pf_x, cap * E * 4));
+    HIPC(hipMalloc(&c.pf_q, cap * QD * 4));
+    HIPC(hipMalloc(&c.pf_att, cap * QD * 4));
+    HIPC(hipMalloc(&c.pf_h, cap * F * 4));
+    HIPC(hipMalloc(&c.pf_aq, cap * maxc));
+    HIPC(hipMalloc(&c.pf_abs, cap * (maxc / 16) * 2));
+    HIPC(hipMalloc(&c.pf_ad, cap * (maxc / 32) * 4));
+    // padded token rows of the activation buffers are read (never stored): keep them finite
+    HIPC(hipMemsetAsync(c.pf_aq, 0, cap * maxc, c.stream));
+    HIPC(hipMemsetAsync(c.pf_abs, 0, cap * (maxc / 16) * 2, c.stream));
+    HIPC(hipMemsetAsync(c.pf_ad, 0, cap * (maxc / 32) * 4, c.stream));
+    c.pf_cap = cap;
+    return true;
+}
+
+bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::string& err) {
+    const Model& m = *c.m;
+    const HParams& hp = m.hp;
+    if (!prefill_supported(m)) { err = "prefill: model shapes not supported by the batched path"; return false; }
+    if (pos0 < 0 || pos0 + n > c.n_ctx) { err = "prefill: positions out of the context"; return false; }
+    if (!prefill_alloc(c, err)) return false;
+    const int E = hp.n_embd, D = hp.head_dim, nq = hp.n_head * D, nk = hp.n_head_kv * D, F = hp.n_ff;
+    const size_t kv_layer = (size_t)hp.n_head_kv * c.n_ctx * D;
+#define PFC(expr)                                                              \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) { err = std::string(#expr) + ": " + hip_err(e_); return false; } \
+    } while (0)
+    for (int b0 = 0; b0 < n; b0 += c.pf_cap) {
+        const int T = std::min(c.pf_cap, n - b0), p0 = pos0 + b0;
+        PFC(hipMemcpyAsync(c.pf_tok, tokens + b0, (size_t)T * 4, hipMemcpyHostToDevice, c.stream));
+        PFC(launch_pf_embed(seg_of(m, m.tok_embd, 0), E, hp.n_vocab, c.pf_tok, c.pf_x, T, c.hist, p0, c.n_ctx, c.stream));
+        for (int l = 0; l < hp.n_layer; ++l) {
+            const Layer& L = m.layers[(size_t)l];
+            PfGemm g;
+            g.T = T; g.aq = c.pf_aq; g.abs = c.pf_abs; g.ad = c.pf_ad;
+            g.kc = c.kc + l * kv_layer; g.vc = c.vc + l * kv_layer; g.rope = c.rope;
+            g.pos0 = p0; g.head_dim = D; g.n_rot = hp.n_rot; g.n_ctx = c.n_ctx;
+            // q, k, v (each quantized for its own activation kind)
+            const DevMat* qkv[3] = {&L.wq, &L.wk, &L.wv};
+            int quant_kind = -1;
+            for (int part = 0; part < 3; ++part) {
+                const DevMat& W = *qkv[part];
+                if (act_kind(W.type) != quant_kind) {
+                    quant_kind = act_kind(W.type);
+                    PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.attn_norm.off_a), hp.eps, E, quant_kind, T,
+                                        c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+                }
+                g.w = seg_of(m, W, 0); g.rows = (int)W.rows; g.cols = E; g.part = part;
+                g.y = c.pf_q; g.ldy = nq;
+                PFC(launch_pf_gemm(g, EPI_QKV, c.stream));
+            }
+            (void)nk;
+            PfAttn at;
+            at.q = c.pf_q; at.out = c.pf_att; at.ldq = nq; at.kc = g.kc; at.vc = g.vc;
+            at.n_ctx = c.n_ctx; at.pos0 = p0; at.gqa = hp.n_head / hp.n_head_kv; at.max_kv = p0 + T;
+            at.scale = 1.0f / sqrtf((float)D);
+            PFC(launch_pf_attn(at, hp.n_head, D, T, c.stream));
+            // attn_output + residual
+            PFC(launch_pf_quant(c.pf_att, nq, nullptr, 0.f, nq, act_kind(L.wo.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+            g.w = seg_of(m, L.wo, 0); g.rows = (int)L.wo.rows; g.cols = nq; g.y = c.pf_x; g.ldy = E;
+            PFC(launch_pf_gemm(g, EPI_ADD, c.stream));
+            // gate/up + SwiGLU
+            PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.ffn_norm.off_a), hp.eps, E, act_kind(L.wg.type), T,
+                                c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+            g.w = seg_of(m, L.wg, 0); g.w2 = seg_of(m, L.wu, 0); g.rows = (int)L.wg.rows; g.cols = E; g.y = c.pf_h; g.ldy = F;
+            if (L.wg.type == L.wu.type) {
+                PFC(launch_pf_gemm(g, EPI_SWIGLU, c.stream));
+            } else {  // gate into h, then h = silu(h) * up
+                if (act_kind(L.wu.type) != act_kind(L.wg.type)) {
+                    err = "prefill: ffn_gate/ffn_up of different activation kinds";
+                    return false;
+                }
+                PFC(launch_pf_gemm(g, EPI_STORE, c.stream));
+                g.w = seg_of(m, L.wu, 0);
+                PFC(launch_pf_gemm(g, EPI_SWIGLU_UP, c.stream));
+            }
+            // down + residual
+            PFC(launch_pf_quant(c.pf_h, F, nullptr, 0.f, F, act_kind(L.wd.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+            g.w = seg_of(m, L.wd, 0); g.rows = (int)L.wd.rows; g.cols = F; g.y = c.pf_x; g.ldy = E;
+            PFC(launch_pf_gemm(g, EPI_ADD, c.stream));
+        }
+    }
+#undef PFC
     return true;
 }
 

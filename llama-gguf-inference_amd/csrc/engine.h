@@ -87,6 +87,13 @@ struct Context {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_bytes = 0, last_us = 0;
     Prof* prof = nullptr;                   // non-null only inside llmi_profile_kernels
+    // batched prefill scratch (allocated on first use; ubatches of <= pf_cap tokens)
+    int pf_cap = 0;
+    int32_t* pf_tok = nullptr;
+    float *pf_x = nullptr, *pf_q = nullptr, *pf_att = nullptr, *pf_h = nullptr;
+    int8_t* pf_aq = nullptr;
+    int16_t* pf_abs = nullptr;
+    float* pf_ad = nullptr;
     ~Context();
 };
 
@@ -98,6 +105,11 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err);
 // run one step via the cached graph of its KV bucket (or eagerly)
 bool step_run(Context& c, int pos, std::string& err);
 double bytes_per_token(const Model& m, int n_kv);
+// batched prefill: can the model's layers run through the MFMA prefill path?
+bool prefill_supported(const Model& m);
+// run tokens [0, n) at positions pos0.. through every layer as batched launches (KV
+// cache written, no logits); enqueued on c.stream, no synchronisation
+bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::string& err);
 void context_clear(Context& c);
 size_t model_tensor_bytes(const Model& m);
 // arena layout of a model for another device (replica); no upload

@@ -24,7 +24,8 @@ inline size_t attn_gran_off(int n_head, int n_ctx) {
 }
 inline size_t attn_scratch_floats(int n_head, int n_ctx) { return attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV + 4; }
 
-enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4 };
+enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4,
+                 EPI_SWIGLU_UP = 5 };  // prefill: y = silu(y) * up (gate/up of different types)
 
 // One weight matrix of a fused matvec launch.
 struct Seg {
@@ -84,6 +85,38 @@ struct EmbArgs {
     int32_t* hist = nullptr;        // token history [n_ctx]
     int n_ctx = 0;
 };
+
+// Batched prefill (prefill.hip.inc): one launch per linear layer over T prompt tokens.
+struct PfGemm {
+    Seg w, w2;                 // weights (SWIGLU: w = gate, w2 = up)
+    int rows = 0, cols = 0;
+    int T = 0;                 // tokens (activation rows are padded to a multiple of 32)
+    const int8_t* aq = nullptr;   // [Tpad][cols] q8 activations, natural order
+    const int16_t* abs = nullptr; // [Tpad][cols/16] bsums (q8_K)
+    const float* ad = nullptr;    // [Tpad][cols/256] (q8_K) or [Tpad][cols/32] (q8_0) d
+    float* y = nullptr;        // STORE / ADD / SWIGLU / QKV q: [T][ldy]
+    int ldy = 0;
+    int part = 0;              // QKV: 0 q (RoPE, f32 to y), 1 k (RoPE, f16 cache), 2 v (f16 cache)
+    uint16_t* kc = nullptr;    // layer K cache [HK][n_ctx][D]
+    uint16_t* vc = nullptr;    // layer V cache [HK][D][n_ctx]
+    const float* rope = nullptr;
+    int pos0 = 0, head_dim = 0, n_rot = 0, n_ctx = 0;
+};
+struct PfAttn {
+    const float* q = nullptr;  // [T][ldq] roped q
+    float* out = nullptr;      // [T][ldq]
+    int ldq = 0;
+    const uint16_t* kc = nullptr, *vc = nullptr;  // layer caches
+    int n_ctx = 0, pos0 = 0, gqa = 1, max_kv = 0;  // max_kv >= pos0 + T (LDS score space)
+    float scale = 0.f;
+};
+bool pf_gemm_ok(int type, int rows, int cols);
+hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* toks, float* X, int T, int32_t* hist,
+                           int pos0, int n_ctx, hipStream_t s);
+hipError_t launch_pf_quant(const float* x, int ldx, const float* nw, float eps, int cols, int act, int T, int8_t* aq,
+                           int16_t* abs, float* ad, hipStream_t s);
+hipError_t launch_pf_gemm(const PfGemm& g, int epi, hipStream_t s);
+hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipStream_t s);
 
 // activation kind of a weight type: 0 = block_q8_K (K-quants), 1 = block_q8_0
 inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }

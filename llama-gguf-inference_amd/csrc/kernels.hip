@@ -2266,4 +2266,7 @@ hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint
     return hipGetLastError();
 }
 
+// batched prefill (MFMA): same translation unit, shares the device helpers above
+#include "prefill.hip.inc"
+
 }  // namespace llmi

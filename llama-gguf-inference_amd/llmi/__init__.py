@@ -103,6 +103,11 @@ class Model:
     def bytes_per_token(self, n_kv: int) -> float:
         return float(lib().llmi_bytes_per_token(self._h, int(n_kv)))
 
+    @property
+    def prefill_supported(self) -> bool:
+        """Whether llama_decode prefills prompts with the batched MFMA path."""
+        return bool(lib().llmi_prefill_supported(self._h))
+
     def arena(self) -> tuple[int, int]:
         p, n = C.c_void_p(), C.c_uint64()
         lib().llmi_model_arena(self._h, C.byref(p), C.byref(n))
