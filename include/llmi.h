@@ -179,6 +179,11 @@ int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t
 int64_t llmi_synth_write_gguf(const char* path, const char* preset, uint64_t seed,
                               int32_t n_layer, int32_t n_vocab, int32_t n_threads);
 
+/* Debug taps of the last decode step (host copy, synchronous): 1 residual x after the
+ * last layer (n_embd), 2 roped q (n_head*head_dim), 3 attention output, 4 SwiGLU output
+ * (n_ff) — the last layer's.  Mirrors the oracle's or_tap.  0 on success. */
+int32_t llmi_debug_tap(struct llama_context* ctx, int32_t which, float* out);
+
 /* ---------- kernel-level entry points (tests and microbenchmarks) ----------
  * All pointers are DEVICE pointers on the current HIP device; the call is enqueued
  * on the NULL stream and synchronised.  Types are ggml type ids (Q4_K=12, Q5_K=13,

@@ -422,6 +422,29 @@ void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec
     if (usec) *usec = ctx->c.last_us;
 }
 
+int32_t llmi_debug_tap(struct llama_context* ctx, int32_t which, float* out) {
+    if (!ctx || !out) { set_err("llmi_debug_tap: bad arguments"); return -1; }
+    Context& c = ctx->c;
+    const HParams& hp = c.m->hp;
+    (void)hipSetDevice(c.m->device);
+    if (which == 7 || which == 8) {  // last layer's K ([HK][n_ctx][D]) or V ([HK][D][n_ctx]) cache, raw f16
+        const size_t kvl = (size_t)hp.n_head_kv * c.n_ctx * hp.head_dim;
+        const uint16_t* base = (which == 7 ? c.kc : c.vc) + (size_t)(hp.n_layer - 1) * kvl;
+        hipError_t e = hipMemcpyAsync(out, base, kvl * 2, hipMemcpyDeviceToHost, c.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+        if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+        return 0;
+    }
+    const float* src = which == 1 ? c.x : which == 2 ? c.q : which == 3 ? c.att : which == 4 ? c.h : nullptr;
+    const size_t n = which == 1 ? hp.n_embd : which == 4 ? hp.n_ff : (size_t)hp.n_head * hp.head_dim;
+    if (!src) { set_err("llmi_debug_tap: unknown tap"); return -1; }
+    (void)hipSetDevice(c.m->device);
+    hipError_t e = hipMemcpyAsync(out, src, n * 4, hipMemcpyDeviceToHost, c.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+    return 0;
+}
+
 int32_t llmi_prefill_supported(const struct llama_model* model) {
     return model && prefill_supported(model->m) ? 1 : 0;
 }

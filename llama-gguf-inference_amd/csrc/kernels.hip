@@ -69,7 +69,15 @@ constexpr bool kNontemporalWeights = LLMI_NT != 0;
 __device__ __forceinline__ float h2f(uint32_t h) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
 }
-__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+// f32 -> f16 with its own rounding.  The empty asm makes the f32 value opaque: without
+// it the compiler folds f2h(a * b) into v_fma_mixlo_f16, ONE rounding of the exact
+// product straight to f16, where ggml rounds to f32 first and then to f16 (a tie in
+// the f32 product then rounds differently: softmax probabilities left the oracle by one
+// f16 ulp, tools/pf_diag9.py).
+__device__ __forceinline__ uint16_t f2h(float f) {
+    __asm__("" : "+v"(f));
+    return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
 
 __device__ __forceinline__ u32x4 ldw(const uint8_t* p) {
     if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x4*)p);
@@ -1309,7 +1317,7 @@ __global__ __launch_bounds__(256) void k_attn_scores8(AttnArgs a) {
     // of two f16 values is exact, so fma(k, q, acc) == acc + (double)(k * q)
     __shared__ __attribute__((aligned(16))) double qs[G][D];
     __shared__ float wmax[4][G];
-    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = (double)(float)(_Float16)a.q[(size_t)g * G * D + i];
+    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = (double)h2f(f2h(a.q[(size_t)g * G * D + i]));
     const int n_kv = a.st->pos + 1;
     __syncthreads();
     LLMI_ATT_STAMP(0, 1)
@@ -1423,7 +1431,7 @@ __global__ __launch_bounds__(512) void k_attn_pv16(AttnArgs a, int kvb) {
 #pragma unroll
     for (int i = 1; i < WPH; ++i) tot += reds[hh * WPH + i];
     const float inv = (float)(1.0 / tot);
-    for (int t = wi * 64 + lane; t < n_kv; t += WPH * 64) sp[t] = (float)(_Float16)(sp[t] * inv);
+    for (int t = wi * 64 + lane; t < n_kv; t += WPH * 64) sp[t] = h2f(f2h(sp[t] * inv));
     for (int t = n_kv + wi * 64 + lane; t < ((n_kv + 3) & ~3); t += WPH * 64) sp[t] = 0.f;
     __syncthreads();
     LLMI_ATT_STAMP(1, 2)
@@ -1523,7 +1531,7 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
     for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(4 * sl + 128 * k, kvb - 4)));
 #pragma unroll
     for (int k = 0; k < (G * D + 511) / 512; ++k)
-        if (tid + 512 * k < G * D) qs[(tid + 512 * k) / D][(tid + 512 * k) % D] = (double)(float)(_Float16)qv[k];
+        if (tid + 512 * k < G * D) qs[(tid + 512 * k) / D][(tid + 512 * k) % D] = (double)h2f(f2h(qv[k]));
     if (tid == 0) s_fault = 0;
     const int n_kv = pos + 1;
     const uint32_t tag = seq * 256u + (uint32_t)a.layer + 1u;
@@ -1633,7 +1641,7 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         const int t = wi * 64 + lane + k * WPH * 64;
-        if (t < n_kv) sp[t] = (float)(_Float16)(sv[k] * inv);
+        if (t < n_kv) sp[t] = h2f(f2h(sv[k] * inv));
         else if (t < ((n_kv + 3) & ~3)) sp[t] = 0.f;
     }
     __syncthreads();

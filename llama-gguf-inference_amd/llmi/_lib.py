@@ -92,6 +92,7 @@ SIGNATURES = {
     "llmi_profile_kernels": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_double),
                                          C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "llmi_prefill_supported": (C.c_int32, [_P]),
+    "llmi_debug_tap": (C.c_int32, [_P, C.c_int32, _P]),
     "llmi_pf_gemm": (C.c_int32, [C.c_int32, _P, C.c_int64, C.c_int64, _P, _P, C.c_float, C.c_int32, _P,
                                  C.POINTER(C.c_double)]),
     "llmi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),

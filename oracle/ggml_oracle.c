@@ -792,6 +792,18 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
 int or_tap(const or_model* m, int which, float* out) {
     if (which == 0) memcpy(out, m->tap_embd, (size_t)m->n_embd * 4);
     else if (which == 1) memcpy(out, m->tap_final, (size_t)m->n_embd * 4);
+    /* last layer's intermediates of the last step: 2 q (roped), 3 attention output,
+     * 4 SwiGLU output, 5 k (roped), 6 v */
+    else if (which == 2) memcpy(out, m->q, (size_t)m->n_head * m->head_dim * 4);
+    else if (which == 3) memcpy(out, m->att, (size_t)m->n_head * m->head_dim * 4);
+    else if (which == 4) memcpy(out, m->hb, (size_t)m->n_ff * 4);
+    else if (which == 5) memcpy(out, m->k, (size_t)m->n_head_kv * m->head_dim * 4);
+    else if (which == 6) memcpy(out, m->v, (size_t)m->n_head_kv * m->head_dim * 4);
+    /* 7 / 8: the last layer's K / V cache, raw f16 [pos][n_head_kv*head_dim] for all n_ctx */
+    else if (which == 7 || which == 8) {
+        const size_t kvl = (size_t)m->n_ctx * m->n_head_kv * m->head_dim;
+        memcpy(out, (which == 7 ? m->kc : m->vc) + (size_t)(m->n_layer - 1) * kvl, kvl * 2);
+    }
     else return -1;
     return 0;
 }
