@@ -250,8 +250,8 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int8",
-            "data": "synthetic: random-init GGUF blocks with the exact Llama-3-8B Q4_K_M shapes/type table "
-                    "(llmi_synth.h); random 128-token prompts",
+            "data": f"synthetic: random-init GGUF blocks with the exact {args.preset} shapes/type table "
+                    f"(llmi_synth.h); random {args.prompt}-token prompts",
             "config": {"workload": f"{args.preset}: {args.prompt}-token prompt -> greedy decode "
                                    f"{args.warmup}+{args.steps} tokens, 1 replica per GPU",
                        "model": args.preset, "prompt_tokens": args.prompt, "ctx_end": eng.pos,
