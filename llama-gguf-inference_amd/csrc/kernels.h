@@ -127,7 +127,7 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
 // attention path for a KV bound: 1 fused (one WG per head), 2 split (scores + PV over
 // (group, 16-dim slice) workgroups), 3 two-kernel long-context path, 4 one-launch
 // exchange (k_attn_x: scores tiles + granule hand-off + PV, kv_bound <= kXAttnMaxKV)
-int attn_path(int n_head, int n_head_kv, int kv_bound);
+int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim);
 // arm (or with nullptrs disarm) per-op kernel timing events for this thread's launches
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);

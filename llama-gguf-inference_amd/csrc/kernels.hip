@@ -2204,7 +2204,7 @@ static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipSt
 
 static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel, 4 exchange (experiments: LLMI_ATTN_MODE)
 void set_attn_mode(int mode) { g_attn_mode = mode; }
-int attn_path(int n_head, int n_head_kv, int kv_bound) {
+int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     const int g = n_head / n_head_kv;
     const bool split_ok = (size_t)g * kv_bound * 4 <= kSplitAttnMaxLds;
     const bool fused_ok = kv_bound <= kFusedAttnMaxKV;
@@ -2213,17 +2213,27 @@ int attn_path(int n_head, int n_head_kv, int kv_bound) {
     if (g_attn_mode == 1 && fused_ok) return 1;
     if (g_attn_mode == 2 && split_ok) return 2;
     if (g_attn_mode == 3) return 3;
-    // auto: the one-launch exchange path up to kXAttnMaxKV (decode step 1.76 -> 1.71 ms at
-    // 8B, ctx 128..640: one boundary fewer; the split path's two launches beyond)
-    if (g_attn_mode == 0 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
+    // auto, from the crossovers measured by tools/attnbench.py (graph-free launches, us;
+    // profiles/r01/attn_modes.md):
+    //   G=4, D=128 (8B, Mistral): fused <= 256 (8.1 vs 8.4 exchange), exchange <= 512,
+    //                             split beyond (640: 10.8 vs 12.9 exchange)
+    //   G=8, D=128 (70B): fused <= 640 (128: 8.1 vs 16.3 exchange), split beyond
+    //   G=8, D=64 (TinyLlama): fused <= 2048 (128: 6.2 vs 9.7; 1280: 15.9 vs 20.9)
+    if (g_attn_mode == 0) {
+        if (g == 8 && fused_ok && kv_bound <= (head_dim == 64 ? 2048 : 640)) return 1;
+        if (g == 4 && fused_ok && kv_bound <= 256) return 1;
+        if (g == 4 && split_ok && kv_bound > 512) return 2;
+        if (g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
+    }
     return split_ok ? 2 : fused_ok ? 1 : 3;
 }
 
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     const int g = n_head / n_head_kv;
-    int path = attn_path(n_head, n_head_kv, kv_bound);
-    if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254)) path = attn_path(n_head, n_head_kv, kXAttnMaxKV + 256);
+    int path = attn_path(n_head, n_head_kv, kv_bound, head_dim);
+    if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254))
+        path = attn_path(n_head, n_head_kv, kXAttnMaxKV + 256, head_dim);
     if (path == 4) {
         if (head_dim == 128 && attn_x_np(128, kv_bound)) return attn_x_g<128>(a, g, n_head_kv, kv_bound, s);
         if (head_dim == 64 && attn_x_np(64, kv_bound)) return attn_x_g<64>(a, g, n_head_kv, kv_bound, s);
