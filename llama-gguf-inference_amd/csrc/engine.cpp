@@ -20,7 +20,7 @@ int wg_per_cu() {
     static const int v = [] {
         const char* e = getenv("LLMI_WG_PER_CU");
         const int n = e ? atoi(e) : 0;
-        return n > 0 ? n : 4;
+        return n > 0 ? n : 2;
     }();
     return v;
 }

@@ -2128,6 +2128,11 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
     const size_t lds = mv_lds_bytes(act, a.cols);
     int blocks = (a.npairs + kMVWaves - 1) / kMVWaves;
     if (blocks > max_blocks) blocks = max_blocks;
+    static const int exp_blocks = [] {  // experiment hook: fixed grid for launch sweeps
+        const char* e = getenv("LLMI_MV_BLOCKS");
+        return e ? atoi(e) : 0;
+    }();
+    if (exp_blocks > 0 && exp_blocks < blocks) blocks = exp_blocks;
 #if defined(LLMI_EXP_BALANCE)
     {  // experiment: equal pairs per wave (fewer workgroups when that divides better)
         const int waves = blocks * kMVWaves, per = (a.npairs + waves - 1) / waves;
