@@ -16,13 +16,10 @@ namespace llmi {
 
 std::string hip_err(hipError_t e) { return std::string(hipGetErrorString(e)); }
 
-int wg_per_cu() {
-    static const int v = [] {
-        const char* e = getenv("LLMI_WG_PER_CU");
-        const int n = e ? atoi(e) : 0;
-        return n > 0 ? n : 2;
-    }();
-    return v;
+int wg_per_cu() {  // read per call (context creation): tests vary it within a process
+    const char* e = getenv("LLMI_WG_PER_CU");
+    const int n = e ? atoi(e) : 0;
+    return n > 0 ? n : 2;
 }
 
 #define HIPC(expr)                                                         \

@@ -116,8 +116,8 @@ size_t model_tensor_bytes(const Model& m);
 bool model_clone_layout(const Model& src, int device, Model& dst, std::string& err);
 
 std::string hip_err(hipError_t e);
-// matvec grid cap = CUs x wg_per_cu() workgroups (env LLMI_WG_PER_CU, default 2: measured
-// best on every config, profiles/r01/wg_sweep.md)
+// matvec grid cap = CUs x wg_per_cu() workgroups (env LLMI_WG_PER_CU, read when a context
+// is created; default 2: measured best on every config, profiles/r01/wg_sweep.md)
 int wg_per_cu();
 int64_t synth_write_gguf(const std::string& path, const std::string& preset, uint64_t seed, int n_layer, int n_vocab,
                          int n_threads, std::string& err);

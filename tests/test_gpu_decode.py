@@ -140,6 +140,19 @@ def test_decode_parity_real_widths(gpu, synth_dir, preset, n_layer, n_vocab):
     assert g == o
 
 
+@pytest.mark.parametrize("wg", ["1", "3", "4"])
+def test_grid_cap_does_not_change_results(gpu, synth_dir, monkeypatch, wg):
+    """Results do not depend on the matvec grid (LLMI_WG_PER_CU, read at context
+    creation): a row's sum is one wave's, whichever wave takes the pair.  Exact
+    Llama-3-8B widths, 2 layers, bit-identical to the oracle at 1, 3 and 4 workgroups
+    per CU (the default 2 runs in test_decode_parity_real_widths)."""
+    path = str(synth_dir / "llama3-8b-q4km-L2-wg.gguf")
+    llmi.write_synthetic_gguf(path, "llama3-8b-q4km", seed=5, n_layer=2)
+    monkeypatch.setenv("LLMI_WG_PER_CU", wg)
+    worst, g, o, *_ = run_parity(path, [1, 7, 300, 9000], 4, n_ctx=64, exact=True)
+    assert g == o
+
+
 def test_profile_kernels_leaves_state(gpu, tiny_models):
     """llmi_profile_kernels times every kernel class (positive times, launch counts of
     the graph) and consumes no tokens: decoding after it is bit-identical."""
