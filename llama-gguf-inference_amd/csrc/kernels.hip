@@ -2041,9 +2041,20 @@ static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream
         const int nj = ((a.cols >> 6) + 63) >> 6;
         const int per = (a.cols / 16 + kKSThreads - 1) / kKSThreads;
         const int mb = g_mv_max_blocks;
-        if (per <= 1) return nj >= 4 ? mv_launch_ks<ACT, NORM, T, EPI, 1, 4>(a, mb, s)
-                                     : mv_launch_ks<ACT, NORM, T, EPI, 1, 2>(a, mb, s);
-        return nj >= 4 ? mv_launch_ks<ACT, NORM, T, EPI, 2, 4>(a, mb, s) : mv_launch_ks<ACT, NORM, T, EPI, 2, 2>(a, mb, s);
+        // K-split width 2 (pair slots of 2 waves, 8 pairs per workgroup round) on every
+        // long row: measured ahead of 4 at 14336 columns (ffn_down Q4_K 10.3 -> 9.8 us,
+        // Q6_K 12.7 -> 12.2 us; profiles/r01/ks_sweep.md).  LLMI_KS=4 forces 4 for
+        // rows of >= 4 items (A/B hook).
+        static const bool ks4 = [] {
+            const char* e = getenv("LLMI_KS");
+            return e && atoi(e) == 4;
+        }();
+        if (ks4 && nj >= 4) {
+            if (per <= 1) return mv_launch_ks<ACT, NORM, T, EPI, 1, 4>(a, mb, s);
+            return mv_launch_ks<ACT, NORM, T, EPI, 2, 4>(a, mb, s);
+        }
+        if (per <= 1) return mv_launch_ks<ACT, NORM, T, EPI, 1, 2>(a, mb, s);
+        return mv_launch_ks<ACT, NORM, T, EPI, 2, 2>(a, mb, s);
     }
     switch (prologue_np(a.cols)) {
         case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
