@@ -2041,18 +2041,21 @@ static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream
         const int nj = ((a.cols >> 6) + 63) >> 6;
         const int per = (a.cols / 16 + kKSThreads - 1) / kKSThreads;
         const int mb = g_mv_max_blocks;
-        // K-split width 2 (pair slots of 2 waves, 8 pairs per workgroup round) on every
-        // long row: measured ahead of 4 at 14336 columns (ffn_down Q4_K 10.3 -> 9.8 us,
-        // Q6_K 12.7 -> 12.2 us; profiles/r01/ks_sweep.md).  LLMI_KS=4 forces 4 for
-        // rows of >= 4 items (A/B hook).
-        static const bool ks4 = [] {
+        // K-split width (waves per pair slot), measured (profiles/r01/ks_sweep.md):
+        //   rows of >= 6 items (70B ffn_down, 28672 columns): KS = 1 when its part buffer
+        //     fits LDS — one pair per wave, no per-round barrier wait (30.7 -> 29.0 us);
+        //   otherwise KS = 2 (8B ffn_down Q4_K 10.3 -> 9.8 us against KS = 4).
+        // LLMI_KS = 2 / 4 forces that width (A/B hook; 4 only for rows of >= 4 items).
+        static const int ks_env = [] {
             const char* e = getenv("LLMI_KS");
-            return e && atoi(e) == 4;
+            return e ? atoi(e) : 0;
         }();
-        if (ks4 && nj >= 4) {
+        if (ks_env == 4 && nj >= 4) {
             if (per <= 1) return mv_launch_ks<ACT, NORM, T, EPI, 1, 4>(a, mb, s);
             return mv_launch_ks<ACT, NORM, T, EPI, 2, 4>(a, mb, s);
         }
+        if (ks_env == 0 && nj >= 6 && per > 1 && ks_part_off(ACT, a.cols) + ks_part_bytes<1>(a.cols) <= 160 * 1024)
+            return mv_launch_ks<ACT, NORM, T, EPI, 2, 1>(a, mb, s);
         if (per <= 1) return mv_launch_ks<ACT, NORM, T, EPI, 1, 2>(a, mb, s);
         return mv_launch_ks<ACT, NORM, T, EPI, 2, 2>(a, mb, s);
     }
