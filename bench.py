@@ -42,9 +42,10 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--model-dir", default=os.environ.get("LLMI_BENCH_DIR", "/tmp/llmi_bench"))
     ap.add_argument("--profile-steps", type=int, default=20)
-    ap.add_argument("--cpu-sample-tokens", type=int, default=8)
+    ap.add_argument("--cpu-sample-tokens", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r02"),
+                    help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
     return ap.parse_args(argv)
 
 
@@ -186,30 +187,76 @@ def log(msg):
 
 
 def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
-    """The oracle (CPU restatement of the reference's NGL=0 numerics, oracle/) timed on
-    this host: n_tokens greedy decode steps of the same GGUF after a 1-token prompt."""
+    """The reference's CPU path (NGL=0) restated — the oracle, oracle/ — timed on this
+    host: the -O3 -march=x86-64-v3 build (bit-identical to the -O2 parity build), ggml's
+    generic fp32 order (the reference's numerics), one thread per physical core up to the
+    box's CPU share (16).  Workload: the same 128-token prompt (its KV rows filled by the
+    oracle's batched prefill, untimed), then n_tokens timed greedy decode steps at
+    context 128+ — a bounded sample of the GPU run's decode.  Beside it the host DRAM
+    streaming-read rate and the decode roofline it implies (bytes/token / host GB/s)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import pyoracle as po
 
-    threads = po.nthreads()
-    om = po.OracleModel(path, n_ctx=n_tokens + 2, threads=threads)
-    lg = om.decode(prompt[0], 0)  # page-in + first step, untimed
-    t = int(np.argmax(lg))
+    po.prefer_simd()
+    phys = po.physical_cores()
+    threads = max(1, min(phys, 16))
+    om = po.OracleModel(path, n_ctx=len(prompt) + n_tokens + 2, threads=threads)
+    t = time.perf_counter()
+    po.set_dot_order(po.DEVICE_ORDER)  # the fast batched path fills the KV rows (untimed)
+    om.prefill(prompt[:-1])
+    po.set_dot_order(po.GENERIC)
+    fill_s = time.perf_counter() - t
+    lg = om.decode(prompt[-1], len(prompt) - 1)  # first step (page-in), untimed
+    tok = int(np.argmax(lg))
     t0 = time.perf_counter()
     for k in range(n_tokens):
-        lg = om.decode(t, k + 1)
-        t = int(np.argmax(lg))
+        lg = om.decode(tok, len(prompt) + k)
+        tok = int(np.argmax(lg))
     dt = time.perf_counter() - t0
+    bpt = om.bytes_per_token(len(prompt) + n_tokens // 2)
     om.close()
-    return {"value": n_tokens / dt, "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"{n_tokens} greedy decode steps (ctx 2..{n_tokens + 1}) of the same synthetic "
-                      f"{os.path.basename(path)}; oracle/ggml_oracle.c generic scalar C, OpenMP {threads} threads"}
+    host_gbps = po.host_stream_gbps(1 << 30, 3, threads)
+    tok_s = n_tokens / dt
+    return {"value": round(tok_s, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "physical_cores": phys,
+            "achieved_GBps": round(tok_s * bpt / 1e9, 2),
+            "host_dram_roofline": {"stream_read_GBps": round(host_gbps, 1),
+                                   "decode_tok_s_at_roofline": round(host_gbps * 1e9 / bpt, 2)},
+            "sample": f"{n_tokens} greedy decode steps at ctx {len(prompt)}..{len(prompt) + n_tokens - 1} after the "
+                      f"same {len(prompt)}-token prompt (KV filled by the oracle's batched prefill in "
+                      f"{fill_s:.1f}s, untimed) on {os.path.basename(path)}; oracle/ggml_oracle.c "
+                      f"-O3 -march=x86-64-v3, ggml generic fp32 order, OpenMP {threads} threads "
+                      f"({phys} physical cores on the host; 16 = the box's CPU share per GPU)"}
+
+
+def env_knobs() -> dict:
+    """Every LLMI_* variable in the environment (recorded in the line); experiment-build
+    knobs are refused: they remove or reorder work inside the timed region."""
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("LLMI_")}
+    bad = [k for k in knobs if k.startswith("LLMI_EXP_")]
+    if bad:
+        raise SystemExit(f"bench.py: refusing to run with experiment knobs set: {bad}")
+    return knobs
+
+
+def committed_profile(profile_dir: str, preset: str) -> dict:
+    """rocprof evidence committed for THIS preset (profiles/<round>/traffic_<preset>.json:
+    FETCH_SIZE bytes per launch of the dominant kernel, rocprof average us); {} if none."""
+    f = os.path.join(profile_dir, f"traffic_{preset}.json")
+    if not os.path.exists(f):
+        return {}
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return {}
+    return d if d.get("preset") == preset else {}
 
 
 def main(argv=None):
     args = parse(argv)
+    knobs = env_knobs()
     dist = Dist(os.environ.get("LLMI_DIST_BACKEND", "nccl"))
     if dist.world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={dist.world}; using WORLD_SIZE")
@@ -226,12 +273,8 @@ def main(argv=None):
     if dist.rank == 0:
         k = prof.get(DOMINANT, {"us": 0.0, "bytes": 0.0})
         achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9 if k["us"] > 0 else 0.0
-        traffic = None
-        if os.path.exists(args.traffic_file):
-            try:
-                traffic = json.load(open(args.traffic_file)).get(DOMINANT, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        prof_c = committed_profile(args.profile_dir, args.preset)
+        traffic = prof_c.get("hbm_bytes_per_launch")
         cpu = None
         if n == 1 and not args.no_cpu_baseline:
             try:
@@ -259,7 +302,13 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "kernel": "k_matvec<0,true,3> (ffn_gate+ffn_up Q4_K + SwiGLU)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "bytes_per_launch": k["bytes"], "us_per_launch": round(k["us"], 3)},
+                         "traffic_source": (prof_c.get("source") if traffic else
+                                            f"null: no FETCH_SIZE pass committed for preset {args.preset}"),
+                         "bytes_per_launch": k["bytes"], "us_per_launch": round(k["us"], 3),
+                         "us_source": "start/stop events on each launch in this run (llmi_profile_kernels)",
+                         "rocprof_us_per_launch": prof_c.get("rocprof_us"),
+                         "rocprof_frac": (round(k["bytes"] / (prof_c["rocprof_us"] * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+                                          if prof_c.get("rocprof_us") else None)},
             "hbm_end_to_end": {"achieved_GBps": round(e2e_gbps, 1),
                                "frac_of_peak": round(e2e_gbps / HBM_PEAK_GBPS, 4),
                                "bytes_per_token": eng.bytes / max(1, args.steps)},
@@ -271,6 +320,7 @@ def main(argv=None):
                         "tok_per_s": round(args.prompt / max(eng.prefill_warm_s, 1e-9), 1)},
             "fanout_s": round(eng.fanout_s, 3),
             "cpu_baseline": cpu,
+            "env": knobs,
         }
         print(json.dumps(result), flush=True)
     dist.close()

@@ -95,7 +95,8 @@ void llama_batch_free(struct llama_batch batch);
  * and every generated token of /v1/chat/completions (docs/API_REFERENCE.md:341-605,
  * proxied by scripts/gateway.py:699-804).
  * Returns 0 ok; 1 no KV slot (pos >= n_ctx; recoverable); 2 aborted;
- * -1 invalid batch; < -1 fatal.  Synchronises the device before returning. */
+ * -1 invalid batch; < -1 fatal (-6: an in-kernel bounded wait gave up, the outputs of
+ * the call are invalid).  Synchronises the device before returning. */
 int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch);
 /* legacy upstream llama_eval: tokens at positions n_past..n_past+n_tokens-1; 0 = ok */
 int llama_eval(struct llama_context* ctx, llama_token* tokens, int32_t n_tokens, int32_t n_past);
@@ -149,6 +150,14 @@ void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec
  * output(+argmax).  0 on success. */
 int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps,
                              double* us, double* bytes, int32_t* launches);
+/* Test options (tests only; no environment variable reaches these): sets `name` to
+ * `value` (value < 0: query) and returns the previous value, -1 for an unknown name.
+ *   "pf_attn_simple"  1: batched-prefill attention one head per workgroup (bit-identical)
+ *   "pf_max_kv"       longest KV length the batched prefill takes (default 32768); a prompt
+ *                     reaching past it continues as decode steps (bit-identical)
+ *   "xspin_limit"     polls before k_attn_x's bounded wait gives up; a give-up makes the
+ *                     decode call return -6 with llmi_last_error set (fault surfacing) */
+int32_t llmi_test_option(const char* name, int32_t value);
 /* Algorithmic bytes of one decode step at KV length n_kv (weights + one embedding row
  * + norms + KV read/write), the numerator of achieved GB/s. */
 double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv);

@@ -236,6 +236,9 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
         const int p0 = batch.pos ? batch.pos[0] : c.n_past;
         int run = 0;
         while (run < n - 1 && rows[(size_t)run] < 0 && (batch.pos ? batch.pos[run] : c.n_past + run) == p0 + run) ++run;
+        // the batched-prefill attention holds one head's scores in LDS: a run reaching past
+        // pf_max_kv() positions goes through decode steps from there on
+        if (p0 + run > pf_max_kv()) run = std::max(0, pf_max_kv() - p0);
         if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
             if (!prefill_enqueue(c, batch.token, run, p0, err)) {
                 set_err("llama_decode: " + err);
@@ -263,8 +266,10 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
         last_pos = std::max(last_pos, pos);
     }
     hipEventRecord(c.ev1, c.stream);
+    context_fault_readback(c);
     hipError_t e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess) { set_err("llama_decode: " + hip_err(e)); return -4; }
+    if (!context_fault_ok(c, err)) { set_err("llama_decode: " + err); return -6; }
     float ms = 0.f;
     hipEventElapsedTime(&ms, c.ev0, c.ev1);
     c.last_us = ms * 1e3;
@@ -352,8 +357,10 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
     if (n_gen > 1)
         (void)hipMemcpyAsync(h.data(), c.hist + pos0 + 1, (size_t)(n_gen - 1) * 4, hipMemcpyDeviceToHost, c.stream);
     (void)hipMemcpyAsync(keys, &c.st->key[(pos0 + n_gen - 1) & 1][0], sizeof(keys), hipMemcpyDeviceToHost, c.stream);
+    context_fault_readback(c);
     hipError_t e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess) { set_err("llmi_generate_greedy: " + hip_err(e)); return -4; }
+    if (!context_fault_ok(c, err)) { set_err("llmi_generate_greedy: " + err); return -6; }
     for (int k = 0; k + 1 < n_gen; ++k) out[k] = h[(size_t)k];
     out[n_gen - 1] = (llama_token)key_token(keys);
     float ms = 0.f;
@@ -414,6 +421,18 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
     c.n_past = pos0;
     return rc;
     API_CATCH(-5)
+}
+
+int32_t llmi_test_option(const char* name, int32_t value) {
+    if (!name) return -1;
+    int* opt = nullptr;
+    if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
+    else if (!strcmp(name, "pf_max_kv")) opt = &g_pf_max_kv;
+    else if (!strcmp(name, "xspin_limit")) opt = &g_xspin_limit;
+    if (!opt) { set_err("llmi_test_option: unknown option"); return -1; }
+    const int old = *opt;
+    if (value >= 0) *opt = value;
+    return old;
 }
 
 void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec) {

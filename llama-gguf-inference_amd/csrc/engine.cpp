@@ -51,6 +51,7 @@ Context::~Context() {
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (fault_host) (void)hipHostFree(fault_host);
     if (stream) (void)hipStreamDestroy(stream);
     (void)hipSetDevice(cur);
 }
@@ -276,6 +277,9 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string&
     HIPC(hipMalloc(&c.h, (size_t)hp.n_ff * 4));
     HIPC(hipMalloc(&c.logits, (size_t)hp.n_vocab * 4));
     HIPC(hipMalloc(&c.scores, attn_scratch_floats(hp.n_head, c.n_ctx) * 4));
+    c.fault_dev = (unsigned*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx) + 2 * (size_t)hp.n_head * kXAttnMaxKV);
+    HIPC(hipHostMalloc((void**)&c.fault_host, 16, hipHostMallocDefault));
+    *c.fault_host = 0;
     HIPC(hipMalloc(&c.kc, kv_elems * 2));
     HIPC(hipMalloc(&c.vc, kv_elems * 2));
     HIPC(hipMalloc(&c.st, sizeof(StepState)));
@@ -318,6 +322,20 @@ void context_clear(Context& c) {
     (void)hipMemcpyAsync(c.st, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
     (void)hipStreamSynchronize(c.stream);
     c.n_past = 0;
+}
+
+void context_fault_readback(Context& c) {
+    (void)hipMemcpyAsync(c.fault_host, c.fault_dev, 4, hipMemcpyDeviceToHost, c.stream);
+}
+
+bool context_fault_ok(Context& c, std::string& err) {
+    if (*c.fault_host == 0) return true;
+    err = "an in-kernel bounded wait gave up (attention hand-off never completed; device fault word " +
+          std::to_string(*c.fault_host) + "); this call's outputs are invalid";
+    *c.fault_host = 0;
+    (void)hipMemsetAsync(c.fault_dev, 0, 4, c.stream);
+    (void)hipStreamSynchronize(c.stream);
+    return false;
 }
 
 bool Prof::arm() {
@@ -371,8 +389,10 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     ea.cols = E; ea.vocab = hp.n_vocab; ea.x = c.x; ea.st = c.st; ea.hist = c.hist; ea.n_ctx = c.n_ctx;
     Prof* P = c.prof;
     const double kvpos = (double)hp.n_head_kv * D * 2.0;  // bytes of K (or V) per layer per position
-    // experiment hook (timing only, results garbage): LLMI_EXP_SKIP = bitmask of kernel
-    // classes left out of the step, to measure each class's marginal cost in the pipeline
+#if defined(LLMI_EXPERIMENTS)
+    // experiment builds only (make EXTRA=-DLLMI_EXPERIMENTS; results garbage, never in
+    // the product library): LLMI_EXP_SKIP = bitmask of kernel classes left out of the
+    // step, LLMI_EXP_XFIRST = multi-round launches also wait for x before the weights
     static const int exp_skip = [] {
         const char* e = getenv("LLMI_EXP_SKIP");
         return e ? atoi(e) : 0;
@@ -381,6 +401,9 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         const char* e = getenv("LLMI_EXP_XFIRST");
         return e ? atoi(e) : 0;
     }();
+#else
+    constexpr int exp_skip = 0, exp_xfirst = 0;
+#endif
     auto want = [P](int k) { return !(exp_skip >> k & 1) && (!P || P->want(k)); };
     // a filtered launch, armed with an event pair when the profiler asks for timing
 #define LLMI_RUN(K, EXPR)                                  \
@@ -433,7 +456,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
         at.layer = l;
         at.gran = (unsigned long long*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx));
-        at.fault = (unsigned*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx) + 2 * (size_t)hp.n_head * kXAttnMaxKV);
+        at.fault = c.fault_dev;
         LLMI_RUN(K_ATTN, launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---

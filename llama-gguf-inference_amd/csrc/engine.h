@@ -85,6 +85,8 @@ struct Context {
     int n_past = 0;
     std::map<int, hipGraphExec_t> graphs;   // by KV bucket
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    unsigned* fault_dev = nullptr;          // device fault word: a bounded in-kernel wait gave up
+    unsigned* fault_host = nullptr;         // pinned copy, read back with every decode call
     double last_bytes = 0, last_us = 0;
     Prof* prof = nullptr;                   // non-null only inside llmi_profile_kernels
     // batched prefill scratch (allocated on first use; ubatches of <= pf_cap tokens)
@@ -111,6 +113,10 @@ bool prefill_supported(const Model& m);
 // cache written, no logits); enqueued on c.stream, no synchronisation
 bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::string& err);
 void context_clear(Context& c);
+// enqueue the device fault word's read-back (before the call's stream sync) ...
+void context_fault_readback(Context& c);
+// ... and after the sync: false (err set, word re-armed) if an in-kernel wait gave up
+bool context_fault_ok(Context& c, std::string& err);
 size_t model_tensor_bytes(const Model& m);
 // arena layout of a model for another device (replica); no upload
 bool model_clone_layout(const Model& src, int device, Model& dst, std::string& err);

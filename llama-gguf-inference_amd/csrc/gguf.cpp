@@ -127,11 +127,23 @@ bool GgufFile::open(const std::string& path, std::string& err) {
     for (size_t i = 0; i < tensors.size(); ++i) {
         GgufTensor& t = tensors[i];
         if (!type_supported(t.type)) { err = "tensor " + t.name + ": unsupported ggml type " + std::to_string(t.type); return false; }
-        int64_t n = t.ne[0] * t.ne[1] * t.ne[2] * t.ne[3];
-        if (t.ne[0] % block_elems(t.type)) { err = "tensor " + t.name + ": row not a whole number of blocks"; return false; }
-        t.nbytes = (size_t)(n / block_elems(t.type)) * (size_t)block_bytes(t.type);
+        // upstream gguf_init_from_file rejects negative dims and element counts past
+        // INT64_MAX; every product and the end offset are computed overflow-checked
+        int64_t n = 1;
+        for (int d = 0; d < 4; ++d) {
+            if (t.ne[d] < 0) { err = "tensor " + t.name + ": negative dimension"; return false; }
+            if (t.ne[d] != 0 && n > INT64_MAX / t.ne[d]) { err = "tensor " + t.name + ": element count overflows"; return false; }
+            n *= t.ne[d];
+        }
+        if (t.ne[0] == 0 || t.ne[0] % block_elems(t.type)) { err = "tensor " + t.name + ": row not a whole number of blocks"; return false; }
+        const uint64_t nblk = (uint64_t)(n / block_elems(t.type));
+        if (nblk > (uint64_t)file_size / (uint64_t)block_bytes(t.type)) { err = "tensor " + t.name + " extends past end of file"; return false; }
+        t.nbytes = (size_t)nblk * (size_t)block_bytes(t.type);
         if (t.offset % alignment) { err = "tensor " + t.name + ": misaligned offset"; return false; }
-        if (data_start + t.offset + t.nbytes > file_size) { err = "tensor " + t.name + " extends past end of file"; return false; }
+        if (t.offset > file_size || data_start > file_size - t.offset || t.nbytes > file_size - data_start - t.offset) {
+            err = "tensor " + t.name + " extends past end of file";
+            return false;
+        }
         t.data = map + data_start + t.offset;
         index_[t.name] = i;
     }

@@ -1593,7 +1593,7 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
 #pragma unroll
             for (int k = 0; k < NS; ++k) ok &= (uint32_t)(x[k] >> 32) == tag;
             if (__all(ok)) break;
-            if (spins > kXSpinLimit) {
+            if (spins > a.spin_limit) {
                 s_fault = 1;
                 break;
             }
@@ -2142,11 +2142,13 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
     const size_t lds = mv_lds_bytes(act, a.cols);
     int blocks = (a.npairs + kMVWaves - 1) / kMVWaves;
     if (blocks > max_blocks) blocks = max_blocks;
-    static const int exp_blocks = [] {  // experiment hook: fixed grid for launch sweeps
+#if defined(LLMI_EXPERIMENTS)
+    static const int exp_blocks = [] {  // experiment builds: fixed grid for launch sweeps
         const char* e = getenv("LLMI_MV_BLOCKS");
         return e ? atoi(e) : 0;
     }();
     if (exp_blocks > 0 && exp_blocks < blocks) blocks = exp_blocks;
+#endif
 #if defined(LLMI_EXP_BALANCE)
     {  // experiment: equal pairs per wave (fewer workgroups when that divides better)
         const int waves = blocks * kMVWaves, per = (a.npairs + waves - 1) / waves;
@@ -2221,6 +2223,13 @@ static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipSt
     return hipErrorInvalidValue;
 }
 
+// Test options (llmi_test_option; never read from the environment): paths that give
+// bit-identical results, or limits lowered so a test reaches a fallback / fault path.
+int g_pf_attn_simple = 0;               // batched-prefill attention: one head per workgroup
+int g_pf_max_kv = kPfAttnMaxKV;         // longest KV the batched-prefill attention takes
+int g_xspin_limit = kXSpinLimit;        // k_attn_x bounded-wait polls before it faults
+int pf_max_kv() { return g_pf_max_kv; }
+
 static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel, 4 exchange (experiments: LLMI_ATTN_MODE)
 void set_attn_mode(int mode) { g_attn_mode = mode; }
 int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
@@ -2247,8 +2256,10 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     return split_ok ? 2 : fused_ok ? 1 : 3;
 }
 
-hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
+hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    AttnArgs a = a0;
+    a.spin_limit = g_xspin_limit;
     const int g = n_head / n_head_kv;
     int path = attn_path(n_head, n_head_kv, kv_bound, head_dim);
     if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254))

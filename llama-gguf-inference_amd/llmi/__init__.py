@@ -34,6 +34,14 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
+def test_option(name: str, value: int = -1) -> int:
+    """llmi_test_option: set a test-only option (value < 0: query); returns the old value."""
+    r = int(lib().llmi_test_option(name.encode(), int(value)))
+    if r < 0:
+        raise LlmiError(last_error())
+    return r
+
+
 def device_count() -> int:
     return int(lib().llmi_device_count())
 

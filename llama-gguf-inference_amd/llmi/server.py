@@ -11,7 +11,8 @@ module answers that contract:
   GET  /v1/models              OpenAI model list
   POST /v1/completions         prompt: str | [token ids]; non-stream or SSE
   POST /v1/chat/completions    messages -> chat template -> tokens; non-stream or SSE
-  Authorization: Bearer <key> required on /v1/* when a key is configured (401 otherwise)
+  Authorization: Bearer <key> required on every route but /health when a key is
+  configured (401 otherwise; llama-server's public endpoints are /health and /v1/health)
 
 Decoding is greedy (temperature is accepted and ignored: the north star's workload is
 greedy); `ignore_eos` and `n_predict` follow llama-server.  Every GPU replica is one
@@ -185,8 +186,10 @@ class Handler(BaseHTTPRequestHandler):
         self.wfile.write(body)
         self.close_connection = True
 
-    def _authorized(self) -> bool:
-        if not self.api_key:
+    PUBLIC = ("/health", "/v1/health")
+
+    def _authorized(self, route: str) -> bool:
+        if not self.api_key or route in self.PUBLIC:
             return True
         return self.headers.get("Authorization", "") == f"Bearer {self.api_key}"
 
@@ -201,15 +204,16 @@ class Handler(BaseHTTPRequestHandler):
     # ---- routes
     def do_GET(self):
         eng = self.engine
-        if self.path.split("?")[0] == "/health":
+        route = self.path.split("?")[0]
+        if route in self.PUBLIC:
             if eng.error:
                 return self._send_json(500, {"status": "error", "error": eng.error})
             if not eng.ready:
                 return self._send_json(503, _error(503, "Loading model", "unavailable_error"))
             return self._send_json(200, {"status": "ok"})
-        if not self._authorized():
+        if not self._authorized(route):
             return self._send_json(401, _error(401, "Invalid API Key", "authentication_error"))
-        if self.path.split("?")[0] == "/v1/models":
+        if route == "/v1/models":
             return self._send_json(200, {"object": "list", "data": [
                 {"id": eng.model_id, "object": "model", "created": int(time.time()), "owned_by": "llmi"}]})
         return self._send_json(404, _error(404, "File Not Found", "not_found_error"))
@@ -217,7 +221,7 @@ class Handler(BaseHTTPRequestHandler):
     def do_POST(self):
         eng = self.engine
         route = self.path.split("?")[0]
-        if route.startswith("/v1/") and not self._authorized():
+        if not self._authorized(route):
             return self._send_json(401, _error(401, "Invalid API Key", "authentication_error"))
         if route not in ("/v1/completions", "/v1/chat/completions", "/completion"):
             return self._send_json(404, _error(404, "File Not Found", "not_found_error"))
@@ -255,7 +259,10 @@ class Handler(BaseHTTPRequestHandler):
         created = int(time.time())
         obj = "chat.completion" if chat else "text_completion"
         if not stream:
-            ids, finish = eng.generate(prompt, max_tokens, ignore_eos, lambda _t: None, chunk=32)
+            try:
+                ids, finish = eng.generate(prompt, max_tokens, ignore_eos, lambda _t: None, chunk=32)
+            except Exception as e:  # a failed llama_decode: OpenAI-shaped 500, not a dropped socket
+                return self._send_json(500, _error(500, str(e), "server_error"))
             text = v.detokenize(ids)
             choice = ({"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": finish}
                       if chat else {"index": 0, "text": text, "logprobs": None, "finish_reason": finish})
@@ -299,6 +306,11 @@ class Handler(BaseHTTPRequestHandler):
             self.wfile.flush()
         except (BrokenPipeError, ConnectionResetError):
             pass
+        except Exception as e:  # decode failed mid-stream: an error event, then close
+            try:
+                event(_error(500, str(e), "server_error"))
+            except (BrokenPipeError, ConnectionResetError):
+                pass
 
 
 def make_server(engine: Engine, host: str, port: int, api_key: Optional[str]) -> ThreadingHTTPServer:

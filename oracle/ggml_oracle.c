@@ -17,6 +17,9 @@
 
 #include <fcntl.h>
 #include <math.h>
+#if defined(__AVX2__)
+#include <immintrin.h>
+#endif
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -399,25 +402,185 @@ static float chunk_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int c)
     return (llmi_h2f(d16) * dA) * (float)isum - (llmi_h2f(m16) * dA) * (float)imin;
 }
 
+/* Unpack one K-quant block into its 256 unsigned quant values in natural element order
+ * (Q4_K 0..15, Q5_K 0..31, Q6_K 0..63; the generic functions' unpack loops, without
+ * Q6_K's -32), then the 16-element integer dots against the q8_K block: every chunk's
+ * integer sums are made of these exactly (sums of products, any grouping). */
+static void block_unpack_kq(int wtype, const uint8_t* blk, uint8_t* u) {
+    if (wtype == OR_Q6_K) {
+        const block_q6_K* x = (const block_q6_K*)blk;
+        const uint8_t* ql = x->ql; const uint8_t* qh = x->qh;
+        uint8_t* a = u;
+        for (int j = 0; j < QK_K; j += 128) {
+            for (int l = 0; l < 32; ++l) {
+                a[l + 0] = (uint8_t)((ql[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4));
+                a[l + 32] = (uint8_t)((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4));
+                a[l + 64] = (uint8_t)((ql[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4));
+                a[l + 96] = (uint8_t)((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4));
+            }
+            a += 128; ql += 64; qh += 32;
+        }
+    } else {
+        const uint8_t* qs; const uint8_t* hm = NULL;
+        if (wtype == OR_Q4_K) qs = ((const block_q4_K*)blk)->qs;
+        else { qs = ((const block_q5_K*)blk)->qs; hm = ((const block_q5_K*)blk)->qh; }
+        for (int j = 0; j < QK_K / 64; ++j) {
+            for (int l = 0; l < 32; ++l) u[64 * j + l] = (uint8_t)(qs[32 * j + l] & 0xF);
+            for (int l = 0; l < 32; ++l) u[64 * j + 32 + l] = (uint8_t)(qs[32 * j + l] >> 4);
+            if (hm) {
+                for (int l = 0; l < 32; ++l) u[64 * j + l] += (hm[l] >> (2 * j)) & 1 ? 16 : 0;
+                for (int l = 0; l < 32; ++l) u[64 * j + 32 + l] += (hm[l] >> (2 * j + 1)) & 1 ? 16 : 0;
+            }
+        }
+    }
+}
+static void block_dots16(const uint8_t* u, const block_q8_K* y, int dots[16]) {
+#if defined(__AVX2__)
+    /* the same exact integer sums (u <= 63, |a| <= 128: no int16 saturation in maddubs) */
+    const __m256i ones = _mm256_set1_epi16(1);
+    for (int j = 0; j < 16; j += 2) {
+        const __m256i uv = _mm256_loadu_si256((const __m256i*)(u + 16 * j));
+        const __m256i av = _mm256_loadu_si256((const __m256i*)(y->qs + 16 * j));
+        const __m256i p4 = _mm256_madd_epi16(_mm256_maddubs_epi16(uv, av), ones); /* 8 x sum of 4 */
+        const __m256i h = _mm256_hadd_epi32(p4, p4);  /* per 128-bit half: [s01, s23, s01, s23] */
+        const __m256i h2 = _mm256_hadd_epi32(h, h);
+        dots[j] = _mm256_extract_epi32(h2, 0);
+        dots[j + 1] = _mm256_extract_epi32(h2, 4);
+    }
+#else
+    for (int j = 0; j < 16; ++j) {
+        int d = 0;
+        for (int t = 0; t < 16; ++t) d += (int)u[16 * j + t] * (int)y->qs[16 * j + t];
+        dots[j] = d;
+    }
+#endif
+}
+
+/* chunk c (64 weights) of a K-quant block from its 16-element dots: the kernel's
+ * dot_chunk (kernels.hip) formula, fp32 exactly as written there */
+static float chunk_from_dots(int wtype, const uint8_t* blk, const block_q8_K* y, const int dots[16], int c) {
+    const int16_t* bs = y->bsums + 4 * c;
+    if (wtype == OR_Q6_K) {
+        const block_q6_K* x = (const block_q6_K*)blk;
+        int isum = 0;
+        for (int m = 0; m < 4; ++m) isum += x->scales[4 * c + m] * (dots[4 * c + m] - 32 * bs[m]);
+        return (llmi_h2f(x->d) * y->d) * (float)isum;
+    }
+    const uint8_t* scales; uint16_t d16, m16;
+    if (wtype == OR_Q4_K) { const block_q4_K* x = (const block_q4_K*)blk; scales = x->scales; d16 = x->d; m16 = x->dmin; }
+    else { const block_q5_K* x = (const block_q5_K*)blk; scales = x->scales; d16 = x->d; m16 = x->dmin; }
+    uint8_t sc0, m0, sc1, m1;
+    get_scale_min_k4(2 * c, scales, &sc0, &m0);
+    get_scale_min_k4(2 * c + 1, scales, &sc1, &m1);
+    const int lo = dots[4 * c] + dots[4 * c + 1], hi = dots[4 * c + 2] + dots[4 * c + 3];
+    const int isum = sc0 * lo + sc1 * hi;
+    const int imin = m0 * (bs[0] + bs[1]) + m1 * (bs[2] + bs[3]);
+    const float dA = y->d;
+    return (llmi_h2f(d16) * dA) * (float)isum - (llmi_h2f(m16) * dA) * (float)imin;
+}
+
 static float vd_device_order(int wtype, int n, const void* w, const void* act) {
     float acc[64];
     for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
     const int nch = n / 64;
-    for (int ci = 0; ci < nch; ++ci) {
-        float v;
-        if (wtype == OR_Q8_0) {
+    if (wtype == OR_Q8_0) {
+        for (int ci = 0; ci < nch; ++ci) {
             const block_q8_0* x = (const block_q8_0*)w + 2 * ci;
             const block_q8_0* y = (const block_q8_0*)act + 2 * ci;
             int s0 = 0, s1 = 0;
             for (int j = 0; j < 32; ++j) { s0 += x[0].qs[j] * y[0].qs[j]; s1 += x[1].qs[j] * y[1].qs[j]; }
-            v = (float)s0 * (llmi_h2f(x[0].d) * llmi_h2f(y[0].d)) + (float)s1 * (llmi_h2f(x[1].d) * llmi_h2f(y[1].d));
-        } else {
-            const size_t bb = or_type_size(wtype);
-            v = chunk_kq(wtype, (const uint8_t*)w + (size_t)(ci / 4) * bb, (const block_q8_K*)act + ci / 4, ci % 4);
+            const float v = (float)s0 * (llmi_h2f(x[0].d) * llmi_h2f(y[0].d)) + (float)s1 * (llmi_h2f(x[1].d) * llmi_h2f(y[1].d));
+            acc[ci % 64] = acc[ci % 64] + v;
         }
-        acc[ci % 64] = acc[ci % 64] + v;
+    } else {
+        const size_t bb = or_type_size(wtype);
+        for (int ib = 0; ib < nch / 4; ++ib) {
+            const uint8_t* blk = (const uint8_t*)w + (size_t)ib * bb;
+            const block_q8_K* y = (const block_q8_K*)act + ib;
+            int dots[16];
+            uint8_t u[QK_K];
+            block_unpack_kq(wtype, blk, u);
+            block_dots16(u, y, dots);
+            for (int c = 0; c < 4; ++c) {
+                const int ci = 4 * ib + c;
+                acc[ci % 64] = acc[ci % 64] + chunk_from_dots(wtype, blk, y, dots, c);
+            }
+        }
     }
     /* xor butterfly, steps 1,2,4,8,16,32 (kernels.hip wave_sum: DPP + permlane swaps) */
+    for (int o = 1; o < 64; o <<= 1) {
+        float nxt[64];
+        for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
+        for (int l = 0; l < 64; ++l) acc[l] = nxt[l];
+    }
+    return acc[0];
+}
+
+/* vd_device_order for a K-quant row whose quant values are already unpacked (u: the
+ * row's block_unpack_kq output) and whose per-block constants are decoded once
+ * (RowConst: h2f(d), h2f(dmin), the 6-bit scales/mins or Q6_K's int8 scales): identical
+ * operations, hoisted out of the token loop of or_prefill. */
+typedef struct { float d, dmin; int sc[16], mn[8]; } RowConst;
+
+static void row_consts(int wtype, const uint8_t* blk, RowConst* rc) {
+    if (wtype == OR_Q6_K) {
+        const block_q6_K* x = (const block_q6_K*)blk;
+        rc->d = llmi_h2f(x->d); rc->dmin = 0.f;
+        for (int j = 0; j < 16; ++j) rc->sc[j] = x->scales[j];
+        return;
+    }
+    const uint8_t* scales; uint16_t d16, m16;
+    if (wtype == OR_Q4_K) { const block_q4_K* x = (const block_q4_K*)blk; scales = x->scales; d16 = x->d; m16 = x->dmin; }
+    else { const block_q5_K* x = (const block_q5_K*)blk; scales = x->scales; d16 = x->d; m16 = x->dmin; }
+    rc->d = llmi_h2f(d16); rc->dmin = llmi_h2f(m16);
+    for (int j = 0; j < 8; ++j) { uint8_t a, b; get_scale_min_k4(j, scales, &a, &b); rc->sc[j] = a; rc->mn[j] = b; }
+}
+
+static float vd_device_order_unpacked(int wtype, int n, const RowConst* rcs, const uint8_t* u, const void* act) {
+    float acc[64];
+    for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
+    for (int ib = 0; ib < n / QK_K; ++ib) {
+        const block_q8_K* y = (const block_q8_K*)act + ib;
+        const RowConst* rc = rcs + ib;
+        int dots[16];
+        block_dots16(u + (size_t)ib * QK_K, y, dots);
+        const float dA = y->d;
+        for (int c = 0; c < 4; ++c) {
+            const int16_t* bs = y->bsums + 4 * c;
+            float v;
+            if (wtype == OR_Q6_K) {
+                int isum = 0;
+                for (int m = 0; m < 4; ++m) isum += rc->sc[4 * c + m] * (dots[4 * c + m] - 32 * bs[m]);
+                v = (rc->d * dA) * (float)isum;
+            } else {
+                const int lo = dots[4 * c] + dots[4 * c + 1], hi = dots[4 * c + 2] + dots[4 * c + 3];
+                const int isum = rc->sc[2 * c] * lo + rc->sc[2 * c + 1] * hi;
+                const int imin = rc->mn[2 * c] * (bs[0] + bs[1]) + rc->mn[2 * c + 1] * (bs[2] + bs[3]);
+                v = (rc->d * dA) * (float)isum - (rc->dmin * dA) * (float)imin;
+            }
+            const int ci = 4 * ib + c;
+            acc[ci % 64] = acc[ci % 64] + v;
+        }
+    }
+    for (int o = 1; o < 64; o <<= 1) {
+        float nxt[64];
+        for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
+        for (int l = 0; l < 64; ++l) acc[l] = nxt[l];
+    }
+    return acc[0];
+}
+
+/* The device order once more, chunk by chunk with per-element unpacking (chunk_kq):
+ * an independent restatement tests pin vd_device_order's vectorised block dots against
+ * (tests/test_oracle_simd.py). */
+float or_vec_dot_device_ref(int wtype, int n, const void* w, const void* act) {
+    float acc[64];
+    for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
+    const int nch = n / 64;
+    if (wtype == OR_Q8_0) return vd_device_order(wtype, n, w, act);
+    const size_t bb = or_type_size(wtype);
+    for (int ci = 0; ci < nch; ++ci)
+        acc[ci % 64] = acc[ci % 64] + chunk_kq(wtype, (const uint8_t*)w + (size_t)(ci / 4) * bb, (const block_q8_K*)act + ci / 4, ci % 4);
     for (int o = 1; o < 64; o <<= 1) {
         float nxt[64];
         for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
@@ -724,6 +887,40 @@ static void matvec_t(const or_tensor* T, const float* x, float* y, int nth) {
     or_matvec(T->type, T->data, T->ne[1], T->ne[0], x, y, nth);
 }
 
+/* Non-flash attention of query head h (roped q, f32[D]) over the layer's first n_kv
+ * cached positions: kq = mul_mat(K_f16, q) with q rounded to f16 (ggml_vec_dot_f16,
+ * double sum), soft_max_ext(kq, scale 1/sqrt(D)) with a double sum, kqv =
+ * mul_mat(V_f16, kq) with the probabilities rounded to f16.  w: f32[n_kv] scratch. */
+static void attn_head(const or_model* m, int l, const float* q, int h, int n_kv, float* w, float* out) {
+    const int HK = m->n_head_kv, D = m->head_dim, kvd = HK * D, g = h / (m->n_head / HK);
+    const uint16_t* kl = m->kc + ((size_t)l * m->n_ctx) * kvd;
+    const uint16_t* vl = m->vc + ((size_t)l * m->n_ctx) * kvd;
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    /* f16-rounded q and K/V values as floats (the same values vd_f16 and the PV loop
+     * form per element; converted once instead of once per use) */
+    float qf[512];
+    for (int d = 0; d < D; ++d) qf[d] = llmi_h2f(llmi_f2h(q[d]));
+    float mx = -INFINITY;
+    for (int t = 0; t < n_kv; ++t) {
+        const uint16_t* kr = kl + (size_t)t * kvd + (size_t)g * D;
+        double sumf = 0.0;  /* ggml_vec_dot_f16 (generic): double accumulation */
+        for (int d = 0; d < D; ++d) sumf += (double)(llmi_h2f(kr[d]) * qf[d]);
+        w[t] = (float)sumf * kq_scale;
+        mx = fmaxf(mx, w[t]);
+    }
+    double sum = 0.0;
+    for (int t = 0; t < n_kv; ++t) { float e = llmi_expf(w[t] - mx); sum += (double)e; w[t] = e; }
+    const float inv = (float)(1.0 / sum);
+    for (int t = 0; t < n_kv; ++t) w[t] = llmi_h2f(llmi_f2h(w[t] * inv));  /* p rounded to f16 */
+    double acc[512];
+    for (int d = 0; d < D; ++d) acc[d] = 0.0;
+    for (int t = 0; t < n_kv; ++t) {  /* per d the same sequential double sum over t */
+        const uint16_t* vr = vl + (size_t)t * kvd + (size_t)g * D;
+        for (int d = 0; d < D; ++d) acc[d] += (double)(llmi_h2f(vr[d]) * w[t]);
+    }
+    for (int d = 0; d < D; ++d) out[d] = (float)acc[d];
+}
+
 /* One decode step of llm_build_llama [upstream llama-model.cpp] with the non-flash
  * attention path: kq = mul_mat(K_f16, q) (q rounded to f16, ggml_vec_dot_f16),
  * soft_max_ext(kq, scale = 1/sqrt(head_dim)) with double sum, kqv = mul_mat(V_f16,
@@ -732,7 +929,7 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
     if (token < 0 || token >= m->n_vocab) { snprintf(g_err, sizeof g_err, "token %d out of range", token); return -1; }
     if (pos < 0 || pos >= m->n_ctx) { snprintf(g_err, sizeof g_err, "pos %d out of ctx", pos); return 1; }
     const int E = m->n_embd, H = m->n_head, HK = m->n_head_kv, D = m->head_dim, F = m->n_ff;
-    const int kvd = HK * D, gqa = H / HK, n_kv = pos + 1;
+    const int kvd = HK * D, n_kv = pos + 1;
     const float* ff = m->rope_freqs ? (const float*)m->rope_freqs->data : NULL;
     /* get_rows(token_embd, token) -> dequantize one row */
     {
@@ -740,7 +937,6 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
         or_dequantize_row(m->tok_embd->type, m->tok_embd->data + (size_t)token * rb, m->x, E);
         memcpy(m->tap_embd, m->x, (size_t)E * 4);
     }
-    const float kq_scale = 1.0f / sqrtf((float)D);
     for (int l = 0; l < m->n_layer; ++l) {
         or_rms_norm_mul(m->x, (const float*)m->L[l].an->data, m->xb, E, m->eps);
         matvec_t(m->L[l].wq, m->xb, m->q, nth);
@@ -752,28 +948,7 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
         uint16_t* vl = m->vc + ((size_t)l * m->n_ctx) * kvd;
         for (int i = 0; i < kvd; ++i) { kl[(size_t)pos * kvd + i] = llmi_f2h(m->k[i]); vl[(size_t)pos * kvd + i] = llmi_f2h(m->v[i]); }
 #pragma omp parallel for schedule(static) num_threads(nth > 0 ? nth : 1)
-        for (int h = 0; h < H; ++h) {
-            const int g = h / gqa;
-            uint16_t qh[512];
-            for (int d = 0; d < D; ++d) qh[d] = llmi_f2h(m->q[(size_t)h * D + d]);
-            float* w = m->sc + (size_t)h * m->n_ctx;
-            float mx = -INFINITY;
-            for (int t = 0; t < n_kv; ++t) {
-                float s = vd_f16(D, kl + (size_t)t * kvd + (size_t)g * D, qh);
-                w[t] = s * kq_scale;
-                mx = fmaxf(mx, w[t]);
-            }
-            double sum = 0.0;
-            for (int t = 0; t < n_kv; ++t) { float e = llmi_expf(w[t] - mx); sum += (double)e; w[t] = e; }
-            const float inv = (float)(1.0 / sum);
-            for (int t = 0; t < n_kv; ++t) w[t] = w[t] * inv;
-            for (int d = 0; d < D; ++d) {
-                double acc = 0.0;
-                for (int t = 0; t < n_kv; ++t)
-                    acc += (double)(llmi_h2f(vl[(size_t)t * kvd + (size_t)g * D + d]) * llmi_h2f(llmi_f2h(w[t])));
-                m->att[(size_t)h * D + d] = (float)acc;
-            }
-        }
+        for (int h = 0; h < H; ++h) attn_head(m, l, m->q + (size_t)h * D, h, n_kv, m->sc + (size_t)h * m->n_ctx, m->att + (size_t)h * D);
         matvec_t(m->L[l].wo, m->att, m->tmp, nth);
         for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
         or_rms_norm_mul(m->x, (const float*)m->L[l].fn->data, m->xb, E, m->eps);
@@ -784,8 +959,106 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
         for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
     }
     memcpy(m->tap_final, m->x, (size_t)E * 4);
+    if (!logits) return 0;  /* prompt token whose logits nobody reads: KV cache only */
     or_rms_norm_mul(m->x, (const float*)m->out_norm->data, m->xb, E, m->eps);
     or_matvec(m->output->type, m->output->data, m->n_vocab, E, m->xb, logits, nth);
+    return 0;
+}
+
+/* T consecutive or_decode steps at positions pos0.. with no logits (a prompt), the
+ * loops reordered for speed: per layer each weight row is unpacked once and dotted with
+ * the T activations (device order: vd_device_order_unpacked; generic order: or_vec_dot
+ * per token), then attention per (token, head).  Every token's operations are exactly
+ * or_decode's (the KV rows a token attends to are written by the same layer before).
+ * Leaves the last token's state (x, taps) as or_decode would.  Test infrastructure for
+ * the long parity tests (2048-token prompts at 7B widths). */
+static void matmul_t(const or_tensor* W, const float* X, int T, float* Y, int nth) {
+    const int wtype = W->type;
+    const int64_t rows = W->ne[1], cols = W->ne[0];
+    const size_t ab = act_bytes(wtype, cols);
+    uint8_t* acts = malloc(ab * (size_t)T);
+    for (int t = 0; t < T; ++t) quantize_act(wtype, X + (size_t)t * cols, acts + ab * t, cols);
+    const size_t row_bytes = (size_t)(cols / or_block_size(wtype)) * or_type_size(wtype);
+    const int kq = wtype == OR_Q4_K || wtype == OR_Q5_K || wtype == OR_Q6_K;
+#pragma omp parallel num_threads(nth > 0 ? nth : 1)
+    {
+        uint8_t* u = malloc((size_t)cols);
+        RowConst* rcs = malloc(sizeof(RowConst) * (size_t)(cols / QK_K + 1));
+        const size_t bb = or_type_size(wtype);
+#pragma omp for schedule(dynamic, 8)
+        for (int64_t r = 0; r < rows; ++r) {
+            const uint8_t* w = (const uint8_t*)W->data + (size_t)r * row_bytes;
+            if (g_dot_order == 1 && kq) {
+                for (int64_t ib = 0; ib < cols / QK_K; ++ib) {
+                    block_unpack_kq(wtype, w + (size_t)ib * bb, u + ib * QK_K);
+                    row_consts(wtype, w + (size_t)ib * bb, rcs + ib);
+                }
+                for (int t = 0; t < T; ++t) Y[(size_t)t * rows + r] = vd_device_order_unpacked(wtype, (int)cols, rcs, u, acts + ab * t);
+            } else {
+                for (int t = 0; t < T; ++t) Y[(size_t)t * rows + r] = or_vec_dot(wtype, (int)cols, w, acts + ab * t);
+            }
+        }
+        free(u);
+        free(rcs);
+    }
+    free(acts);
+}
+
+int or_prefill(or_model* m, const int32_t* tokens, int T, int pos0, int nth) {
+    if (T <= 0 || pos0 < 0 || pos0 + T > m->n_ctx) { snprintf(g_err, sizeof g_err, "prefill range out of ctx"); return 1; }
+    for (int t = 0; t < T; ++t)
+        if (tokens[t] < 0 || tokens[t] >= m->n_vocab) { snprintf(g_err, sizeof g_err, "token %d out of range", tokens[t]); return -1; }
+    const int E = m->n_embd, H = m->n_head, HK = m->n_head_kv, D = m->head_dim, F = m->n_ff, kvd = HK * D, QD = H * D;
+    const float* ff = m->rope_freqs ? (const float*)m->rope_freqs->data : NULL;
+    float* X = malloc((size_t)T * E * 4); float* XB = malloc((size_t)T * E * 4); float* TMP = malloc((size_t)T * E * 4);
+    float* Q = malloc((size_t)T * QD * 4); float* K = malloc((size_t)T * kvd * 4); float* V = malloc((size_t)T * kvd * 4);
+    float* ATT = malloc((size_t)T * QD * 4); float* HB = malloc((size_t)T * F * 4); float* HB2 = malloc((size_t)T * F * 4);
+    const size_t rb = tensor_bytes(m->tok_embd) / m->n_vocab;
+    for (int t = 0; t < T; ++t) or_dequantize_row(m->tok_embd->type, m->tok_embd->data + (size_t)tokens[t] * rb, X + (size_t)t * E, E);
+    for (int l = 0; l < m->n_layer; ++l) {
+        for (int t = 0; t < T; ++t) or_rms_norm_mul(X + (size_t)t * E, (const float*)m->L[l].an->data, XB + (size_t)t * E, E, m->eps);
+        matmul_t(m->L[l].wq, XB, T, Q, nth);
+        matmul_t(m->L[l].wk, XB, T, K, nth);
+        matmul_t(m->L[l].wv, XB, T, V, nth);
+        uint16_t* kl = m->kc + ((size_t)l * m->n_ctx) * kvd;
+        uint16_t* vl = m->vc + ((size_t)l * m->n_ctx) * kvd;
+        for (int t = 0; t < T; ++t) {
+            rope_norm(Q + (size_t)t * QD, H, D, m->n_rot, pos0 + t, m->rope_base, ff);
+            rope_norm(K + (size_t)t * kvd, HK, D, m->n_rot, pos0 + t, m->rope_base, ff);
+            for (int i = 0; i < kvd; ++i) {
+                kl[(size_t)(pos0 + t) * kvd + i] = llmi_f2h(K[(size_t)t * kvd + i]);
+                vl[(size_t)(pos0 + t) * kvd + i] = llmi_f2h(V[(size_t)t * kvd + i]);
+            }
+        }
+#pragma omp parallel num_threads(nth > 0 ? nth : 1)
+        {
+            float* w = malloc((size_t)m->n_ctx * 4);
+#pragma omp for schedule(dynamic, 1)
+            for (int th = 0; th < T * H; ++th) {
+                const int t = th / H, h = th % H;
+                attn_head(m, l, Q + (size_t)t * QD + (size_t)h * D, h, pos0 + t + 1, w, ATT + (size_t)t * QD + (size_t)h * D);
+            }
+            free(w);
+        }
+        matmul_t(m->L[l].wo, ATT, T, TMP, nth);
+        for (size_t i = 0; i < (size_t)T * E; ++i) X[i] = TMP[i] + X[i];
+        for (int t = 0; t < T; ++t) or_rms_norm_mul(X + (size_t)t * E, (const float*)m->L[l].fn->data, XB + (size_t)t * E, E, m->eps);
+        matmul_t(m->L[l].wg, XB, T, HB, nth);
+        matmul_t(m->L[l].wu, XB, T, HB2, nth);
+        for (size_t i = 0; i < (size_t)T * F; ++i) HB[i] = llmi_silu(HB[i]) * HB2[i];
+        matmul_t(m->L[l].wd, HB, T, TMP, nth);
+        for (size_t i = 0; i < (size_t)T * E; ++i) X[i] = TMP[i] + X[i];
+        if (l == m->n_layer - 1) {  /* the last token's taps, as or_decode leaves them */
+            memcpy(m->q, Q + (size_t)(T - 1) * QD, (size_t)QD * 4);
+            memcpy(m->k, K + (size_t)(T - 1) * kvd, (size_t)kvd * 4);
+            memcpy(m->v, V + (size_t)(T - 1) * kvd, (size_t)kvd * 4);
+            memcpy(m->att, ATT + (size_t)(T - 1) * QD, (size_t)QD * 4);
+            memcpy(m->hb, HB + (size_t)(T - 1) * F, (size_t)F * 4);
+        }
+    }
+    memcpy(m->x, X + (size_t)(T - 1) * E, (size_t)E * 4);
+    memcpy(m->tap_final, m->x, (size_t)E * 4);
+    free(X); free(XB); free(TMP); free(Q); free(K); free(V); free(ATT); free(HB); free(HB2);
     return 0;
 }
 
@@ -806,4 +1079,29 @@ int or_tap(const or_model* m, int which, float* out) {
     }
     else return -1;
     return 0;
+}
+
+/* Host DRAM streaming-read rate (bench.py's CPU roofline beside the CPU baseline): every
+ * thread sums its share of a `bytes` buffer (touched first), best of `reps` passes.
+ * Returns GB/s. */
+double or_host_stream_gbps(size_t bytes, int reps, int nth) {
+    const size_t n = bytes / 8;
+    uint64_t* buf = (uint64_t*)malloc(n * 8);
+    if (!buf) return -1.0;
+#pragma omp parallel for schedule(static) num_threads(nth > 0 ? nth : 1)
+    for (size_t i = 0; i < n; ++i) buf[i] = i;
+    double best = 0.0;
+    volatile uint64_t sink = 0;
+    for (int r = 0; r < reps; ++r) {
+        const double t0 = omp_get_wtime();
+        uint64_t s = 0;
+#pragma omp parallel for schedule(static) reduction(+ : s) num_threads(nth > 0 ? nth : 1)
+        for (size_t i = 0; i < n; ++i) s += buf[i];
+        const double dt = omp_get_wtime() - t0;
+        sink += s;
+        if (dt > 0 && (double)bytes / dt / 1e9 > best) best = (double)bytes / dt / 1e9;
+    }
+    (void)sink;
+    free(buf);
+    return best;
 }

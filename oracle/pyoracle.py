@@ -12,13 +12,25 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "libggml_oracle.so")
+LIB_GENERIC = os.path.join(HERE, "build", "libggml_oracle.so")
+LIB_SIMD = os.path.join(HERE, "build", "libggml_oracle_simd.so")
+# LLMI_ORACLE=simd selects the -O3 -march=x86-64-v3 build of the same source (bit-identical
+# results, tests/test_oracle_simd.py); default: the -O2 generic build
+LIB = LIB_SIMD if os.environ.get("LLMI_ORACLE") == "simd" else LIB_GENERIC
 
 F32, F16, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 8, 12, 13, 14, 15
 BLOCK_ELEMS = {F32: 1, F16: 1, Q8_0: 32, Q4_K: 256, Q5_K: 256, Q6_K: 256, Q8_K: 256}
 BLOCK_BYTES = {F32: 4, F16: 2, Q8_0: 34, Q4_K: 144, Q5_K: 176, Q6_K: 210, Q8_K: 292}
 
 _lib = None
+
+
+def prefer_simd() -> None:
+    """Use the -O3 -march=x86-64-v3 build (bit-identical, faster) if the library is not
+    loaded yet in this process (the GPU tests call this; CPU tests keep the -O2 build)."""
+    global LIB
+    if _lib is None and os.path.exists(LIB_SIMD):
+        LIB = LIB_SIMD
 
 
 def build() -> str:
@@ -45,6 +57,7 @@ def lib() -> C.CDLL:
         "or_quantize_row_q8_K": (None, [P, P, C.c_int64]),
         "or_quantize_row_q8_0": (None, [P, P, C.c_int64]),
         "or_vec_dot": (C.c_float, [C.c_int, C.c_int, P, P]),
+        "or_vec_dot_device_ref": (C.c_float, [C.c_int, C.c_int, P, P]),
         "or_matvec": (C.c_int, [C.c_int, P, C.c_int64, C.c_int64, P, P, C.c_int]),
         "or_rms_norm_mul": (None, [P, P, P, C.c_int, C.c_float]),
         "or_set_dot_order": (None, [C.c_int]),
@@ -55,6 +68,8 @@ def lib() -> C.CDLL:
         "or_model_info": (None, [P, P]),
         "or_decode": (C.c_int, [P, C.c_int32, C.c_int32, P, C.c_int]),
         "or_kv_clear": (None, [P]),
+        "or_prefill": (C.c_int, [P, P, C.c_int, C.c_int32, C.c_int]),
+        "or_host_stream_gbps": (C.c_double, [C.c_size_t, C.c_int, C.c_int]),
         "or_tap": (C.c_int, [P, C.c_int, P]),
         "or_bytes_per_token": (C.c_double, [P, C.c_int]),
     }
@@ -72,6 +87,29 @@ def _p(a: np.ndarray):
 
 def nthreads() -> int:
     return max(1, min(16, os.cpu_count() or 1))
+
+
+def physical_cores() -> int:
+    """Physical cores of this host (unique (package, core) pairs in /proc/cpuinfo)."""
+    pairs, phys, core = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("physical id"):
+                    phys = ln.split(":")[1].strip()
+                elif ln.startswith("core id"):
+                    core = ln.split(":")[1].strip()
+                elif not ln.strip():
+                    if core is not None:
+                        pairs.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    return len(pairs) or (os.cpu_count() or 1)
+
+
+def host_stream_gbps(nbytes: int = 1 << 30, reps: int = 3, threads: int = 0) -> float:
+    return float(lib().or_host_stream_gbps(int(nbytes), int(reps), threads or nthreads()))
 
 
 def dequantize(type_: int, raw: np.ndarray, n: int) -> np.ndarray:
@@ -145,12 +183,21 @@ class OracleModel:
          self.n_rot, self.n_ctx, self.head_dim, self.file_type) = (int(v) for v in info)
         self.threads = threads or nthreads()
 
-    def decode(self, token: int, pos: int) -> np.ndarray:
-        out = np.empty(self.n_vocab, dtype=np.float32)
-        rc = lib().or_decode(self._h, int(token), int(pos), _p(out), self.threads)
+    def decode(self, token: int, pos: int, logits: bool = True) -> np.ndarray | None:
+        """One decode step; logits=False skips the output head (prompt tokens)."""
+        out = np.empty(self.n_vocab, dtype=np.float32) if logits else None
+        rc = lib().or_decode(self._h, int(token), int(pos), _p(out) if logits else None, self.threads)
         if rc != 0:
             raise RuntimeError(f"or_decode rc={rc}: " + lib().or_last_error().decode())
         return out
+
+    def prefill(self, tokens, pos0: int = 0) -> None:
+        """T decode steps at pos0.. with no logits (or_prefill: the same operations per
+        token, loops reordered so each weight row is unpacked once)."""
+        toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
+        rc = lib().or_prefill(self._h, _p(toks), int(toks.size), int(pos0), self.threads)
+        if rc != 0:
+            raise RuntimeError(f"or_prefill rc={rc}: " + lib().or_last_error().decode())
 
     def tap(self, which: int) -> np.ndarray:
         out = np.empty(self.n_embd, dtype=np.float32)

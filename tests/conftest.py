@@ -43,6 +43,9 @@ def gpu():
     import torch
 
     assert torch.cuda.is_available(), "gpu-marked test needs a visible HIP device"
+    import pyoracle
+
+    pyoracle.prefer_simd()  # bit-identical to the -O2 build (tests/test_oracle_simd.py), faster
     torch.zeros(1, device="cuda")  # initialise torch's HIP state before any libllmi call
     import llmi
 

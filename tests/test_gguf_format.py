@@ -75,3 +75,33 @@ def test_block_statistics_q4k(tmp_path):
     n = t["ne"][0] * t["ne"][1]
     w = po.dequantize(Q4_K, np.frombuffer(t["data"], np.uint8), n)
     assert abs(float(w.mean())) < 5e-3 and 0.01 < float(w.std()) < 0.04
+
+
+def _patch_first_tensor_dims(src: str, dst: str, ne0: int, ne1: int) -> None:
+    """Rewrite ne[0], ne[1] of the token_embd tensor info (u64 name len + name + u32
+    n_dims + u64 ne[]) in a copy of a GGUF file."""
+    import struct
+
+    raw = bytearray(open(src, "rb").read())
+    name = b"token_embd.weight"
+    i = raw.find(struct.pack("<Q", len(name)) + name)
+    assert i > 0
+    p = i + 8 + len(name) + 4
+    raw[p:p + 16] = struct.pack("<qq", ne0, ne1)
+    open(dst, "wb").write(bytes(raw))
+
+
+@pytest.mark.parametrize("ne0,ne1,msg", [(256, -5, "negative dimension"),
+                                         (1 << 40, 1 << 40, "overflows"),
+                                         (256, 1 << 50, "past end of file")])
+def test_malformed_tensor_dims_rejected(tmp_path, ne0, ne1, msg):
+    """Negative dims, element counts past INT64_MAX and sizes past the end of the file
+    are rejected by the loader (as upstream gguf_init_from_file does) instead of
+    wrapping the byte count and reading outside the mmap (vocab_only: no GPU needed)."""
+    src = str(tmp_path / "ok.gguf")
+    llmi.write_synthetic_gguf(src, "tiny-mixed", seed=1)
+    bad = str(tmp_path / "bad.gguf")
+    _patch_first_tensor_dims(src, bad, ne0, ne1)
+    llmi.Model(src, vocab_only=True).close()
+    with pytest.raises(llmi.LlmiError, match=msg):
+        llmi.Model(bad, vocab_only=True)

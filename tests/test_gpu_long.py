@@ -1,0 +1,257 @@
+"""Long and full-width parity runs against the oracle (device order), through the C ABI
+and the HTTP front end — the BASELINE.json configs the shorter tests do not reach:
+
+- C1: TinyLlama-1.1B Q8_0 (exact widths, all 22 layers), 16-token greedy decode driven
+  through llmi.server over HTTP the way the reference gateway sends it, ids equal to the
+  oracle's;
+- C4: Mistral-7B widths (2 layers), a 2048-token prompt through the batched MFMA
+  prefill (four 512-token ubatches), then decode steps — logits bit-identical to the
+  oracle, once with the all-Q6_K table and once with the Q5_K_M table;
+- >= 4096 positions: a tiny model's prompt of 4100 tokens, then decode steps on every
+  attention path the dispatch can pick at that length (auto = split, fused, two-kernel);
+- the prefill-length limit: a prompt reaching past the batched-prefill attention's KV
+  limit continues as decode steps, bit-identical;
+- the fault path: a bounded in-kernel wait that gives up makes llama_decode return -6
+  instead of NaN logits;
+- the north star's "within 1e-3 of the CPU path" against ggml's GENERIC fp32 order at
+  the 8B / TinyLlama / 70B widths, reported (fraction of steps within 1e-3, worst |d|,
+  first greedy divergence and its top-2 margin) into $LLMI_REPORT_DIR/parity_generic.json.
+"""
+from __future__ import annotations
+
+import http.client
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import llmi
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_run(path, prompt, n_ctx, n_gen, order=po.DEVICE_ORDER):
+    """Oracle logits after the prompt (batched or_prefill for all but the last token)
+    and for n_gen greedy steps after it."""
+    po.set_dot_order(order)
+    try:
+        om = po.OracleModel(path, n_ctx=n_ctx)
+        if len(prompt) > 1:
+            om.prefill(prompt[:-1])
+        lo = om.decode(prompt[-1], len(prompt) - 1)
+        out = [lo]
+        pos = len(prompt)
+        for _ in range(n_gen):
+            lo = om.decode(int(np.argmax(lo)), pos)
+            out.append(lo)
+            pos += 1
+        om.close()
+        return out
+    finally:
+        po.set_dot_order(po.GENERIC)
+
+
+def _gpu_run(path, prompt, n_ctx, n_gen):
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=n_ctx)
+    assert c.decode(prompt) == 0
+    out = [c.logits(-1)]
+    pos = len(prompt)
+    for _ in range(n_gen):
+        t = c.greedy(-1)
+        assert t == int(np.argmax(out[-1]))
+        assert c.decode([t], pos=[pos]) == 0
+        out.append(c.logits(-1))
+        pos += 1
+    return m, out
+
+
+def _assert_same(got, want):
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(g, w), f"step {k}: max |d| {np.abs(g - w).max():.3g}"
+
+
+# ---- C1: TinyLlama through the HTTP front end ---------------------------------------
+def test_tinyllama_http_greedy16_vs_oracle(gpu, synth_dir):
+    """TinyLlama-shaped Q8_0 GGUF (E 2048, 22 layers, V 32000), prompt
+    BOS + 16 ids uniform in [3, V) (seed 2), greedy 16 tokens with temperature 0, top_k
+    1, repeat_penalty 1.0, ignore_eos, sent as the gateway forwards it (lowercase
+    headers, Bearer key, Connection: close); the ids equal the oracle's greedy ids."""
+    from llmi.server import Engine, make_server
+
+    path = str(synth_dir / "tinyllama-q8_0-full.gguf")
+    if not os.path.exists(path):
+        llmi.write_synthetic_gguf(path, "tinyllama-q8_0", seed=1)
+    rng = np.random.default_rng(2)
+    prompt = [1] + [int(t) for t in rng.integers(3, 32000, 16)]
+    want_logits = _oracle_run(path, prompt, 64, 15)
+    want = [int(np.argmax(lo)) for lo in want_logits]
+
+    eng = Engine(path, 64, 99, [0])
+    eng.load()
+    assert eng.ready, eng.error
+    srv = make_server(eng, "127.0.0.1", 0, "k-test")
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        body = json.dumps({"prompt": prompt, "max_tokens": 16, "temperature": 0, "top_k": 1, "repeat_penalty": 1.0,
+                           "ignore_eos": True})
+        conn = http.client.HTTPConnection("127.0.0.1", srv.server_address[1], timeout=120)
+        conn.request("POST", "/v1/completions", body=body,
+                     headers={"content-type": "application/json", "Authorization": "Bearer k-test",
+                              "Connection": "close"})
+        r = conn.getresponse()
+        d = json.loads(r.read())
+        conn.close()
+        assert r.status == 200
+        assert d["llmi"]["tokens"] == want
+        assert d["usage"] == {"prompt_tokens": 17, "completion_tokens": 16, "total_tokens": 33}
+    finally:
+        srv.shutdown()
+        srv.server_close()
+
+
+# ---- C4: 2048-token prompts at Mistral widths ----------------------------------------
+@pytest.mark.parametrize("preset", ["mistral7b-q6k", "mistral7b-q5km"])
+def test_mistral_2048_prefill_vs_oracle(gpu, synth_dir, preset):
+    """SURVEY.md §8d C4 (2 layers, full V 32000): a 2048-token prompt through the batched
+    prefill, then 3 decode steps; logits bit-identical to the oracle at every step."""
+    path = str(synth_dir / f"{preset}-L2-full.gguf")
+    if not os.path.exists(path):
+        llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=2)
+    rng = np.random.default_rng(11)
+    prompt = [1] + [int(t) for t in rng.integers(3, 32000, 2047)]
+    m, got = _gpu_run(path, prompt, 2304, 3)
+    assert m.prefill_supported
+    _assert_same(got, _oracle_run(path, prompt, 2304, 3))
+
+
+# ---- >= 4096 positions on every attention path ----------------------------------------
+_LONG = {}
+
+
+def _long_oracle(path, prompt):
+    key = (path, len(prompt))
+    if key not in _LONG:
+        _LONG[key] = _oracle_run(path, prompt, 4352, 4)
+    return _LONG[key]
+
+
+@pytest.mark.parametrize("preset,mode", [("tiny-mixed-d128", "0"), ("tiny-mixed-d128", "1"),
+                                         ("tiny-mixed-d128", "3"), ("tiny-mixed", "0")])
+def test_decode_past_4096_positions(gpu, tiny_models, monkeypatch, preset, mode):
+    """A 4100-token prompt (batched prefill) and 4 decode steps at positions 4100-4103
+    with the attention path forced (LLMI_ATTN_MODE, read at context creation): 0 auto
+    (split at this length), 1 fused one-workgroup-per-head, 3 two-kernel."""
+    path = tiny_models[preset]
+    rng = np.random.default_rng(41)
+    prompt = [1] + [int(t) for t in rng.integers(3, 700, 4099)]
+    monkeypatch.setenv("LLMI_ATTN_MODE", mode)
+    try:
+        _, got = _gpu_run(path, prompt, 4352, 4)
+    finally:
+        monkeypatch.setenv("LLMI_ATTN_MODE", "0")
+        llmi.Context(llmi.Model(path), n_ctx=32).close()  # reset the process-wide mode
+    _assert_same(got, _long_oracle(path, prompt))
+
+
+def test_prompt_past_prefill_kv_limit(gpu, tiny_models, monkeypatch):
+    """A prompt reaching past the batched-prefill attention's KV limit (lowered to 200
+    for the test) is prefilled up to the limit and continues as decode steps: logits
+    bit-identical to the oracle and to all-decode-step processing."""
+    path = tiny_models["tiny-mixed"]
+    rng = np.random.default_rng(12)
+    prompt = [1] + [int(t) for t in rng.integers(3, 700, 299)]
+    old = llmi.test_option("pf_max_kv", 200)
+    try:
+        _, got = _gpu_run(path, prompt, 512, 2)
+    finally:
+        llmi.test_option("pf_max_kv", old)
+    _assert_same(got, _oracle_run(path, prompt, 512, 2))
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    _, steps = _gpu_run(path, prompt, 512, 2)
+    _assert_same(got, steps)
+
+
+def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
+    """k_attn_x's hand-off waits are bounded; with the bound lowered to 0 polls a wait
+    gives up, and the decode call reports it (-6, llmi_last_error) instead of returning
+    0 with NaN logits.  With the bound restored the context decodes normally again."""
+    path = tiny_models["tiny-mixed-d128"]
+    monkeypatch.setenv("LLMI_ATTN_MODE", "4")
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=512)
+    rng = np.random.default_rng(13)
+    prompt = [1] + [int(t) for t in rng.integers(3, 700, 199)]
+    assert c.decode(prompt) == 0
+    old = llmi.test_option("xspin_limit", 0)
+    codes, msgs = [], []
+    try:
+        t = c.greedy(-1)
+        for k in range(40):
+            rc = c.decode([t], pos=[len(prompt) + k])
+            codes.append(rc)
+            if rc == -6:
+                msgs.append(llmi.last_error())
+            if rc == 0:
+                lg = c.logits(-1)
+                assert np.isfinite(lg).all(), "a call that returned 0 has non-finite logits"
+    finally:
+        llmi.test_option("xspin_limit", old)
+        monkeypatch.setenv("LLMI_ATTN_MODE", "0")
+    assert -6 in codes, f"no wait gave up in 40 steps: {codes}"
+    assert all("bounded wait" in e for e in msgs), msgs
+    c.kv_clear()
+    assert c.decode(prompt) == 0 and np.isfinite(c.logits(-1)).all()
+    c.close()
+    llmi.Context(m, n_ctx=32).close()
+
+
+# ---- north star tolerance against ggml's generic fp32 order (reported) ----------------
+@pytest.mark.parametrize("preset,n_vocab", [("llama3-8b-q4km", 0), ("tinyllama-q8_0", 0), ("llama3-70b-q4km", 32000)])
+def test_generic_order_tolerance_report(gpu, synth_dir, preset, n_vocab):
+    """GPU logits vs the oracle in ggml's GENERIC fp32 order (the restatement of the
+    reference's CPU numerics; the GPU is bit-identical to the DEVICE order): per step
+    max |d|; reported, with loose sanity bounds only (the drift is activation-requant
+    flips)."""
+    path = str(synth_dir / f"{preset}-L2-rep.gguf")
+    if not os.path.exists(path):
+        llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=2, n_vocab=n_vocab)
+    rng = np.random.default_rng(21)
+    prompt = [1] + [int(t) for t in rng.integers(3, 30000, 7)]
+    n_gen = 12
+    po.set_dot_order(po.GENERIC)
+    om = po.OracleModel(path, n_ctx=64)
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=64)
+    diffs, margins, first_div = [], [], None
+    cur_g = cur_o = prompt[0]
+    for step in range(len(prompt) + n_gen - 1):
+        lo = om.decode(cur_o, step)
+        assert c.decode([cur_g], pos=[step]) == 0
+        lg = c.logits(-1)
+        diffs.append(float(np.abs(lg - lo).max()))
+        srt = np.sort(lo)
+        margins.append(float(srt[-1] - srt[-2]))
+        if step + 1 < len(prompt):
+            cur_g = cur_o = prompt[step + 1]
+        else:
+            cur_g, cur_o = int(np.argmax(lg)), int(np.argmax(lo))
+            if cur_g != cur_o and first_div is None:
+                first_div = {"step": step, "gpu": cur_g, "oracle": cur_o, "top2_margin": margins[-1]}
+            cur_g = cur_o  # follow the oracle's sequence so every step compares the same context
+    om.close()
+    within = float(np.mean(np.array(diffs) <= 1e-3))
+    rep = {"preset": preset, "n_layer": 2, "steps": len(diffs), "frac_within_1e-3": within,
+           "worst_abs_diff": max(diffs), "median_abs_diff": float(np.median(diffs)),
+           "first_greedy_divergence": first_div, "min_top2_margin": min(margins)}
+    print(json.dumps(rep))
+    out_dir = os.environ.get("LLMI_REPORT_DIR")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, "parity_generic.jsonl"), "a") as f:
+            f.write(json.dumps(rep) + "\n")
+    assert max(diffs) < 1.0  # sanity: an O(1) error would be a bug, not association

@@ -89,6 +89,31 @@ def test_auth_required_on_v1(server):
     r, raw = req(port, "POST", "/v1/completions", {"prompt": [1, 5]},
                  headers={"Authorization": "Bearer wrong"})
     assert r.status == 401
+    # llama-server's non-/v1 completion route is not public either (only /health is)
+    r, raw = req(port, "POST", "/completion", {"prompt": [1, 5]}, auth=False)
+    assert r.status == 401
+    r, raw = req(port, "POST", "/completion", {"prompt": [1, 5], "max_tokens": 2})
+    assert r.status == 200
+    r, raw = req(port, "GET", "/v1/health", auth=False)
+    assert r.status == 200
+
+
+def test_decode_failure_is_json_500(server):
+    """A failing llama_decode inside generate() answers an OpenAI-shaped 500 (non-stream)
+    or an error event before the close (SSE), never a dropped connection."""
+    eng, port = server
+    eng.ready = True
+
+    def boom(*a, **k):
+        raise RuntimeError("llama_decode returned -4")
+
+    eng.generate = boom
+    r, raw = req(port, "POST", "/v1/completions", {"prompt": [1, 5], "max_tokens": 3})
+    d = json.loads(raw)
+    assert r.status == 500 and d["error"]["type"] == "server_error" and "-4" in d["error"]["message"]
+    r, raw = req(port, "POST", "/v1/completions", {"prompt": [1, 5], "max_tokens": 3, "stream": True})
+    events = [e for e in raw.decode().split("\n\n") if e]
+    assert r.status == 200 and json.loads(events[-1][6:])["error"]["code"] == 500
 
 
 def test_models(server):
