@@ -156,7 +156,9 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
  *   "pf_max_kv"       longest KV length the batched prefill takes (default 32768); a prompt
  *                     reaching past it continues as decode steps (bit-identical)
  *   "xspin_limit"     polls before k_attn_x's bounded wait gives up; a give-up makes the
- *                     decode call return -6 with llmi_last_error set (fault surfacing) */
+ *                     decode call return -6 with llmi_last_error set (fault surfacing)
+ *   "xtag_skew"       1: k_attn_x consumers wait for a tag no producer writes (with
+ *                     xspin_limit 0: every such wait gives up at once; fault-path test) */
 int32_t llmi_test_option(const char* name, int32_t value);
 /* Algorithmic bytes of one decode step at KV length n_kv (weights + one embedding row
  * + norms + KV read/write), the numerator of achieved GB/s. */

@@ -154,7 +154,7 @@ struct llama_context* llama_init_from_model(struct llama_model* model, struct ll
 
 void llama_free(struct llama_context* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->c.m->device);
+    (void)hipSetDevice(ctx->c.device);  // never reads the model: it may be freed already
     if (ctx->outs) (void)hipFree(ctx->outs);
     if (ctx->keys_pinned) (void)hipHostFree(ctx->keys_pinned);
     delete ctx;
@@ -217,6 +217,7 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
         if (pos >= c.n_ctx) { set_err("llama_decode: no KV slot (position >= n_ctx)"); return 1; }
     }
     if (hipSetDevice(c.m->device) != hipSuccess) { set_err("hipSetDevice"); return -2; }
+    (void)hipGetLastError();  // launch wrappers report hipGetLastError: drop an unrelated stale one
     if (n_out > 0 && !ensure_outs(ctx, n_out)) return -2;
     c.out_rows = rows;
     c.n_outputs = n_out;
@@ -343,6 +344,7 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
     if (first < 0 || first >= hp.n_vocab) { set_err("llmi_generate_greedy: token out of range"); return -1; }
     if (pos0 < 0 || pos0 + n_gen > c.n_ctx) { set_err("llmi_generate_greedy: exceeds n_ctx"); return 1; }
     (void)hipSetDevice(c.m->device);
+    (void)hipGetLastError();
     std::string err;
     double bytes = 0;
     if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
@@ -429,6 +431,7 @@ int32_t llmi_test_option(const char* name, int32_t value) {
     if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
     else if (!strcmp(name, "pf_max_kv")) opt = &g_pf_max_kv;
     else if (!strcmp(name, "xspin_limit")) opt = &g_xspin_limit;
+    else if (!strcmp(name, "xtag_skew")) opt = &g_xtag_skew;
     if (!opt) { set_err("llmi_test_option: unknown option"); return -1; }
     const int old = *opt;
     if (value >= 0) *opt = value;

@@ -44,7 +44,7 @@ Model::~Model() {
 Context::~Context() {
     int cur = 0;
     (void)hipGetDevice(&cur);
-    if (m) (void)hipSetDevice(m->device);
+    if (m) (void)hipSetDevice(device);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     void* bufs[] = {x, q, att, h, logits, scores, rope, kc, vc, st, hist, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad};
     for (void* b : bufs)
@@ -194,6 +194,7 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
     HIPC(hipMalloc(&M.arena, M.arena_bytes));
     M.owns_arena = true;
     if (no_upload) return true;
+    (void)hipGetLastError();  // launch_repack reports hipGetLastError: start from a clean slate
     // ---- upload: H2D + on-device repack of the unaligned block types ----
     struct Item { const GgufTensor* t; DevMat* m; };
     std::vector<Item> items;
@@ -253,6 +254,7 @@ bool model_clone_layout(const Model& src, int device, Model& dst, std::string& e
 bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string& err) {
     const HParams& hp = m->hp;
     c.m = m;
+    c.device = m->device;
     c.n_ctx = n_ctx > 0 ? n_ctx : std::min(hp.n_ctx_train > 0 ? hp.n_ctx_train : 4096, 4096);
     // padded like upstream llama.cpp's KV cache (multiple of 256): the attention kernels
     // read V rows in 16-B (8-position) pieces and K in 64-position tiles

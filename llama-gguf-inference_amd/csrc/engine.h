@@ -67,6 +67,7 @@ struct Prof {
 
 struct Context {
     Model* m = nullptr;
+    int device = 0;                         // m->device, kept so teardown never reads *m
     int n_ctx = 0;
     bool use_graphs = true;
     hipStream_t stream = nullptr;

@@ -19,7 +19,7 @@ constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_boun
 constexpr int kXAttnMaxKV = 1024;  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
-extern int g_pf_attn_simple, g_pf_max_kv, g_xspin_limit;
+extern int g_pf_attn_simple, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
 int pf_max_kv();  // llama_decode hands prompt runs reaching past this KV length to decode steps
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
 // + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
@@ -78,6 +78,7 @@ struct AttnArgs {
     unsigned long long* gran = nullptr;   // k_attn_x: [H][kXAttnMaxKV] {tag, score} granules
     unsigned* fault = nullptr;            // k_attn_x: set when a bounded wait timed out
     int spin_limit = 1 << 22;             // k_attn_x: polls before a wait gives up (set at launch)
+    int tag_skew = 0;                     // test option: consumers expect tag + skew
     unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [kernel][block][wave][4] stamps
 };
 

@@ -1535,6 +1535,7 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
     if (tid == 0) s_fault = 0;
     const int n_kv = pos + 1;
     const uint32_t tag = seq * 256u + (uint32_t)a.layer + 1u;
+    const uint32_t want = tag + (uint32_t)a.tag_skew;  // test option: 1 = a hand-off that never completes
     __syncthreads();
     LLMI_ATT_STAMP(0, 1)
     // 2. scores of the tile -> granules
@@ -1591,9 +1592,9 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
         for (int spins = 0;; ++spins) {
             bool ok = true;
 #pragma unroll
-            for (int k = 0; k < NS; ++k) ok &= (uint32_t)(x[k] >> 32) == tag;
+            for (int k = 0; k < NS; ++k) ok &= (uint32_t)(x[k] >> 32) == want;
             if (__all(ok)) break;
-            if (spins > a.spin_limit) {
+            if (spins >= a.spin_limit) {
                 s_fault = 1;
                 break;
             }
@@ -1601,7 +1602,7 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
                 const int t = wi * 64 + lane + k * WPH * 64;
-                if ((uint32_t)(x[k] >> 32) != tag && t < n_kv)
+                if ((uint32_t)(x[k] >> 32) != want && t < n_kv)
                     x[k] = __hip_atomic_load(gh + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
@@ -2228,6 +2229,7 @@ static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipSt
 int g_pf_attn_simple = 0;               // batched-prefill attention: one head per workgroup
 int g_pf_max_kv = kPfAttnMaxKV;         // longest KV the batched-prefill attention takes
 int g_xspin_limit = kXSpinLimit;        // k_attn_x bounded-wait polls before it faults
+int g_xtag_skew = 0;                    // k_attn_x consumers expect tag + skew (1: never matches)
 int pf_max_kv() { return g_pf_max_kv; }
 
 static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel, 4 exchange (experiments: LLMI_ATTN_MODE)
@@ -2260,6 +2262,7 @@ hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int h
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     AttnArgs a = a0;
     a.spin_limit = g_xspin_limit;
+    a.tag_skew = g_xtag_skew;
     const int g = n_head / n_head_kv;
     int path = attn_path(n_head, n_head_kv, kv_bound, head_dim);
     if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254))

@@ -177,9 +177,10 @@ def test_prompt_past_prefill_kv_limit(gpu, tiny_models, monkeypatch):
 
 
 def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
-    """k_attn_x's hand-off waits are bounded; with the bound lowered to 0 polls a wait
-    gives up, and the decode call reports it (-6, llmi_last_error) instead of returning
-    0 with NaN logits.  With the bound restored the context decodes normally again."""
+    """k_attn_x's hand-off waits are bounded; with the bound lowered to 0 polls and the
+    consumers waiting for a tag no producer writes (test options, captured into the step
+    graph of the next KV bucket), every wait gives up, and each decode call reports it (-6, llmi_last_error) instead of returning 0 with
+    NaN logits.  With the options restored the context decodes normally again."""
     path = tiny_models["tiny-mixed-d128"]
     monkeypatch.setenv("LLMI_ATTN_MODE", "4")
     m = llmi.Model(path)
@@ -188,11 +189,12 @@ def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
     prompt = [1] + [int(t) for t in rng.integers(3, 700, 199)]
     assert c.decode(prompt) == 0
     old = llmi.test_option("xspin_limit", 0)
+    llmi.test_option("xtag_skew", 1)
     codes, msgs = [], []
     try:
         t = c.greedy(-1)
-        for k in range(40):
-            rc = c.decode([t], pos=[len(prompt) + k])
+        for k in range(4):  # positions 256+: a KV bucket whose step graph is captured now
+            rc = c.decode([t], pos=[256 + k])
             codes.append(rc)
             if rc == -6:
                 msgs.append(llmi.last_error())
@@ -201,8 +203,9 @@ def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
                 assert np.isfinite(lg).all(), "a call that returned 0 has non-finite logits"
     finally:
         llmi.test_option("xspin_limit", old)
+        llmi.test_option("xtag_skew", 0)
         monkeypatch.setenv("LLMI_ATTN_MODE", "0")
-    assert -6 in codes, f"no wait gave up in 40 steps: {codes}"
+    assert codes == [-6] * 4, codes
     assert all("bounded wait" in e for e in msgs), msgs
     c.kv_clear()
     assert c.decode(prompt) == 0 and np.isfinite(c.logits(-1)).all()
