@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 
 #include "common.h"
 
@@ -116,6 +117,33 @@ struct PfAttn {
     int n_ctx = 0, pos0 = 0, gqa = 1, max_kv = 0;  // max_kv >= pos0 + T (LDS score space)
     float scale = 0.f;
 };
+// Persistent decode step (step.hip): one launch per token, the layer ops as phases
+// separated by in-launch grid barriers, the next phase's weights in flight across each
+// barrier.  The phases' matvec descriptors are a device-side table built at context
+// creation (the per-op launches' MVArgs, unchanged).
+struct StepArgs {
+    const MVArgs* mv = nullptr;     // device table of the matvec phases: [layer][QKV, O, gate/up, down], output
+    int n_layer = 0;
+    Seg out;                        // output
+    const float* onorm = nullptr;   // output_norm
+    int E = 0, F = 0, H = 0, HK = 0, D = 0, n_rot = 0, n_ctx = 0, V = 0;
+    float eps = 0.f, scale = 0.f;
+    float *x = nullptr, *q = nullptr, *att = nullptr, *h = nullptr, *logits = nullptr;
+    float *scores = nullptr, *tmax = nullptr;
+    uint16_t *kc = nullptr, *vc = nullptr;
+    const float* rope = nullptr;
+    StepState* st = nullptr;
+    int32_t* hist = nullptr;
+    unsigned* bar = nullptr;        // barrier shards [kStepBarWords] u32, zeroed before every launch
+    unsigned* fault = nullptr;      // context fault word (a bounded wait gave up)
+    int kv_bound = 0;
+    unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [workgroup][512][arrive, release]
+};
+constexpr int kStepBarWords = 9 * 16;
+// can the persistent step run this model / KV bound on this device (residency, LDS)?
+bool step_supported(const StepArgs& a, int device, std::string* why);
+hipError_t launch_step(const StepArgs& a, hipStream_t s);
+
 bool pf_gemm_ok(int type, int rows, int cols);
 hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* toks, float* X, int T, int32_t* hist,
                            int pos0, int n_ctx, hipStream_t s);
@@ -125,7 +153,7 @@ hipError_t launch_pf_gemm(const PfGemm& g, int epi, hipStream_t s);
 hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipStream_t s);
 
 // activation kind of a weight type: 0 = block_q8_K (K-quants), 1 = block_q8_0
-inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
+__host__ __device__ inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
 size_t mv_lds_bytes(int act, int cols);
 
 // All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).

@@ -1,0 +1,777 @@
+// mv_device.h — device helpers of the quantized matvec shared by the per-op kernels
+// (kernels.hip) and the persistent decode step (step.hip): cross-lane exchange, the
+// activation prologue (RMSNorm + q8_K / q8_0 quantization, bit-exact with ggml), the
+// chunk-planar weight loads, the per-chunk integer dot products with ggml's fp32 combine,
+// row-pair bookkeeping and the epilogues.  Everything here is __device__ inline.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "../../include/llmi_math.h"
+
+namespace llmi {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Weight loads are nontemporal (nt): every weight byte is read once per token by one
+// CU, so keeping it in L2/MALL only evicts the activations and KV.  Measured with the
+// statically counted prologue (tools/mvbench.py, graph-replayed): 2-10 % faster on
+// every shape (output 128256x4096 Q6_K: 78.8 -> 70.8 us); end to end 555 -> 581 tok/s.
+// (Before the prologue stopped waiting on vmcnt(0), nt measured slower.)
+#ifndef LLMI_NT
+#define LLMI_NT 1
+#endif
+constexpr bool kNontemporalWeights = LLMI_NT != 0;
+
+__device__ __forceinline__ float h2f(uint32_t h) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+}
+// f32 -> f16 with its own rounding.  The empty asm makes the f32 value opaque: without
+// it the compiler folds f2h(a * b) into v_fma_mixlo_f16, ONE rounding of the exact
+// product straight to f16, where ggml rounds to f32 first and then to f16 (a tie in
+// the f32 product then rounds differently: softmax probabilities left the oracle by one
+// f16 ulp, tools/pf_diag9.py).
+__device__ __forceinline__ uint16_t f2h(float f) {
+    __asm__("" : "+v"(f));
+    return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+__device__ __forceinline__ u32x4 ldw(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x4*)p);
+    else return *(const u32x4*)p;
+}
+__device__ __forceinline__ u32x2 ldw8(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const u32x2*)p);
+    else return *(const u32x2*)p;
+}
+__device__ __forceinline__ uint32_t ldw4(const uint8_t* p) {
+    if constexpr (kNontemporalWeights) return __builtin_nontemporal_load((const uint32_t*)p);
+    else return *(const uint32_t*)p;
+}
+__device__ __forceinline__ int dot4(uint32_t a, int b, int c) {
+    return __builtin_amdgcn_sdot4((int)a, b, c, false);
+}
+// ---- cross-lane exchange without LDS round trips (VALU latency): DPP within 16-lane
+// rows, v_permlane16/32_swap across rows / halves (gfx950).  xor_partner<o>(v) returns
+// v of lane L^o for o in {1,2,4,8,16,32}; for o = 4 / 8 the DPP row_half_mirror /
+// row_mirror partner (lane 7-i / 15-i) is used, which equals lane L^4 / L^8 whenever
+// the value is already uniform over aligned 4- / 8-lane groups, i.e. inside a
+// butterfly after the xor-1/xor-2 (and xor-4) steps.  Every butterfly below runs the
+// steps in the order 1, 2, 4, 8, 16, 32; the oracle's device order models exactly that.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int O>
+__device__ __forceinline__ uint32_t xor_partner_u32(uint32_t v) {
+    if constexpr (O == 1) return dpp_u32<0xB1>(v);        // quad_perm [1,0,3,2]
+    else if constexpr (O == 2) return dpp_u32<0x4E>(v);   // quad_perm [2,3,0,1]
+    else if constexpr (O == 4) return dpp_u32<0x141>(v);  // row_half_mirror
+    else if constexpr (O == 8) return dpp_u32<0x140>(v);  // row_mirror
+    else if constexpr (O == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return ((threadIdx.x >> 4) & 1) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return ((threadIdx.x >> 5) & 1) ? r[0] : r[1];
+    }
+}
+template <int O>
+__device__ __forceinline__ float xor_partner(float v) { return __uint_as_float(xor_partner_u32<O>(__float_as_uint(v))); }
+template <int O>
+__device__ __forceinline__ int xor_partner_i(int v) { return (int)xor_partner_u32<O>((uint32_t)v); }
+template <int O>
+__device__ __forceinline__ double xor_partner_d(double v) {
+    const unsigned long long u = __double_as_longlong(v);
+    const uint32_t lo = xor_partner_u32<O>((uint32_t)u), hi = xor_partner_u32<O>((uint32_t)(u >> 32));
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+// 64-lane sum, all lanes receive the result (butterfly 1,2,4,8,16,32)
+__device__ __forceinline__ float wave_sum(float v) {
+    v += xor_partner<1>(v);
+    v += xor_partner<2>(v);
+    v += xor_partner<4>(v);
+    v += xor_partner<8>(v);
+    v += xor_partner<16>(v);
+    v += xor_partner<32>(v);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += xor_partner_d<1>(v);
+    v += xor_partner_d<2>(v);
+    v += xor_partner_d<4>(v);
+    v += xor_partner_d<8>(v);
+    v += xor_partner_d<16>(v);
+    v += xor_partner_d<32>(v);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, xor_partner<1>(v));
+    v = fmaxf(v, xor_partner<2>(v));
+    v = fmaxf(v, xor_partner<4>(v));
+    v = fmaxf(v, xor_partner<8>(v));
+    v = fmaxf(v, xor_partner<16>(v));
+    v = fmaxf(v, xor_partner<32>(v));
+    return v;
+}
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ----------------------------------------------------------------------------------
+// LDS image of the quantized activation, in the weights' chunk-part order (common.h):
+//   K-quants (block_q8_K): LO[k][ch], HI[k][ch]: 16 int8 each = activation of the
+//     weights in the low / high nibbles of quant part k of chunk ch (chunk weights
+//     16k..16k+15 and 32+16k..32+16k+15); BS[4ch+i] = bsums in natural order;
+//     D[b] per 256-block.
+//   Q8_0 (block_q8_0): LO[k][ch] (k < 4) = elements 64ch+16k..+15; D[b] per 32-block
+//     (f16-rounded, as stored by quantize_row_q8_0).
+// Lane L reads LO[k][L + 64j]: 16 consecutive 16-B slots per ds_read_b128 lane group,
+// conflict-free.
+// ----------------------------------------------------------------------------------
+struct Lds {
+    uint8_t* lo;
+    uint8_t* hi;
+    int16_t* bs;
+    float* d;
+    double* red;
+};
+__host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+// byte offsets of the regions; act 0 = q8_K (K-quant weights), 1 = q8_0
+__host__ __device__ inline size_t lds_hi_off(int act, int cols) { return act ? (size_t)cols : (size_t)cols / 2; }
+__host__ __device__ inline size_t lds_bs_off(int act, int cols) { return (size_t)cols; }
+__host__ __device__ inline size_t lds_d_off(int act, int cols) { return a16((size_t)cols + (act ? 0 : (size_t)cols / 8)); }
+__host__ __device__ inline size_t lds_red_off(int act, int cols) {
+    return a16(lds_d_off(act, cols) + (size_t)(act ? cols / 32 : cols / 256) * 4);
+}
+// (mv_lds_bytes: defined in kernels.hip)
+
+__device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
+    Lds l;
+    l.lo = smem;
+    l.hi = smem + lds_hi_off(act, cols);
+    l.bs = (int16_t*)(smem + lds_bs_off(act, cols));
+    l.d = (float*)(smem + lds_d_off(act, cols));
+    l.red = (double*)(smem + lds_red_off(act, cols));
+    return l;
+}
+
+// workgroup double sum of a matvec workgroup (NW waves; pairwise tree over waves)
+template <int NW = kMVWaves>
+__device__ double block_sum_d(double v, double* red) {
+    v = wave_sum_d(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) r[w] = red[w];
+#pragma unroll
+    for (int o = 1; o < NW; o <<= 1)
+#pragma unroll
+        for (int w = 0; w + o < NW; w += 2 * o) r[w] = r[w] + r[w + o];
+    return r[0];
+}
+
+// ----------------------------------------------------------------------------------
+// Prologue: [RMSNorm] + activation quantization into LDS.
+// Thread t handles 16-element sub-blocks sb = t + 256k; the 16 lanes of one DPP row
+// hold the 16 sub-blocks of one 256-element Q8_K block, two adjacent lanes one Q8_0
+// block.  Bit-exact with ggml:
+//   rms_norm: sum += (double)(x*x); mean = (float)(sum/n); scale = 1/sqrtf(mean+eps);
+//             y = (x*scale)*w                          (ggml_compute_forward_rms_norm + mul)
+//   q8_K:     first max |y| (signed) -> iscale = -127/max; q = min(127, nearest_int(iscale*y));
+//             bsums per 16; d = 1/iscale; all-zero block -> d = 0, q = 0 (quantize_row_q8_K_ref)
+//   q8_0:     d = amax/127 (stored f16), q = roundf(y * (d ? 1/d : 0))   (quantize_row_q8_0_ref)
+// ----------------------------------------------------------------------------------
+// Quantize one 16-element sub-block (values already normed) into the LDS image.
+template <int ACT>
+__device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const float (&v)[16]) {
+    const int tid = threadIdx.x;
+    int q[16];
+    uint8_t* dst;
+    if constexpr (ACT == 0) {
+        // max |y| of the Q8_K block (order-free), then the SIGNED value ggml keeps: the
+        // first element (lowest index) whose |y| equals it ('if (ax > amax)' scan).  Key =
+        // (index within the block) * 2 + sign, minimised over the 16 lanes of the block.
+        float am = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+        am = fmaxf(am, xor_partner<1>(am));
+        am = fmaxf(am, xor_partner<2>(am));
+        am = fmaxf(am, xor_partner<4>(am));
+        am = fmaxf(am, xor_partner<8>(am));
+        int key = 0x7fffffff;
+#pragma unroll
+        for (int j = 15; j >= 0; --j)
+            key = fabsf(v[j]) == am ? (((sb & 15) * 16 + j) << 1) | (v[j] < 0.f ? 1 : 0) : key;
+        key = min(key, xor_partner_i<1>(key));
+        key = min(key, xor_partner_i<2>(key));
+        key = min(key, xor_partner_i<4>(key));
+        key = min(key, xor_partner_i<8>(key));
+        const float mv = (key & 1) ? -am : am;
+        float dval = 0.f;
+        int bsum = 0;
+        if (am == 0.f) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) q[j] = 0;
+        } else {
+            const float iscale = -127.f / mv;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int t = llmi_nearest_int(iscale * v[j]);
+                q[j] = t < 127 ? t : 127;
+                bsum += q[j];
+            }
+            dval = 1.0f / iscale;
+        }
+        // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: lo part k=qq (qq<2), hi part k=qq-2
+        const int nch = cols >> 6, ch = sb >> 2, qq = sb & 3;
+        const int hoff = qq < 2 ? 0 : (int)(L.hi - L.lo);  // (no pointer select: it spills to scratch)
+        dst = L.lo + hoff + 16 * ((qq & 1) * nch + ch);
+        L.bs[sb] = (int16_t)bsum;
+        if ((tid & 15) == 0) L.d[sb >> 4] = dval;
+    } else {
+        float am = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+        am = fmaxf(am, xor_partner<1>(am));
+        const float d = am / 127;
+        const float id = d != 0.f ? 1.0f / d : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
+        if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
+        const int nch = cols >> 6;
+        dst = L.lo + 16 * ((sb & 3) * nch + (sb >> 2));
+    }
+    u32x4 pk;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
+                ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
+    *(u32x4*)dst = pk;
+}
+
+// Prologue in two halves so a caller can put the weight prefetch between them:
+// issue() loads this thread's first NP sub-blocks of x (and norm w) into registers —
+// UNCONDITIONALLY (indices clamped), so the load count is static and the first use
+// waits with vmcnt(#weight loads issued after them) instead of vmcnt(0), i.e. the
+// prologue never waits for the weight prefetch; finish() computes the norm,
+// quantizes and writes LDS.  NP = ceil(cols / (16 * kMVThreads)) rounded up to 1/2/4
+// (chosen at launch); sub-blocks beyond NP are loaded inside finish().
+template <bool NORM, int NP>
+struct ProRegs {
+    float x[NP][16];
+    float w[NORM ? NP : 1][16];
+};
+template <bool NORM, int NP, int NT = kMVThreads>
+__device__ __forceinline__ void mv_prologue_issue(const MVArgs& A, ProRegs<NORM, NP>& R) {
+    const int nsub = A.cols / 16;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int sb = min((int)threadIdx.x + i * NT, nsub - 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
+            R.x[i][4 * k + 0] = xv.x; R.x[i][4 * k + 1] = xv.y; R.x[i][4 * k + 2] = xv.z; R.x[i][4 * k + 3] = xv.w;
+            if constexpr (NORM) {
+                const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                R.w[i][4 * k + 0] = wv.x; R.w[i][4 * k + 1] = wv.y; R.w[i][4 * k + 2] = wv.z; R.w[i][4 * k + 3] = wv.w;
+            }
+        }
+    }
+}
+template <bool NORM, int NP>
+__device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM, NP>& R, int i, int sb, float (&v)[16],
+                                         float (&w)[16]) {
+    if (i < NP) {
+#pragma unroll
+        for (int ii = 0; ii < NP; ++ii)
+            if (ii == i) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    v[j] = R.x[ii][j];
+                    if constexpr (NORM) w[j] = R.w[ii][j];
+                }
+            }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 xv = *(const float4*)(A.x + sb * 16 + 4 * k);
+            v[4 * k + 0] = xv.x; v[4 * k + 1] = xv.y; v[4 * k + 2] = xv.z; v[4 * k + 3] = xv.w;
+            if constexpr (NORM) {
+                const float4 wv = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                w[4 * k + 0] = wv.x; w[4 * k + 1] = wv.y; w[4 * k + 2] = wv.z; w[4 * k + 3] = wv.w;
+            }
+        }
+    }
+}
+template <int ACT, bool NORM, int NP, int NT = kMVThreads>
+__device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
+    const int tid = threadIdx.x, cols = A.cols;
+    const int nsub = cols / 16;
+    float scale = 1.0f;
+    if constexpr (NORM) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NP; ++i)  // register-held sub-blocks (static indices)
+            if (tid + i * NT < nsub) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) s += (double)(R.x[i][j] * R.x[i][j]);
+            }
+        for (int sb = tid + NP * NT; sb < nsub; sb += NT) {  // rest (cols > NP*16*threads)
+            float v[16], w[16];
+            load_sub<NORM, NP>(A, R, NP, sb, v, w);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) s += (double)(v[j] * v[j]);
+        }
+        s = block_sum_d<NT / 64>(s, L.red);
+        const float mean = (float)(s / (double)cols);
+        scale = 1.0f / sqrtf(mean + A.eps);
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int sb = tid + i * NT;
+        if (sb < nsub) {
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                v[j] = R.x[i][j];
+                if constexpr (NORM) v[j] = (v[j] * scale) * R.w[i][j];
+            }
+            quant_sub<ACT>(L, cols, sb, v);
+        }
+    }
+    for (int sb = tid + NP * NT; sb < nsub; sb += NT) {
+        float v[16], w[16];
+        load_sub<NORM, NP>(A, R, NP, sb, v, w);
+        if constexpr (NORM) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = (v[j] * scale) * w[j];
+        }
+        quant_sub<ACT>(L, cols, sb, v);
+    }
+}
+template <int ACT, bool NORM>
+__device__ __forceinline__ void mv_prologue(const MVArgs& A, const Lds& L) {
+    ProRegs<NORM, 1> R;
+    mv_prologue_issue<NORM, 1>(A, R);
+    mv_prologue_finish<ACT, NORM, 1>(A, L, R);
+}
+
+// ----------------------------------------------------------------------------------
+// Per-type 64-weight chunk: load (global) and integer dot against the LDS activation
+// ----------------------------------------------------------------------------------
+constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u, M1 = 0x01010101u;
+
+// upstream get_scale_min_k4 on the 12 scale bytes held as three words (branchless:
+// j varies per lane, so both forms are computed and selected)
+__device__ __forceinline__ void scale_min(int j, uint32_t s0, uint32_t s1, uint32_t s2, int& sc, int& m) {
+    const int k = (j & 3) * 8;
+    const uint32_t b0 = (s0 >> k) & 0xffu, b1 = (s1 >> k) & 0xffu, b2 = (s2 >> k) & 0xffu;
+    const uint32_t sc_hi = (b2 & 0xFu) | ((b0 >> 6) << 4), m_hi = (b2 >> 4) | ((b1 >> 6) << 4);
+    sc = (int)(j < 4 ? (b0 & 63u) : sc_hi);
+    m = (int)(j < 4 ? (b1 & 63u) : m_hi);
+}
+// 4 bits -> the low bit of 4 bytes
+__device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x00204081u) & M1; }
+
+template <int T>
+__host__ __device__ constexpr int kparts() { return T == T_Q8_0 ? 4 : 2; }
+
+// One chunk of one row in registers.
+struct Raw {
+    u32x4 q0, q1, q2, q3;  // quant parts (q2, q3: Q8_0 only)
+    u32x4 hdr;             // Q4_K/Q5_K block header; Q6_K: 2-bit highs (4 dwords)
+    u32x2 qh;              // Q5_K fifth bits (lo 32, hi 32)
+    uint32_t e0;           // Q6_K chunk scales (4 x int8); Q8_0: the two fp16 d
+    uint32_t e1;           // Q6_K fp16 d
+};
+
+// Row view: uniform per-row base pointers (SGPRs) so per-lane addressing is a small
+// 32-bit offset: quant part k of chunk ch at qa + (k*nch + ch)*16.
+struct RowPtr {
+    const uint8_t* qa;  // A plane, this row
+    const uint8_t* hb;  // H plane, this row
+    const uint8_t* sb;  // S plane, this row
+    const uint8_t* db;  // D plane, this row
+};
+template <int T>
+__device__ __forceinline__ RowPtr row_ptr(const Seg& s, int row, int cols) {
+    RowPtr r;
+    const size_t nch = (size_t)(cols >> 6), nblk = (T == T_Q8_0) ? (size_t)(cols >> 5) : (size_t)(cols >> 8);
+    r.qa = s.a + (size_t)row * nch * (T == T_Q8_0 ? 64 : 32);
+    r.hb = s.h + (size_t)row * nch * (T == T_Q6_K ? 16 : 8);
+    r.sb = s.s + (size_t)row * nblk * 16;
+    r.db = s.d + (size_t)row * nblk * 2;
+    return r;
+}
+
+template <int T>
+__device__ __forceinline__ Raw load_chunk(const RowPtr& rp, int ch, int nch) {
+    Raw r;
+    const uint32_t o = (uint32_t)ch * 16, step = (uint32_t)nch * 16;
+    r.q0 = ldw(rp.qa + o);
+    r.q1 = ldw(rp.qa + o + step);
+    if constexpr (T == T_Q4_K || T == T_Q5_K) {
+        // the block header is shared by the 4 lanes of a block: default policy (nt loads
+        // of duplicated addresses were fetched once per lane: +24 % FETCH_SIZE)
+        r.hdr = *(const u32x4*)(rp.sb + (uint32_t)(ch >> 2) * 16);
+        if constexpr (T == T_Q5_K) r.qh = ldw8(rp.hb + (uint32_t)ch * 8);
+    } else if constexpr (T == T_Q6_K) {
+        r.hdr = ldw(rp.hb + (uint32_t)ch * 16);
+        r.e0 = ldw4(rp.sb + (uint32_t)ch * 4);
+        r.e1 = *(const uint16_t*)(rp.db + (uint32_t)(ch >> 2) * 2);
+    } else {
+        r.q2 = ldw(rp.qa + o + 2 * step);
+        r.q3 = ldw(rp.qa + o + 3 * step);
+        r.e0 = ldw4(rp.db + (uint32_t)ch * 4);
+    }
+    return r;
+}
+
+struct Act {
+    i32x4 a0, a1, a2, a3;  // K: lo part 0, lo part 1, hi part 0, hi part 1; Q8_0: parts 0..3
+    int bs[4];
+    float d0, d1;
+};
+template <int ACT>
+__device__ __forceinline__ Act load_act(const Lds& L, int ch, int nch) {
+    Act a;
+    const int step = nch * 16;
+    a.a0 = *(const i32x4*)(L.lo + 16 * ch);
+    a.a1 = *(const i32x4*)(L.lo + 16 * ch + step);
+    if constexpr (ACT == 0) {
+        a.a2 = *(const i32x4*)(L.hi + 16 * ch);
+        a.a3 = *(const i32x4*)(L.hi + 16 * ch + step);
+        const uint2 bw = *(const uint2*)(L.bs + 4 * ch);
+        a.bs[0] = (int16_t)(bw.x & 0xffff); a.bs[1] = (int16_t)(bw.x >> 16);
+        a.bs[2] = (int16_t)(bw.y & 0xffff); a.bs[3] = (int16_t)(bw.y >> 16);
+        a.d0 = L.d[ch >> 2];
+    } else {
+        a.a2 = *(const i32x4*)(L.lo + 16 * ch + 2 * step);
+        a.a3 = *(const i32x4*)(L.lo + 16 * ch + 3 * step);
+        const float2 dd = *(const float2*)(L.d + 2 * ch);
+        a.d0 = dd.x;
+        a.d1 = dd.y;
+    }
+    return a;
+}
+
+// ggml_vec_dot_<T>_q8_K restricted to one 64-weight chunk; exact int32 sums, fp32
+// combine exactly as ggml's per-block formula (d_w*d_a*isum - dmin_w*d_a*imin).
+template <int T>
+__device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, int ch) {
+    if constexpr (T == T_Q4_K || T == T_Q5_K) {
+        const int c = ch & 3;
+        int sc0, m0, sc1, m1;
+        scale_min(2 * c, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
+        scale_min(2 * c + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
+        int lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const u32x4 q = k ? r.q1 : r.q0;
+            const i32x4 al = k ? a.a1 : a.a0, ah = k ? a.a3 : a.a2;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                uint32_t l4 = q[m] & M4, h4 = (q[m] >> 4) & M4;
+                if constexpr (T == T_Q5_K) {
+                    l4 |= spread4((r.qh.x >> (16 * k + 4 * m)) & 0xFu) << 4;
+                    h4 |= spread4((r.qh.y >> (16 * k + 4 * m)) & 0xFu) << 4;
+                }
+                lo = dot4(l4, al[m], lo);
+                hi = dot4(h4, ah[m], hi);
+            }
+        }
+        const int isum = sc0 * lo + sc1 * hi;
+        const int imin = m0 * (a.bs[0] + a.bs[1]) + m1 * (a.bs[2] + a.bs[3]);
+        const float d = h2f(r.hdr.x), dmin = h2f(r.hdr.x >> 16);
+        return (d * a.d0) * (float)isum - (dmin * a.d0) * (float)imin;
+    } else if constexpr (T == T_Q6_K) {
+        int dm[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const u32x4 q = k ? r.q1 : r.q0;
+            const i32x4 al = k ? a.a1 : a.a0, ah = k ? a.a3 : a.a2;
+            const uint32_t hl = r.hdr[k], hh = r.hdr[2 + k];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t ulo = (q[m] & M4) | (((hl >> (2 * m)) & M2) << 4);
+                const uint32_t uhi = ((q[m] >> 4) & M4) | (((hh >> (2 * m)) & M2) << 4);
+                dm[k] = dot4(ulo, al[m], dm[k]);
+                dm[2 + k] = dot4(uhi, ah[m], dm[2 + k]);
+            }
+        }
+        int isum = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) isum += (int)(int8_t)(r.e0 >> (8 * m)) * (dm[m] - 32 * a.bs[m]);
+        return (h2f(r.e1) * a.d0) * (float)isum;
+    } else {
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            s0 = dot4(r.q0[m], a.a0[m], s0);
+            s0 = dot4(r.q1[m], a.a1[m], s0);
+            s1 = dot4(r.q2[m], a.a2[m], s1);
+            s1 = dot4(r.q3[m], a.a3[m], s1);
+        }
+        return (float)s0 * (h2f(r.e0) * a.d0) + (float)s1 * (h2f(r.e0 >> 16) * a.d1);
+    }
+}
+
+// (the descriptor type is a template parameter: the persistent step reads its phase
+// descriptors through the constant address space, step.hip)
+template <class MA>
+__device__ __forceinline__ Seg pick(const MA& A, int si) {
+    Seg s;
+    s.a = si == 0 ? A.seg[0].a : si == 1 ? A.seg[1].a : A.seg[2].a;
+    s.h = si == 0 ? A.seg[0].h : si == 1 ? A.seg[1].h : A.seg[2].h;
+    s.s = si == 0 ? A.seg[0].s : si == 1 ? A.seg[1].s : A.seg[2].s;
+    s.d = si == 0 ? A.seg[0].d : si == 1 ? A.seg[1].d : A.seg[2].d;
+    s.type = si == 0 ? A.seg[0].type : si == 1 ? A.seg[1].type : A.seg[2].type;
+    s.rows = si == 0 ? A.seg[0].rows : si == 1 ? A.seg[1].rows : A.seg[2].rows;
+    s.row0 = si == 0 ? A.seg[0].row0 : si == 1 ? A.seg[1].row0 : A.seg[2].row0;
+    return s;
+}
+
+// ----------------------------------------------------------------------------------
+// Row-pair work items.  A wave streams its pairs p = w0, w0+G, ... (G = 4*gridDim.x);
+// item j of a pair is piece P = lane + 64*j of both rows (NJ = ceil(pieces/64)).
+// ----------------------------------------------------------------------------------
+struct PairRef {
+    Seg sa, sb;
+    int ra, rb;
+    int vb;      // (an int, not a bool: no padding bytes for SROA to keep in scratch)
+    int type;  // common type of both rows, or -1 if they differ
+};
+
+template <int EPI, class MA>
+__device__ __forceinline__ PairRef pair_ref(const MA& A, int p) {
+    PairRef r;
+    if constexpr (EPI == EPI_SWIGLU) {
+        r.sa = pick(A, 0);
+        r.sb = pick(A, 1);
+        r.ra = r.rb = p;
+        r.vb = true;
+    } else {
+        const int g = A.seg[0].row0 + 2 * p;
+        int si = 0;
+        if (A.nseg > 1 && g >= A.seg[1].row0) si = 1;
+        if (A.nseg > 2 && g >= A.seg[2].row0) si = 2;
+        r.sa = pick(A, si);
+        r.sb = r.sa;
+        r.ra = g - r.sa.row0;
+        r.rb = r.ra + 1;
+        r.vb = r.rb < r.sa.rows;
+    }
+    r.type = r.sa.type == r.sb.type ? r.sa.type : -1;
+    return r;
+}
+
+template <int T>
+struct PairRaw {
+    Raw a, b;
+};
+template <int T>
+struct PairRows {
+    RowPtr a, b;
+};
+
+template <int T>
+__device__ __forceinline__ PairRows<T> pair_rows(const PairRef& r, int cols) {
+    PairRows<T> pr;
+    pr.a = row_ptr<T>(r.sa, r.ra, cols);
+    pr.b = row_ptr<T>(r.sb, r.vb ? r.rb : r.ra, cols);
+    return pr;
+}
+
+// Unconditional loads (the chunk index is clamped to a valid one; callers discard the
+// contribution of out-of-range lanes): straight-line code lets the compiler count
+// vmcnt exactly, so the next item's loads stay in flight while this one is reduced.
+template <int T>
+__device__ __forceinline__ PairRaw<T> load_item(const PairRows<T>& pr, int ch, int nch) {
+    PairRaw<T> w;
+    const int c = ch < nch ? ch : nch - 1;
+    w.a = load_chunk<T>(pr.a, c, nch);
+    w.b = load_chunk<T>(pr.b, c, nch);
+    return w;
+}
+
+// Row sums of a pair: one 64-lane butterfly per row (steps 1,2,4,8,16,32; DPP and
+// permlane swaps, no LDS), the oracle's device order models this tree exactly.
+struct PairSum {
+    float a, b;
+};
+__device__ __forceinline__ PairSum reduce_pair(float acc_a, float acc_b) {
+    return {wave_sum(acc_a), wave_sum(acc_b)};
+}
+
+// ordered key of (logit, row): larger logit wins, ties -> smaller row (first max wins,
+// as upstream llama_sampler_greedy's strict '>' scan)
+__device__ __forceinline__ unsigned long long argmax_key(float v, int row) {
+    if (v == 0.f) v = 0.f;  // -0 == +0
+    uint32_t u = __float_as_uint(v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
+}
+
+// Global accesses of data handed between the phases of ONE launch (the persistent step,
+// step.hip): write-through `sc1` stores and `sc1` loads (relaxed agent-scope atomics),
+// the hand-off form MI355X_MICROARCH.md §visibility validates without acquire fences.
+// WT = false: plain accesses (separate launches hand over at kernel boundaries).
+typedef unsigned int __attribute__((address_space(1))) gu32_t;
+typedef unsigned short __attribute__((address_space(1))) gu16_t;
+typedef unsigned long long __attribute__((address_space(1))) gu64_t;
+template <bool WT>
+__device__ __forceinline__ void st_f32(float* p, float v) {
+    if constexpr (WT) __hip_atomic_store((gu32_t*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <bool WT>
+__device__ __forceinline__ float ld_f32(const float* p) {
+    if constexpr (WT) return __uint_as_float(__hip_atomic_load((const gu32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    else return *p;
+}
+template <bool WT>
+__device__ __forceinline__ void st_u32(void* p, uint32_t v) {
+    if constexpr (WT) __hip_atomic_store((gu32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *(uint32_t*)p = v;
+}
+template <bool WT>
+__device__ __forceinline__ void st_u16(uint16_t* p, uint16_t v) {
+    if constexpr (WT) __hip_atomic_store((gu16_t*)p, (unsigned short)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+// Epilogue of one finished pair (every lane holds both row sums; lane 0 writes).
+template <int EPI, bool WT = false, class MA>
+__device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, PairSum v, int pos,
+                                         unsigned long long& best) {
+    const int lane = threadIdx.x & 63;
+    const float va = v.a, vb = v.b;
+    if (lane != 0) return;
+    if constexpr (EPI == EPI_STORE) {
+        st_f32<WT>(A.y + r.sa.row0 + r.ra, va);
+        if (r.vb) st_f32<WT>(A.y + r.sa.row0 + r.rb, vb);
+    } else if constexpr (EPI == EPI_ADD) {
+        float* ya = A.y + r.sa.row0 + r.ra;
+        st_f32<WT>(ya, ld_f32<WT>(ya) + va);
+        if (r.vb) {
+            float* yb = A.y + r.sa.row0 + r.rb;
+            st_f32<WT>(yb, ld_f32<WT>(yb) + vb);
+        }
+    } else if constexpr (EPI == EPI_LOGITS) {
+        A.y[r.ra] = va;
+        unsigned long long k = argmax_key(va, r.ra);
+        best = k > best ? k : best;
+        if (r.vb) {
+            A.y[r.rb] = vb;
+            k = argmax_key(vb, r.rb);
+            best = k > best ? k : best;
+        }
+    } else if constexpr (EPI == EPI_SWIGLU) {
+        st_f32<WT>(A.y + p, llmi_silu(va) * vb);
+    } else if constexpr (EPI == EPI_QKV) {
+        // sa.row0 tells q (0), k (nq) or v (nq+nk); rows (ra, ra+1) are a RoPE pair
+        const int hd = A.head_dim;
+        const int h = r.ra / hd, d = r.ra - h * hd;
+        if (r.sa.row0 < A.nq + A.nk) {
+            float o0 = va, o1 = vb;
+            if (d < A.n_rot) {  // ggml rope NORM mode on the adjacent pair (d, d+1)
+                const float2 cs = *(const float2*)(A.rope + ((size_t)pos * (A.n_rot / 2) + d / 2) * 2);
+                o0 = va * cs.x - vb * cs.y;
+                o1 = va * cs.y + vb * cs.x;
+            }
+            if (r.sa.row0 == 0) {
+                st_f32<WT>(A.y + r.ra, o0);
+                st_f32<WT>(A.y + r.ra + 1, o1);
+            } else {
+                const uint32_t w = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
+                st_u32<WT>(A.kc + ((size_t)h * A.n_ctx + pos) * hd + d, w);
+            }
+        } else {
+            st_u16<WT>(A.vc + ((size_t)h * hd + d) * A.n_ctx + pos, f2h(va));
+            st_u16<WT>(A.vc + ((size_t)h * hd + d + 1) * A.n_ctx + pos, f2h(vb));
+        }
+    }
+}
+
+// Non-pipelined fallback for pairs whose type is not the kernel's primary type (the
+// Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs).
+template <int ACT, int T>
+__device__ __forceinline__ float generic_row(const Seg& s, int row, int cols, const Lds& L) {
+    const int nch = cols >> 6;
+    const RowPtr rp = row_ptr<T>(s, row, cols);
+    float acc = 0.f;
+    for (int ch = threadIdx.x & 63; ch < nch; ch += 64) {
+        const Raw w = load_chunk<T>(rp, ch, nch);
+        acc += dot_chunk<T>(w, load_act<ACT>(L, ch, nch), ch);
+    }
+    return acc;
+}
+template <int ACT>
+__device__ __forceinline__ float generic_row_any(int type, const Seg& s, int row, int cols, const Lds& L) {
+    if constexpr (ACT == 1) {
+        return generic_row<1, T_Q8_0>(s, row, cols, L);
+    } else {
+        switch (type) {
+            case T_Q4_K: return generic_row<0, T_Q4_K>(s, row, cols, L);
+            case T_Q5_K: return generic_row<0, T_Q5_K>(s, row, cols, L);
+            case T_Q6_K: return generic_row<0, T_Q6_K>(s, row, cols, L);
+            default: return 0.f;
+        }
+    }
+}
+
+// get_rows: element e of row `row` dequantized from the device layout (bit-exact with
+// upstream dequantize_row_*)
+__device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int cols) {
+    switch (w.type) {
+        case T_F32: return ((const float*)w.a)[(size_t)row * cols + e];
+        case T_F16: return h2f(((const uint16_t*)w.a)[(size_t)row * cols + e]);
+        case T_Q4_K:
+        case T_Q5_K:
+        case T_Q6_K: {
+            const int nch = cols >> 6, nbr = cols >> 8;
+            const int ch = e >> 6, t = e & 63, hi = t >= 32, l = t & 31, k = l >> 4, i = l & 15;
+            const size_t gb = (size_t)row * nbr + (e >> 8);
+            const uint8_t qb = w.a[(size_t)row * nch * 32 + (size_t)(k * nch + ch) * 16 + i];
+            int q = hi ? (qb >> 4) : (qb & 0xF);
+            if (w.type == T_Q6_K) {  // H dword (2*hi + k), byte i&3, bits 2*(i>>2)
+                const uint8_t hb = w.h[((size_t)row * nch + ch) * 16 + (2 * hi + k) * 4 + (i & 3)];
+                q |= ((hb >> (2 * (i >> 2))) & 3) << 4;
+                const float d = h2f(*(const uint16_t*)(w.d + gb * 2));
+                const int sc = (int8_t)w.s[gb * 16 + ((e & 255) >> 4)];
+                return d * (float)sc * (float)(q - 32);
+            }
+            const uint32_t* s32 = (const uint32_t*)(w.s + gb * 16);
+            int sc, m;
+            scale_min(2 * (ch & 3) + hi, s32[1], s32[2], s32[3], sc, m);
+            if (w.type == T_Q5_K) q += ((ldw4(w.h + ((size_t)row * nch + ch) * 8 + 4 * hi) >> l) & 1) << 4;
+            const float d = h2f(s32[0]), dmin = h2f(s32[0] >> 16);
+            const float d1 = d * (float)sc, m1 = dmin * (float)m;
+            return d1 * (float)q - m1;
+        }
+        case T_Q8_0: {
+            const int nch = cols >> 6, ch = e >> 6, t = e & 63;
+            const uint8_t qb = w.a[(size_t)row * nch * 64 + (size_t)((t >> 4) * nch + ch) * 16 + (t & 15)];
+            return (float)(int8_t)qb * h2f(*(const uint16_t*)(w.d + ((size_t)row * (cols / 32) + e / 32) * 2));
+        }
+        default: return 0.f;
+    }
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#define LLMI_MAX64_STEP(O)                                                                        \
+    {                                                                                             \
+        const uint32_t lo = xor_partner_u32<O>((uint32_t)v), hi = xor_partner_u32<O>((uint32_t)(v >> 32)); \
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;                         \
+        v = o > v ? o : v;                                                                        \
+    }
+    LLMI_MAX64_STEP(1) LLMI_MAX64_STEP(2) LLMI_MAX64_STEP(4) LLMI_MAX64_STEP(8) LLMI_MAX64_STEP(16) LLMI_MAX64_STEP(32)
+#undef LLMI_MAX64_STEP
+    return v;
+}
+
+}  // namespace llmi

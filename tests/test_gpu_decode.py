@@ -217,3 +217,32 @@ def test_golden_greedy16_on_gpu(gpu):
             cur = c.greedy(-1)
             ids.append(cur)
     assert ids == [int(i) for i in z["ids_device"]]
+
+
+@pytest.mark.parametrize("preset,n_layer,n_vocab", [("llama3-8b-q4km", 2, 0), ("tinyllama-q8_0", 2, 0),
+                                                    ("mistral7b-q5km", 2, 0), ("mistral7b-q6k", 2, 0),
+                                                    ("llama3-70b-q4km", 2, 32000)])
+def test_persistent_step_matches_launches(gpu, synth_dir, monkeypatch, preset, n_layer, n_vocab):
+    """The persistent one-launch step (step.hip) and the per-op launches give bit-identical
+    logits at every step, and LLMI_STEP selects the path (1: persistent, 0 / unset: launches).  (The tiny
+    presets mix gate/up weight types, which the step leaves to the per-op launches.)"""
+    path = str(synth_dir / f"{preset}-L{n_layer}-step.gguf")
+    llmi.write_synthetic_gguf(path, preset, seed=7, n_layer=n_layer, n_vocab=n_vocab)
+    prompt = [1, 100, 2000, 31000, 9, 17]
+    res = []
+    for step in ("1", "0"):
+        monkeypatch.setenv("LLMI_STEP", step)
+        m = llmi.Model(path)
+        c = llmi.Context(m, n_ctx=128)
+        assert c.step_path(5) == (1 if step == "1" else 0), llmi.last_error()
+        out = []
+        for pos, t in enumerate(prompt):
+            assert c.decode([t], pos=[pos]) == 0
+            out.append(c.logits(-1))
+        g = c.greedy(-1)
+        seq = c.generate_greedy(g, len(prompt), 12)
+        res.append((out, seq))
+        c.close()
+    for k, (a, b) in enumerate(zip(res[0][0], res[1][0])):
+        assert np.array_equal(a, b), f"step {k}: max |d| {np.abs(a - b).max():.3g}"
+    assert res[0][1] == res[1][1]
