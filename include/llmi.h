@@ -56,7 +56,8 @@ struct llama_context_params {
     uint32_t n_ctx;        /* 0 = model's context_length capped at 4096 */
     uint32_t n_batch;      /* max tokens per llama_decode call (logical batch) */
     uint32_t n_ubatch;
-    uint32_t n_seq_max;    /* llmi: 1 sequence per context (one replica = one stream) */
+    uint32_t n_seq_max;    /* sequences (KV caches) per context; >= 2 enables batched
+                              decode steps (continuous batching, up to 8 per step) */
     int32_t n_threads;     /* ignored (GPU) */
     bool use_graphs;       /* llmi: replay the decode step as a HIP graph (default true) */
 };
@@ -124,6 +125,12 @@ int32_t llama_model_desc(const struct llama_model* model, char* buf, size_t buf_
 uint32_t llama_n_ctx(const struct llama_context* ctx);
 /* upstream llama_memory_clear / llama_kv_self_clear: reset the KV cache of ctx */
 void llama_kv_self_clear(struct llama_context* ctx);
+/* upstream llama_kv_self_seq_rm / llama_memory_seq_rm (the server's slot release and
+ * prompt-cache truncation): remove positions [p0, p1) of seq_id (-1: every sequence).
+ * Only tail removal (p1 < 0) is supported; p0 <= 0 clears the sequence. */
+bool llama_kv_self_seq_rm(struct llama_context* ctx, llama_seq_id seq_id, llama_pos p0, llama_pos p1);
+/* upstream llama_memory_seq_pos_max: last position held by seq_id, -1 if empty */
+int32_t llmi_seq_pos_max(const struct llama_context* ctx, llama_seq_id seq_id);
 
 /* ---------- llmi extras ---------- */
 const char* llmi_last_error(void);
@@ -135,6 +142,13 @@ llama_token llmi_greedy_ith(struct llama_context* ctx, int32_t i);
  * the device (token feedback through the on-device argmax; no host round trip per
  * token).  out[k] = token sampled after step k.  Returns n_gen or < 0 on error. */
 int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_gen, llama_token* out);
+/* Continuous-batching form: n (1..8) distinct sequences seqs[k] of a context created with
+ * n_seq_max >= 2 advance together, one batched step per token (every weight byte read
+ * once per step for all of them).  Sequence k starts from first[k] at pos0[k];
+ * out[k * n_gen + j] = its token after step j, bit-identical to llmi_generate_greedy of
+ * that sequence alone.  Returns n_gen or < 0 on error. */
+int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const int32_t* seqs, const llama_token* first,
+                                   const int32_t* pos0, int32_t n_gen, llama_token* out);
 /* Roofline accounting of the last llama_decode / llmi_generate_greedy call:
  * algorithmic HBM bytes it streamed and its device time in microseconds. */
 void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec);

@@ -1,0 +1,361 @@
+// batch.hip — batched decode (continuous batching): up to
+// kMaxBatch sequences advance one token per step, every weight byte streamed once for all
+// of them.
+//
+// k_mvn is the matvec (kernels.hip k_matvec) with NT activation vectors: the prologue
+// quantizes the NT inputs into NT LDS images exactly as the single-token prologue does
+// (per-16 sub-block q8_K / q8_0, RMSNorm with a double sum); the main loop loads a row
+// pair's chunk once and forms NT integer dot products against it (the nibble / 6-bit
+// unpacking is shared), each token accumulated per lane in the matvec's order and
+// reduced by the same 64-lane butterfly — so every sequence's results are bit-identical
+// to its own single-token decode.  At NT = 8 the kernel does ~4x the VALU work of the
+// single-token matvec, still under the HBM time of the weight stream.
+//
+// Attention runs the split kernels' bodies (mv_device.h) with a third grid dimension
+// over the batch slots, each slot reading its own sequence's KV cache.
+#include "kernels.h"
+#include "mv_device.h"
+
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace llmi {
+
+namespace {
+
+constexpr int kBT = 512, kBW = kBT / 64;  // threads / waves per workgroup
+
+__host__ __device__ inline size_t img_bytes(int act, int cols) { return a16(lds_red_off(act, cols)); }
+
+// per-token LDS image t at smem + t * img; the shared reduction scratch after the NT images
+__device__ __forceinline__ Lds carve_t(uint8_t* smem, int act, int cols, int t, size_t img) {
+    Lds L = carve(smem + (size_t)t * img, act, cols);
+    return L;
+}
+
+// NT activation vectors (x + t * x_stride) -> NT LDS images: [RMSNorm] + quantization,
+// bit-exact per token with the single-token prologue (the double sum of squares is exact
+// in any association in practice, as for the K-split kernel's 1024-thread prologue).
+// Work item i = tid + kBT k is (token i / nsub, sub-block i % nsub): the 16 lanes of a
+// DPP row hold the 16 sub-blocks of one 256-element block of one token, as quant_sub needs.
+template <int ACT, bool NORM, int NT>
+__device__ __forceinline__ void bprologue(const MVArgs& A, uint8_t* smem, size_t img, double* red) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int cols = A.cols, nsub = cols >> 4, nitem = NT * nsub;
+    float scale[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) scale[t] = 1.0f;
+    if constexpr (NORM) {
+        double part[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) part[t] = 0.0;
+        for (int i = tid; i < nitem; i += kBT) {
+            const int t = i / nsub, sb = i - t * nsub;
+            const float* xs = A.x + (size_t)t * A.x_stride + sb * 16;
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = *(const float4*)(xs + 4 * k);
+                s += (double)(v.x * v.x); s += (double)(v.y * v.y); s += (double)(v.z * v.z); s += (double)(v.w * v.w);
+            }
+#pragma unroll
+            for (int u = 0; u < NT; ++u)
+                if (u == t) part[u] += s;
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const double w = wave_sum_d(part[t]);
+            if (lane == 0) red[t * kBW + wave] = w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            double r[kBW];
+#pragma unroll
+            for (int w = 0; w < kBW; ++w) r[w] = red[t * kBW + w];
+#pragma unroll
+            for (int o = 1; o < kBW; o <<= 1)
+#pragma unroll
+                for (int w = 0; w + o < kBW; w += 2 * o) r[w] = r[w] + r[w + o];
+            const float mean = (float)(r[0] / (double)cols);
+            scale[t] = 1.0f / sqrtf(mean + A.eps);
+        }
+    }
+    for (int i = tid; i < nitem; i += kBT) {
+        const int t = i / nsub, sb = i - t * nsub;
+        const float* xs = A.x + (size_t)t * A.x_stride + sb * 16;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 xv = *(const float4*)(xs + 4 * k);
+            v[4 * k] = xv.x; v[4 * k + 1] = xv.y; v[4 * k + 2] = xv.z; v[4 * k + 3] = xv.w;
+        }
+        if constexpr (NORM) {
+            float sc = 1.0f;
+#pragma unroll
+            for (int u = 0; u < NT; ++u)
+                if (u == t) sc = scale[u];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 w = *(const float4*)(A.nw + sb * 16 + 4 * k);
+                v[4 * k + 0] = (v[4 * k + 0] * sc) * w.x;
+                v[4 * k + 1] = (v[4 * k + 1] * sc) * w.y;
+                v[4 * k + 2] = (v[4 * k + 2] * sc) * w.z;
+                v[4 * k + 3] = (v[4 * k + 3] * sc) * w.w;
+            }
+        }
+        quant_sub<ACT>(carve_t(smem, ACT, cols, t, img), cols, sb, v);
+    }
+    __syncthreads();
+}
+
+// the per-token view of the launch's descriptor for the epilogue
+__device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t) {
+    MVArgs B = A;
+    B.y = A.y + (size_t)t * A.y_stride;
+    const int seq = A.tseq ? A.tseq[t] : 0;
+    B.kc = A.kc ? A.kc + (size_t)seq * A.kv_stride : nullptr;
+    B.vc = A.vc ? A.vc + (size_t)seq * A.kv_stride : nullptr;
+    return B;
+}
+
+}  // namespace
+
+template <int ACT, bool NORM, int EPI, int T, int NT>
+__global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const size_t img = img_bytes(ACT, A.cols);
+    double* red = (double*)(smem + NT * img);
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform((int)(threadIdx.x >> 6));
+    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+    const int G = gridDim.x * kBW;
+    int pos[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) pos[t] = A.tpos ? A.tpos[t] : 0;
+    unsigned long long best[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) best[t] = 0;
+    bprologue<ACT, NORM, NT>(A, smem, img, red);
+
+    int p = blockIdx.x * kBW + wave;
+    if (p < A.npairs) {
+        PairRef r = pair_ref<EPI>(A, p);
+        PairRows<T> rows = pair_rows<T>(r, A.cols);
+        PairRaw<T> cur = load_item<T>(rows, lane, nch);
+        int j = 0;
+        float acc_a[NT], acc_b[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc_a[t] = acc_b[t] = 0.f;
+        for (;;) {
+            int pn = p, jn = j + 1;
+            PairRef rn = r;
+            PairRows<T> rowsn = rows;
+            if (jn == NJ) {
+                jn = 0;
+                pn = p + G;
+                if (pn < A.npairs) {
+                    rn = pair_ref<EPI>(A, pn);
+                    rowsn = pair_rows<T>(rn, A.cols);
+                }
+            }
+            const bool has_next = pn < A.npairs;
+            PairRaw<T> nxt{};
+            if (has_next) nxt = load_item<T>(rowsn, lane + 64 * jn, nch);
+            const int ch = lane + 64 * j;
+            const int chc = ch < nch ? ch : nch - 1;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const Act act = load_act<ACT>(carve_t(smem, ACT, A.cols, t, img), chc, nch);
+                const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
+                acc_a[t] += ch < nch ? va : 0.f;
+                acc_b[t] += ch < nch ? vb : 0.f;
+            }
+            if (j == NJ - 1) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const MVArgs B = token_view(A, t);
+                    epilogue<EPI>(B, r, p, reduce_pair(acc_a[t], acc_b[t]), pos[t], best[t]);
+                    acc_a[t] = acc_b[t] = 0.f;
+                }
+            }
+            if (!has_next) break;
+            cur = nxt;
+            p = pn;
+            j = jn;
+            r = rn;
+            rows = rowsn;
+        }
+    }
+    if constexpr (EPI == EPI_LOGITS) {
+        // per token: workgroup max of the waves' keys, one atomic into the slot of its
+        // sequence's StepState; workgroup 0 advances the sequence's next position
+        unsigned long long* wred = (unsigned long long*)red;
+        for (int t = 0; t < NT; ++t) {
+            __syncthreads();
+            unsigned long long bt = 0;
+#pragma unroll
+            for (int u = 0; u < NT; ++u)
+                if (u == t) bt = best[u];
+            if (lane == 0) wred[wave] = bt;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long b = wred[0];
+                for (int w = 1; w < kBW; ++w) b = wred[w] > b ? wred[w] : b;
+                StepState* st = A.st + (A.tseq ? A.tseq[t] : 0);
+                const int pt = A.tpos[t];
+                if (b) atomicMax(&st->key[pt & 1][blockIdx.x % kArgSlots], b);
+                if (blockIdx.x == 0) st->pos_next = pt + 1;
+            }
+        }
+    }
+}
+
+// batched step entry: per slot (blockIdx.y) the token (host-provided for this position,
+// else the argmax of the sequence's previous step), the sequence state, the embedding row
+__global__ __launch_bounds__(256) void k_bembed(BEmbArgs a) {
+    const int s = blockIdx.y;
+    const int seq = a.tseq[s];
+    StepState* st = a.st + seq;
+    const int pos = st->pos_next;
+    __shared__ int s_tok;
+    if (threadIdx.x < 64) {
+        const unsigned long long k = wave_max_u64(st->key[(pos + 1) & 1][threadIdx.x]);
+        if (threadIdx.x == 0) {
+            int tok = st->token_in_pos == pos ? st->token_in : (int)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+            if (tok < 0 || tok >= a.vocab) tok = 0;
+            s_tok = tok;
+        }
+    }
+    __syncthreads();
+    const int tok = s_tok;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < kArgSlots) st->key[pos & 1][threadIdx.x] = 0;
+        if (threadIdx.x == 0) {
+            st->pos = pos;
+            st->token = tok;
+            st->seq = st->seq + 1u;
+            if (pos >= 0 && pos < a.n_ctx) a.hist[(size_t)seq * a.n_ctx + pos] = tok;
+            a.tpos[s] = pos;
+        }
+    }
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e < a.cols) a.x[(size_t)s * a.cols + e] = dequant_elem(a.w, tok, e, a.cols);
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_battn_scores8(BAttnArgs b) {
+    const AttnArgs a = b.a[blockIdx.z];
+    attn_scores8_body<D, G>(a);
+}
+template <int D, int G>
+__global__ __launch_bounds__(512) void k_battn_pv16(BAttnArgs b, int kvb) {
+    const AttnArgs a = b.a[blockIdx.z];
+    attn_pv16_body<D, G>(a, kvb);
+}
+
+// ---- launchers -----------------------------------------------------------------------------
+size_t mvn_lds_bytes(int act, int cols, int nt) { return (size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8; }
+
+template <typename K>
+static int mvn_grid(K kernel, int npairs, size_t lds, int max_blocks) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, size_t, int>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple((const void*)kernel, lds, dev);
+    int cap = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) {
+            cap = it->second;
+        } else {
+            if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            int occ = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kBT, lds) != hipSuccess || occ <= 0) occ = 1;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
+            cap = std::min(occ, 2) * cus;  // as the single-token matvec: at most 2 workgroups per CU
+            cache.emplace(key, cap);
+        }
+    }
+    int blocks = (npairs + kBW - 1) / kBW;
+    blocks = std::min(blocks, std::min(cap, max_blocks));
+    return std::max(blocks, 1);
+}
+
+template <int ACT, bool NORM, int EPI, int T, int NT>
+static hipError_t mvn_launch(const MVArgs& a, int max_blocks, hipStream_t s) {
+    auto k = k_mvn<ACT, NORM, EPI, T, NT>;
+    const size_t lds = mvn_lds_bytes(ACT, a.cols, NT);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int blocks = mvn_grid(k, a.npairs, lds, max_blocks);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBT), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int ACT, bool NORM, int EPI, int T>
+static hipError_t mvn_nt(const MVArgs& a, int nt, int mb, hipStream_t s) {
+    switch (nt) {
+        case 1: return mvn_launch<ACT, NORM, EPI, T, 1>(a, mb, s);
+        case 2: return mvn_launch<ACT, NORM, EPI, T, 2>(a, mb, s);
+        case 3: case 4: return mvn_launch<ACT, NORM, EPI, T, 4>(a, mb, s);
+        default: return mvn_launch<ACT, NORM, EPI, T, 8>(a, mb, s);
+    }
+}
+
+template <int ACT, int T>
+static hipError_t mvn_epi(const MVArgs& a, int epi, int nt, int mb, hipStream_t s) {
+    const bool norm = a.nw != nullptr;
+    switch (epi) {
+        case EPI_ADD: return norm ? hipErrorInvalidValue : mvn_nt<ACT, false, EPI_ADD, T>(a, nt, mb, s);
+        case EPI_STORE: return norm ? mvn_nt<ACT, true, EPI_STORE, T>(a, nt, mb, s) : mvn_nt<ACT, false, EPI_STORE, T>(a, nt, mb, s);
+        case EPI_QKV: return mvn_nt<ACT, true, EPI_QKV, T>(a, nt, mb, s);
+        case EPI_SWIGLU: return mvn_nt<ACT, true, EPI_SWIGLU, T>(a, nt, mb, s);
+        case EPI_LOGITS: return mvn_nt<ACT, true, EPI_LOGITS, T>(a, nt, mb, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
+    if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0 || nt < 1 || nt > kMaxBatch) return hipErrorInvalidValue;
+    const int t = a.seg[0].type;
+    for (int i = 1; i < a.nseg; ++i)
+        if (a.seg[i].type != t) return hipErrorInvalidValue;  // callers group segments by type
+    // the padded token count (3 -> 4, 5..7 -> 8) reads rows of the batch buffers past nt:
+    // the caller keeps kMaxBatch rows allocated and finite
+    switch (t) {
+        case T_Q4_K: return mvn_epi<0, T_Q4_K>(a, epi, nt, max_blocks, s);
+        case T_Q5_K: return mvn_epi<0, T_Q5_K>(a, epi, nt, max_blocks, s);
+        case T_Q6_K: return mvn_epi<0, T_Q6_K>(a, epi, nt, max_blocks, s);
+        case T_Q8_0: return mvn_epi<1, T_Q8_0>(a, epi, nt, max_blocks, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s) {
+    if (a.nt < 1 || a.nt > kMaxBatch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bembed, dim3((a.cols + 255) / 256, a.nt), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
+                             hipStream_t s) {
+    if (nt < 1 || nt > kMaxBatch || n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    const int g = n_head / n_head_kv;
+    const size_t lds = (size_t)g * kv_bound * 4;
+    if (lds > kSplitAttnMaxLds) return hipErrorInvalidValue;
+#define LLMI_BATT(D_, G_)                                                                                    \
+    if (head_dim == D_ && g == G_) {                                                                         \
+        hipLaunchKernelGGL((k_battn_scores8<D_, G_>), dim3(n_head_kv, (kv_bound + 31) / 32, nt), dim3(256), 0, s, b); \
+        hipLaunchKernelGGL((k_battn_pv16<D_, G_>), dim3(n_head_kv, D_ / 16, nt), dim3(512), lds, s, b, kv_bound); \
+        return hipGetLastError();                                                                            \
+    }
+    LLMI_BATT(128, 1) LLMI_BATT(128, 2) LLMI_BATT(128, 4) LLMI_BATT(128, 8)
+    LLMI_BATT(64, 1) LLMI_BATT(64, 2) LLMI_BATT(64, 4) LLMI_BATT(64, 8)
+#undef LLMI_BATT
+    return hipErrorInvalidValue;
+}
+
+}  // namespace llmi

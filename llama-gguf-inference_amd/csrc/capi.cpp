@@ -143,7 +143,7 @@ struct llama_context* llama_init_from_model(struct llama_model* model, struct ll
     auto* ctx = new llama_context();
     ctx->owner = model;
     std::string err;
-    if (!context_init(&model->m, (int)params.n_ctx, params.use_graphs, ctx->c, err)) {
+    if (!context_init(&model->m, (int)params.n_ctx, params.use_graphs, (int)std::max<uint32_t>(1u, params.n_seq_max), ctx->c, err)) {
         set_err(err);
         delete ctx;
         return nullptr;
@@ -197,6 +197,58 @@ void llama_batch_free(struct llama_batch b) {
 // shortest prompt run taken by the batched prefill path (shorter runs: decode steps)
 static constexpr int kPrefillMin = 2;
 
+static int seq_past_of(const Context& c, int s) { return s == c.cur_seq ? c.n_past : c.seq_past[(size_t)s]; }
+static void set_seq_past(Context& c, int s, int v) {
+    if (s == c.cur_seq) c.n_past = v;
+    else c.seq_past[(size_t)s] = v;
+}
+
+static void copy_out(llama_context* ctx, int r, const float* logits_dev, const StepState* st, int pos) {
+    Context& c = ctx->c;
+    const size_t V = (size_t)c.m->hp.n_vocab;
+    (void)hipMemcpyAsync(ctx->outs + (size_t)r * V * 4, logits_dev, V * 4, hipMemcpyDeviceToDevice, c.stream);
+    (void)hipMemcpyAsync(ctx->keys_pinned + (size_t)r * kArgSlots, &st->key[pos & 1][0], 8 * kArgSlots, hipMemcpyDeviceToHost,
+                         c.stream);
+}
+
+// One sequence's tokens (batch indices idx, positions pos) through the single-sequence
+// path: the batched prefill of the leading run of consecutive, logit-less tokens (leaving
+// at least the last token to a decode step), then decode steps.
+// LLMI_NO_PREFILL=1 runs every token as a decode step.
+static bool run_seq(llama_context* ctx, const llama_batch& batch, int seq, const std::vector<int>& idx,
+                    const std::vector<int>& pos, const std::vector<int>& rows, double& bytes, std::string& err) {
+    Context& c = ctx->c;
+    context_select_seq(c, seq);
+    const int n = (int)idx.size();
+    int i0 = 0;
+    const char* no_pf_env = getenv("LLMI_NO_PREFILL");
+    const bool no_pf = no_pf_env && atoi(no_pf_env) != 0;
+    const int p0 = pos[0];
+    int run = 0;
+    while (run < n - 1 && rows[(size_t)idx[(size_t)run]] < 0 && pos[(size_t)run] == p0 + run) ++run;
+    // the batched-prefill attention holds one head's scores in LDS: a run reaching past
+    // pf_max_kv() positions goes through decode steps from there on
+    if (p0 + run > pf_max_kv()) run = std::max(0, pf_max_kv() - p0);
+    if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
+        std::vector<int32_t> toks((size_t)run);
+        for (int i = 0; i < run; ++i) toks[(size_t)i] = batch.token[idx[(size_t)i]];
+        if (!prefill_enqueue(c, toks.data(), run, p0, err)) return false;
+        for (int i = 0; i < run; ++i) bytes += bytes_per_token(*c.m, p0 + i + 1);
+        i0 = run;
+    }
+    for (int i = i0; i < n; ++i) {
+        const int p = pos[(size_t)i];
+        if (launch_state_set(c.st, batch.token[idx[(size_t)i]], p, c.stream) != hipSuccess || !step_run(c, p, err)) {
+            if (err.empty()) err = "launch failed";
+            return false;
+        }
+        bytes += bytes_per_token(*c.m, p + 1);
+        const int r = rows[(size_t)idx[(size_t)i]];
+        if (r >= 0) copy_out(ctx, r, c.logits, c.st, p);
+    }
+    return true;
+}
+
 int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
     API_TRY
     if (!ctx) { set_err("null context"); return -1; }
@@ -209,12 +261,22 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
     int n_out = 0;
     for (int i = 0; i < n; ++i)
         if (batch.logits ? batch.logits[i] != 0 : i == n - 1) rows[(size_t)i] = n_out++;
+    // tokens by sequence (llama_batch.seq_id[i][0]; no seq_id: sequence 0), in batch order
+    std::vector<std::vector<int>> by_seq((size_t)c.n_seq), pos_of((size_t)c.n_seq);
     for (int i = 0; i < n; ++i) {
         const int tok = batch.token[i];
         if (tok < 0 || tok >= hp.n_vocab) { set_err("llama_decode: token id out of range"); return -1; }
-        const int pos = batch.pos ? batch.pos[i] : c.n_past + i;
+        int s = 0;
+        if (batch.seq_id && batch.n_seq_id) {
+            if (batch.n_seq_id[i] > 1) { set_err("llama_decode: a token shared by several sequences is not supported"); return -1; }
+            if (batch.n_seq_id[i] == 1) s = batch.seq_id[i][0];
+        }
+        if (s < 0 || s >= c.n_seq) { set_err("llama_decode: seq_id out of range (n_seq_max)"); return -1; }
+        const int pos = batch.pos ? batch.pos[i] : seq_past_of(c, s) + (int)by_seq[(size_t)s].size();
         if (pos < 0) { set_err("llama_decode: negative position"); return -1; }
         if (pos >= c.n_ctx) { set_err("llama_decode: no KV slot (position >= n_ctx)"); return 1; }
+        by_seq[(size_t)s].push_back(i);
+        pos_of[(size_t)s].push_back(pos);
     }
     if (hipSetDevice(c.m->device) != hipSuccess) { set_err("hipSetDevice"); return -2; }
     (void)hipGetLastError();  // launch wrappers report hipGetLastError: drop an unrelated stale one
@@ -226,45 +288,44 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
     std::string err;
     double bytes = 0;
     hipEventRecord(c.ev0, c.stream);
-    int last_pos = c.n_past - 1;
-    // Batched prefill of the longest leading run of tokens that need no logits and sit at
-    // consecutive positions (the prompt), leaving at least the last token to the decode
-    // step.  LLMI_NO_PREFILL=1 runs every token as a decode step.
-    int i0 = 0;
-    {
-        const char* no_pf_env = getenv("LLMI_NO_PREFILL");
-        const bool no_pf = no_pf_env && atoi(no_pf_env) != 0;
-        const int p0 = batch.pos ? batch.pos[0] : c.n_past;
-        int run = 0;
-        while (run < n - 1 && rows[(size_t)run] < 0 && (batch.pos ? batch.pos[run] : c.n_past + run) == p0 + run) ++run;
-        // the batched-prefill attention holds one head's scores in LDS: a run reaching past
-        // pf_max_kv() positions goes through decode steps from there on
-        if (p0 + run > pf_max_kv()) run = std::max(0, pf_max_kv() - p0);
-        if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
-            if (!prefill_enqueue(c, batch.token, run, p0, err)) {
-                set_err("llama_decode: " + err);
+    // sequences with one token each advance together through batched steps (batch.hip,
+    // up to kMaxBatch per step); the others run one sequence at a time
+    std::vector<int> singles;
+    for (int s = 0; s < c.n_seq; ++s)
+        if (by_seq[(size_t)s].size() == 1) singles.push_back(s);
+    if (singles.size() < 2) singles.clear();
+    for (size_t g = 0; g < singles.size(); g += kMaxBatch) {
+        const int nt = (int)std::min<size_t>(kMaxBatch, singles.size() - g);
+        const int* seqs = singles.data() + g;
+        int max_pos = 0;
+        for (int k = 0; k < nt; ++k) {
+            const int s = seqs[k], p = pos_of[(size_t)s][0];
+            max_pos = std::max(max_pos, p);
+            if (launch_state_set(c.st0 + s, batch.token[by_seq[(size_t)s][0]], p, c.stream) != hipSuccess) {
+                set_err("llama_decode: state set failed");
                 return -3;
             }
-            for (int i = 0; i < run; ++i) bytes += bytes_per_token(*c.m, p0 + i + 1);
-            last_pos = std::max(last_pos, p0 + run - 1);
-            i0 = run;
+        }
+        if (!bstep_run(c, nt, seqs, max_pos, err)) {
+            // not batchable here (context beyond the batched attention's LDS bound, mixed
+            // gate/up types): these sequences take the single-sequence path below
+            err.clear();
+            singles.resize(g);
+            break;
+        }
+        for (int k = 0; k < nt; ++k) {
+            const int s = seqs[k], p = pos_of[(size_t)s][0];
+            bytes += bytes_per_token(*c.m, p + 1) / nt;  // weights once for the group, KV per sequence
+            const int r = rows[(size_t)by_seq[(size_t)s][0]];
+            if (r >= 0) copy_out(ctx, r, c.blogits + (size_t)k * hp.n_vocab, c.st0 + s, p);
         }
     }
-    for (int i = i0; i < n; ++i) {
-        const int pos = batch.pos ? batch.pos[i] : c.n_past + i;
-        if (launch_state_set(c.st, batch.token[i], pos, c.stream) != hipSuccess || !step_run(c, pos, err)) {
-            set_err("llama_decode: " + (err.empty() ? std::string("launch failed") : err));
+    for (int s = 0; s < c.n_seq; ++s) {
+        if (by_seq[(size_t)s].empty() || std::find(singles.begin(), singles.end(), s) != singles.end()) continue;
+        if (!run_seq(ctx, batch, s, by_seq[(size_t)s], pos_of[(size_t)s], rows, bytes, err)) {
+            set_err("llama_decode: " + err);
             return -3;
         }
-        bytes += bytes_per_token(*c.m, pos + 1);
-        const int r = rows[(size_t)i];
-        if (r >= 0) {
-            (void)hipMemcpyAsync(ctx->outs + (size_t)r * hp.n_vocab * 4, c.logits, (size_t)hp.n_vocab * 4,
-                                 hipMemcpyDeviceToDevice, c.stream);
-            (void)hipMemcpyAsync(ctx->keys_pinned + (size_t)r * kArgSlots, &c.st->key[pos & 1][0], 8 * kArgSlots,
-                                 hipMemcpyDeviceToHost, c.stream);
-        }
-        last_pos = std::max(last_pos, pos);
     }
     hipEventRecord(c.ev1, c.stream);
     context_fault_readback(c);
@@ -275,7 +336,12 @@ int32_t llama_decode(struct llama_context* ctx, struct llama_batch batch) {
     hipEventElapsedTime(&ms, c.ev0, c.ev1);
     c.last_us = ms * 1e3;
     c.last_bytes = bytes;
-    c.n_past = last_pos + 1;
+    for (int s = 0; s < c.n_seq; ++s) {
+        if (by_seq[(size_t)s].empty()) continue;
+        int last = seq_past_of(c, s) - 1;
+        for (int p : pos_of[(size_t)s]) last = std::max(last, p);
+        set_seq_past(c, s, last + 1);
+    }
     return 0;
     API_CATCH(-5)
 }
@@ -373,6 +439,93 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
     c.n_outputs = 0;
     return n_gen;
     API_CATCH(-5)
+}
+
+int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const int32_t* seqs, const llama_token* first,
+                                   const int32_t* pos0, int32_t n_gen, llama_token* out) {
+    API_TRY
+    if (!ctx || n <= 0 || n > kMaxBatch || !seqs || !first || !pos0 || !out || n_gen <= 0) {
+        set_err("llmi_generate_greedy_batch: bad arguments (1..8 sequences)");
+        return -1;
+    }
+    Context& c = ctx->c;
+    const HParams& hp = c.m->hp;
+    int max_end = 0;
+    for (int k = 0; k < n; ++k) {
+        if (seqs[k] < 0 || seqs[k] >= c.n_seq) { set_err("llmi_generate_greedy_batch: seq out of range (n_seq_max)"); return -1; }
+        for (int j = 0; j < k; ++j)
+            if (seqs[j] == seqs[k]) { set_err("llmi_generate_greedy_batch: repeated sequence"); return -1; }
+        if (first[k] < 0 || first[k] >= hp.n_vocab) { set_err("llmi_generate_greedy_batch: token out of range"); return -1; }
+        if (pos0[k] < 0 || pos0[k] + n_gen > c.n_ctx) { set_err("llmi_generate_greedy_batch: exceeds n_ctx"); return 1; }
+        max_end = std::max(max_end, pos0[k] + n_gen);
+    }
+    (void)hipSetDevice(c.m->device);
+    (void)hipGetLastError();
+    std::string err;
+    double bytes = 0;
+    for (int k = 0; k < n; ++k)
+        if (launch_state_set(c.st0 + seqs[k], first[k], pos0[k], c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
+    hipEventRecord(c.ev0, c.stream);
+    for (int j = 0; j < n_gen; ++j) {
+        int max_pos = 0;
+        for (int k = 0; k < n; ++k) {
+            max_pos = std::max(max_pos, pos0[k] + j);
+            bytes += bytes_per_token(*c.m, pos0[k] + j + 1) / n;
+        }
+        if (!bstep_run(c, n, seqs, max_pos, err)) { set_err("llmi_generate_greedy_batch: " + err); return -3; }
+    }
+    hipEventRecord(c.ev1, c.stream);
+    std::vector<int32_t> h((size_t)n * n_gen);
+    std::vector<unsigned long long> keys((size_t)n * kArgSlots);
+    for (int k = 0; k < n; ++k) {
+        const int32_t* hist = c.hist0 + (size_t)seqs[k] * c.n_ctx;
+        if (n_gen > 1)
+            (void)hipMemcpyAsync(h.data() + (size_t)k * n_gen, hist + pos0[k] + 1, (size_t)(n_gen - 1) * 4, hipMemcpyDeviceToHost,
+                                 c.stream);
+        (void)hipMemcpyAsync(keys.data() + (size_t)k * kArgSlots, &c.st0[seqs[k]].key[(pos0[k] + n_gen - 1) & 1][0],
+                             8 * kArgSlots, hipMemcpyDeviceToHost, c.stream);
+    }
+    context_fault_readback(c);
+    hipError_t e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) { set_err("llmi_generate_greedy_batch: " + hip_err(e)); return -4; }
+    if (!context_fault_ok(c, err)) { set_err("llmi_generate_greedy_batch: " + err); return -6; }
+    for (int k = 0; k < n; ++k) {
+        for (int j = 0; j + 1 < n_gen; ++j) out[(size_t)k * n_gen + j] = h[(size_t)k * n_gen + j];
+        out[(size_t)k * n_gen + n_gen - 1] = (llama_token)key_token(keys.data() + (size_t)k * kArgSlots);
+        set_seq_past(c, seqs[k], pos0[k] + n_gen);
+    }
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, c.ev0, c.ev1);
+    c.last_us = ms * 1e3;
+    c.last_bytes = bytes;
+    c.n_outputs = 0;
+    (void)max_end;
+    return n_gen;
+    API_CATCH(-5)
+}
+
+bool llama_kv_self_seq_rm(struct llama_context* ctx, llama_seq_id seq_id, llama_pos p0, llama_pos p1) {
+    if (!ctx) return false;
+    Context& c = ctx->c;
+    if (seq_id >= c.n_seq) return false;
+    if (p1 >= 0) { set_err("llama_kv_self_seq_rm: only tail removal [p0, inf) is supported"); return false; }
+    const int lo = seq_id < 0 ? 0 : seq_id, hi = seq_id < 0 ? c.n_seq : seq_id + 1;
+    (void)hipSetDevice(c.device);
+    for (int s = lo; s < hi; ++s) {
+        if (p0 <= 0) {
+            context_clear_seq(c, s);
+        } else {
+            // positions >= p0 are rewritten before any step attends to them (a step at
+            // position p reads KV rows [0, p]): truncation is a bookkeeping change
+            set_seq_past(c, s, std::min(seq_past_of(c, s), (int)p0));
+        }
+    }
+    return true;
+}
+
+int32_t llmi_seq_pos_max(const struct llama_context* ctx, llama_seq_id seq_id) {
+    if (!ctx || seq_id < 0 || seq_id >= ctx->c.n_seq) return -1;
+    return seq_past_of(ctx->c, seq_id) - 1;
 }
 
 int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps, double* us,

@@ -46,8 +46,9 @@ Context::~Context() {
     (void)hipGetDevice(&cur);
     if (m) (void)hipSetDevice(device);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
-    void* bufs[] = {x, q, att, h, logits, scores, rope, kc, vc, st, hist, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad,
-                    step_mv, step_bar, step_trace};
+    for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
+    void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad,
+                    step_mv, step_bar, step_trace, bx, bq, batt, bh, blogits, bscores, btpos, btseq};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -252,7 +253,7 @@ bool model_clone_layout(const Model& src, int device, Model& dst, std::string& e
     return true;
 }
 
-bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string& err) {
+bool context_init(Model* m, int n_ctx, bool use_graphs, int n_seq, Context& c, std::string& err) {
     const HParams& hp = m->hp;
     c.m = m;
     c.device = m->device;
@@ -283,10 +284,16 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string&
     c.fault_dev = (unsigned*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx) + 2 * (size_t)hp.n_head * kXAttnMaxKV);
     HIPC(hipHostMalloc((void**)&c.fault_host, 16, hipHostMallocDefault));
     *c.fault_host = 0;
-    HIPC(hipMalloc(&c.kc, kv_elems * 2));
-    HIPC(hipMalloc(&c.vc, kv_elems * 2));
-    HIPC(hipMalloc(&c.st, sizeof(StepState)));
-    HIPC(hipMalloc(&c.hist, (size_t)c.n_ctx * 4));
+    if (n_seq < 1 || n_seq > 64) { err = "n_seq_max must be in [1, 64]"; return false; }
+    c.n_seq = n_seq;
+    c.kv_seq_elems = kv_elems;
+    const int nalloc = n_seq > 1 ? n_seq + 1 : 1;  // + the dummy sequence of padded batch slots
+    HIPC(hipMalloc(&c.kc0, kv_elems * 2 * nalloc));
+    HIPC(hipMalloc(&c.vc0, kv_elems * 2 * nalloc));
+    HIPC(hipMalloc(&c.st0, sizeof(StepState) * nalloc));
+    HIPC(hipMalloc(&c.hist0, (size_t)c.n_ctx * 4 * nalloc));
+    c.seq_past.assign((size_t)n_seq, 0);
+    c.kc = c.kc0; c.vc = c.vc0; c.st = c.st0; c.hist = c.hist0; c.cur_seq = 0;
     // RoPE table [pos][n_rot/2][cos,sin]: ggml_rope_cache_init's iterative theta, computed
     // on the host with libm cosf/sinf exactly as the CPU path does
     const int half = hp.n_rot / 2;
@@ -355,20 +362,53 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string&
     return true;
 }
 
+void context_select_seq(Context& c, int s) {
+    if (s < 0 || s >= std::max(1, c.n_seq + (c.n_seq > 1 ? 1 : 0))) return;
+    if (s != c.cur_seq && c.cur_seq < (int)c.seq_past.size()) c.seq_past[(size_t)c.cur_seq] = c.n_past;
+    c.cur_seq = s;
+    c.kc = c.kc0 + (size_t)s * c.kv_seq_elems;
+    c.vc = c.vc0 + (size_t)s * c.kv_seq_elems;
+    c.st = c.st0 + s;
+    c.hist = c.hist0 + (size_t)s * c.n_ctx;
+    if (s < (int)c.seq_past.size()) c.n_past = c.seq_past[(size_t)s];
+}
+
+void context_clear_seq(Context& c, int s) {
+    (void)hipSetDevice(c.device);
+    (void)hipMemsetAsync(c.kc0 + (size_t)s * c.kv_seq_elems, 0, c.kv_seq_elems * 2, c.stream);
+    (void)hipMemsetAsync(c.vc0 + (size_t)s * c.kv_seq_elems, 0, c.kv_seq_elems * 2, c.stream);
+    (void)hipMemsetAsync(c.hist0 + (size_t)s * c.n_ctx, 0, (size_t)c.n_ctx * 4, c.stream);
+    StepState s0{};
+    s0.token_in = -1;
+    s0.token_in_pos = -1;
+    (void)hipMemcpyAsync(c.st0 + s, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
+    (void)hipStreamSynchronize(c.stream);
+    if (s < (int)c.seq_past.size()) c.seq_past[(size_t)s] = 0;
+    if (s == c.cur_seq) c.n_past = 0;
+}
+
 void context_clear(Context& c) {
     const HParams& hp = c.m->hp;
-    const size_t kv_elems = (size_t)hp.n_layer * hp.n_head_kv * (size_t)c.n_ctx * hp.head_dim;
+    const int nalloc = c.n_seq > 1 ? c.n_seq + 1 : 1;
+    const size_t kv_elems = (size_t)hp.n_layer * hp.n_head_kv * (size_t)c.n_ctx * hp.head_dim * nalloc;
     (void)hipSetDevice(c.m->device);
-    (void)hipMemsetAsync(c.kc, 0, kv_elems * 2, c.stream);
-    (void)hipMemsetAsync(c.vc, 0, kv_elems * 2, c.stream);
-    (void)hipMemsetAsync(c.hist, 0, (size_t)c.n_ctx * 4, c.stream);
+    (void)hipMemsetAsync(c.kc0, 0, kv_elems * 2, c.stream);
+    (void)hipMemsetAsync(c.vc0, 0, kv_elems * 2, c.stream);
+    (void)hipMemsetAsync(c.hist0, 0, (size_t)c.n_ctx * 4 * nalloc, c.stream);
+    for (int s = 1; s < nalloc; ++s) {
+        StepState s1{};
+        s1.token_in = -1;
+        s1.token_in_pos = -1;
+        (void)hipMemcpyAsync(c.st0 + s, &s1, sizeof s1, hipMemcpyHostToDevice, c.stream);
+    }
+    std::fill(c.seq_past.begin(), c.seq_past.end(), 0);
     // attention scratch incl. k_attn_x's granules: the step sequence restarts at 0 below,
     // so no granule of an earlier sequence may keep a tag the new one will use
     (void)hipMemsetAsync(c.scores, 0, attn_scratch_floats(hp.n_head, c.n_ctx) * 4, c.stream);
     StepState s0{};
     s0.token_in = -1;
     s0.token_in_pos = -1;
-    (void)hipMemcpyAsync(c.st, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
+    (void)hipMemcpyAsync(c.st0, &s0, sizeof s0, hipMemcpyHostToDevice, c.stream);
     (void)hipStreamSynchronize(c.stream);
     c.n_past = 0;
 }
@@ -554,7 +594,7 @@ StepArgs step_args(const Context& c, int kv_bound) {
 // one decode step as [k_embed, memset of the barrier shards, k_step] when the persistent
 // step takes this KV bound, else the per-op launches
 static bool step_enqueue_any(Context& c, int kv_bound, std::string& err) {
-    if (c.use_step) {
+    if (c.use_step && c.cur_seq == 0) {
         const StepArgs a = step_args(c, kv_bound);
         if (step_supported(a, c.device, nullptr)) {
             EmbArgs ea;
@@ -574,7 +614,8 @@ bool step_run(Context& c, int pos, std::string& err) {
     const int bucket = pos / 256;
     const int kv_bound = std::min(c.n_ctx, (bucket + 1) * 256);
     if (!c.use_graphs) return step_enqueue_any(c, kv_bound, err);
-    auto it = c.graphs.find(bucket);
+    const int gkey = bucket * 256 + c.cur_seq;
+    auto it = c.graphs.find(gkey);
     if (it == c.graphs.end()) {
         hipGraph_t g = nullptr;
         HIPC(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
@@ -587,7 +628,141 @@ bool step_run(Context& c, int pos, std::string& err) {
         hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
         if (ei != hipSuccess) { err = "hipGraphInstantiate: " + hip_err(ei); return false; }
-        it = c.graphs.emplace(bucket, ex).first;
+        it = c.graphs.emplace(gkey, ex).first;
+    }
+    HIPC(hipGraphLaunch(it->second, c.stream));
+    return true;
+}
+
+// ---------------------------------------------------------------------------------
+// Batched decode (batch.hip): nt sequences advance one token per
+// step; every launch streams its weights once for all of them.  Per step: k_bembed, then
+// per layer QKV (k_mvn, segments grouped by weight type), the split attention over a
+// third grid dimension of slots, attn_output, gate/up, down; the output head (k_mvn
+// LOGITS) leaves each sequence's argmax in its own StepState slots.
+// ---------------------------------------------------------------------------------
+static bool balloc(Context& c, std::string& err) {
+    if (c.bx) return true;
+    const HParams& hp = c.m->hp;
+    const size_t B = kMaxBatch, E = hp.n_embd, QD = (size_t)hp.n_head * hp.head_dim, F = hp.n_ff, V = hp.n_vocab;
+    HIPC(hipMalloc(&c.bx, B * E * 4));
+    HIPC(hipMalloc(&c.bq, B * QD * 4));
+    HIPC(hipMalloc(&c.batt, B * QD * 4));
+    HIPC(hipMalloc(&c.bh, B * F * 4));
+    HIPC(hipMalloc(&c.blogits, B * V * 4));
+    HIPC(hipMalloc(&c.bscores, B * attn_scratch_floats(hp.n_head, c.n_ctx) * 4));
+    HIPC(hipMalloc(&c.btpos, B * 4));
+    HIPC(hipMalloc(&c.btseq, B * 4));
+    // padded slots read these rows: finite (zeros); their positions 0
+    HIPC(hipMemset(c.bx, 0, B * E * 4));
+    HIPC(hipMemset(c.batt, 0, B * QD * 4));
+    HIPC(hipMemset(c.bh, 0, B * F * 4));
+    HIPC(hipMemset(c.btpos, 0, B * 4));
+    HIPC(hipMemset(c.btseq, 0, B * 4));
+    return true;
+}
+
+static int bpad(int nt) { return nt <= 1 ? 1 : nt == 2 ? 2 : nt <= 4 ? 4 : 8; }
+
+static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std::string& err) {
+    const Model& m = *c.m;
+    const HParams& hp = m.hp;
+    const int E = hp.n_embd, D = hp.head_dim, QD = hp.n_head * D, nk = hp.n_head_kv * D, F = hp.n_ff, V = hp.n_vocab;
+    const size_t kv_layer = (size_t)hp.n_head_kv * c.n_ctx * D;
+#define BC(expr)                                                                          \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) { err = std::string(#expr) + ": " + hip_err(e_); return false; } \
+    } while (0)
+    BEmbArgs ea;
+    ea.w = seg_of(m, m.tok_embd, 0); ea.cols = E; ea.vocab = V; ea.n_ctx = c.n_ctx; ea.nt = nt;
+    ea.x = c.bx; ea.st = c.st0; ea.hist = c.hist0; ea.tseq = c.btseq; ea.tpos = c.btpos;
+    BC(launch_bembed(ea, c.stream));
+    MVArgs base;
+    base.tpos = c.btpos; base.tseq = c.btseq; base.kv_stride = c.kv_seq_elems; base.st = c.st0;
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const Layer& L = m.layers[(size_t)l];
+        // QKV + RoPE + f16 KV write, one launch per run of same-type segments
+        const Seg qkv[3] = {seg_of(m, L.wq, 0), seg_of(m, L.wk, QD), seg_of(m, L.wv, QD + nk)};
+        for (int i = 0; i < 3;) {
+            int j = i;
+            MVArgs a = base;
+            a.nseg = 0;
+            int rows = 0;
+            while (j < 3 && qkv[j].type == qkv[i].type) { a.seg[a.nseg++] = qkv[j]; rows += qkv[j].rows; ++j; }
+            a.cols = E; a.x = c.bx; a.x_stride = E; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps;
+            a.y = c.bq; a.y_stride = QD; a.kc = c.kc0 + l * kv_layer; a.vc = c.vc0 + l * kv_layer; a.rope = c.rope;
+            a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = QD; a.nk = nk; a.npairs = rows / 2;
+            BC(launch_mvn(a, EPI_QKV, nt, c.max_blocks, c.stream));
+            i = j;
+        }
+        BAttnArgs ba;
+        const size_t scr = attn_scratch_floats(hp.n_head, c.n_ctx);
+        for (int s = 0; s < nt; ++s) {
+            AttnArgs& at = ba.a[s];
+            const size_t sq = (size_t)seqs[s] * c.kv_seq_elems;
+            at.q = c.bq + (size_t)s * QD; at.kc = c.kc0 + sq + l * kv_layer; at.vc = c.vc0 + sq + l * kv_layer;
+            at.scores = c.bscores + (size_t)s * scr; at.tmax = at.scores + (size_t)hp.n_head * c.n_ctx;
+            at.out = c.batt + (size_t)s * QD; at.st = c.st0 + seqs[s]; at.n_ctx = c.n_ctx;
+            at.scale = 1.0f / sqrtf((float)D); at.layer = l;
+        }
+        BC(launch_battention(ba, nt, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
+        MVArgs o = base;
+        o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = QD; o.x = c.batt; o.x_stride = QD; o.y = c.bx; o.y_stride = E;
+        o.npairs = (E + 1) / 2;
+        BC(launch_mvn(o, EPI_ADD, nt, c.max_blocks, c.stream));
+        MVArgs gu = base;
+        gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2; gu.cols = E; gu.x = c.bx; gu.x_stride = E;
+        gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps; gu.y = c.bh; gu.y_stride = F; gu.npairs = F;
+        BC(launch_mvn(gu, EPI_SWIGLU, nt, c.max_blocks, c.stream));
+        MVArgs dn = base;
+        dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = F; dn.x = c.bh; dn.x_stride = F; dn.y = c.bx; dn.y_stride = E;
+        dn.npairs = (E + 1) / 2;
+        BC(launch_mvn(dn, EPI_ADD, nt, c.max_blocks, c.stream));
+    }
+    MVArgs lo = base;
+    lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.bx; lo.x_stride = E;
+    lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.blogits; lo.y_stride = V;
+    lo.npairs = (V + 1) / 2;
+    BC(launch_mvn(lo, EPI_LOGITS, nt, c.max_blocks, c.stream));
+#undef BC
+    return true;
+}
+
+bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err) {
+    const HParams& hp = c.m->hp;
+    if (nt < 1 || nt > kMaxBatch || c.n_seq < 2) { err = "batched step: 1..8 slots of a context with n_seq_max >= 2"; return false; }
+    for (const Layer& L : c.m->layers)
+        if (L.wg.type != L.wu.type) { err = "batched step: ffn_gate / ffn_up of different types"; return false; }
+    if (!balloc(c, err)) return false;
+    const int bucket = max_pos / 256;
+    const int kv_bound = std::min(c.n_ctx, (bucket + 1) * 256);
+    if ((size_t)(hp.n_head / hp.n_head_kv) * kv_bound * 4 > kSplitAttnMaxLds) { err = "batched step: context too long"; return false; }
+    // slot -> sequence map (padded slots -> the dummy sequence n_seq)
+    std::vector<int> map((size_t)kMaxBatch, c.n_seq);
+    for (int s = 0; s < nt; ++s) map[(size_t)s] = seqs[s];
+    if (map != c.btseq_host) {
+        HIPC(hipMemcpyAsync(c.btseq, map.data(), kMaxBatch * 4, hipMemcpyHostToDevice, c.stream));
+        HIPC(hipStreamSynchronize(c.stream));
+        c.btseq_host = map;
+    }
+    if (!c.use_graphs) return bstep_enqueue(c, nt, seqs, kv_bound, err);
+    std::string key = std::to_string(bucket) + ":" + std::to_string(nt);
+    for (int s = 0; s < nt; ++s) key += "," + std::to_string(seqs[s]);
+    auto it = c.bgraphs.find(key);
+    if (it == c.bgraphs.end()) {
+        hipGraph_t g = nullptr;
+        HIPC(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+        std::string e2;
+        const bool ok = bstep_enqueue(c, nt, seqs, kv_bound, e2);
+        hipError_t ec = hipStreamEndCapture(c.stream, &g);
+        if (!ok) { err = "capture: " + e2; if (g) (void)hipGraphDestroy(g); return false; }
+        if (ec != hipSuccess) { err = "hipStreamEndCapture: " + hip_err(ec); return false; }
+        hipGraphExec_t ex = nullptr;
+        hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ei != hipSuccess) { err = "hipGraphInstantiate: " + hip_err(ei); return false; }
+        it = c.bgraphs.emplace(key, ex).first;
     }
     HIPC(hipGraphLaunch(it->second, c.stream));
     return true;

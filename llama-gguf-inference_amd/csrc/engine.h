@@ -68,6 +68,16 @@ struct Prof {
 struct Context {
     Model* m = nullptr;
     int device = 0;                         // m->device, kept so teardown never reads *m
+    // sequences (llama_context_params.n_seq_max): each has its own KV cache, StepState
+    // and token history; kc/vc/st/hist below point at the CURRENT sequence's (cur_seq),
+    // kc0/vc0/st0/hist0 at sequence 0 of the arrays.  With n_seq > 1 one extra (dummy)
+    // sequence backs the padded slots of a batched step.
+    int n_seq = 1, cur_seq = 0;
+    size_t kv_seq_elems = 0;                // K (or V) cache elements per sequence
+    uint16_t *kc0 = nullptr, *vc0 = nullptr;
+    StepState* st0 = nullptr;
+    int32_t* hist0 = nullptr;
+    std::vector<int> seq_past;              // per sequence: positions decoded
     int n_ctx = 0;
     bool use_graphs = true;
     hipStream_t stream = nullptr;
@@ -89,7 +99,12 @@ struct Context {
     std::vector<unsigned long long> out_keys;  // per output: argmax key
     int n_outputs = 0;
     int n_past = 0;
-    std::map<int, hipGraphExec_t> graphs;   // by KV bucket
+    std::map<int, hipGraphExec_t> graphs;   // by KV bucket * 256 + sequence
+    // batched decode (batch.hip): kMaxBatch rows each, allocated on first use
+    float *bx = nullptr, *bq = nullptr, *batt = nullptr, *bh = nullptr, *blogits = nullptr, *bscores = nullptr;
+    int *btpos = nullptr, *btseq = nullptr;
+    std::vector<int> btseq_host;            // the slot -> sequence map btseq holds
+    std::map<std::string, hipGraphExec_t> bgraphs;  // by (slots, sequences, KV bucket)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     unsigned* fault_dev = nullptr;          // device fault word: a bounded in-kernel wait gave up
     unsigned* fault_host = nullptr;         // pinned copy, read back with every decode call
@@ -107,7 +122,14 @@ struct Context {
 
 // all return false and set err on failure
 bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& m, std::string& err);
-bool context_init(Model* m, int n_ctx, bool use_graphs, Context& c, std::string& err);
+bool context_init(Model* m, int n_ctx, bool use_graphs, int n_seq, Context& c, std::string& err);
+// point the single-sequence paths (step_run, prefill_enqueue, state) at sequence s
+void context_select_seq(Context& c, int s);
+// clear one sequence's KV cache, history and state
+void context_clear_seq(Context& c, int s);
+// one batched decode step of nt sequences seqs[0..nt) (their StepStates hold token and
+// position), replayed from a graph per (slots, sequences, KV bucket of max_pos)
+bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err);
 // enqueue one decode step for a state already set (token_in/pos_next); kv_bound >= pos+1
 bool step_enqueue(Context& c, int kv_bound, std::string& err);
 // the persistent step's arguments for a KV bound (step.hip)

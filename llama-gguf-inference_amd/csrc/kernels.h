@@ -63,6 +63,14 @@ struct MVArgs {
     int split_pairs = 0;                   // two-type launches: pairs of the first type group ...
     int split_wgs = 0;                     // ... and the workgroups that run them (set by launch_matvec)
     int xfirst = 0;                        // experiment: multi-round launches also wait for x before weights
+    // batched decode (batch.hip, k_mvn): token t of the batch is one decode step of
+    // sequence tseq[t] at position tpos[t]; x / y rows are x_stride / y_stride floats
+    // apart; the sequence's KV cache is kv_stride elements past the first one; LOGITS
+    // uses the sequence's StepState (st + tseq[t]) for its argmax slots
+    int x_stride = 0, y_stride = 0;
+    const int* tpos = nullptr;
+    const int* tseq = nullptr;
+    size_t kv_stride = 0;
 };
 
 struct AttnArgs {
@@ -82,6 +90,26 @@ struct AttnArgs {
     int tag_skew = 0;                     // test option: consumers expect tag + skew
     unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [kernel][block][wave][4] stamps
 };
+
+// Batched decode (batch.hip): up to kMaxBatch sequences advance one token per step.
+constexpr int kMaxBatch = 8;
+struct BAttnArgs {
+    AttnArgs a[kMaxBatch];  // per batch slot (its sequence's caches, q, scratch, state)
+};
+struct BEmbArgs {
+    Seg w;
+    int cols = 0, vocab = 0, n_ctx = 0, nt = 0;
+    float* x = nullptr;           // [nt][cols]
+    StepState* st = nullptr;      // per sequence
+    int32_t* hist = nullptr;      // [seq][n_ctx]
+    const int* tseq = nullptr;    // slot -> sequence
+    int* tpos = nullptr;          // slot -> position of this step (written)
+};
+hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s);
+hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s);
+hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
+                             hipStream_t s);
+size_t mvn_lds_bytes(int act, int cols, int nt);
 
 struct EmbArgs {
     Seg w;                          // token_embd in device layout

@@ -461,15 +461,7 @@ __global__ __launch_bounds__(256) void k_attn_pv(AttnArgs a) {
 }
 
 
-#if defined(LLMI_EXP_TRACE)
-// per-wave stamps of the attention kernels: trace[(k * 4096 + block) * 16 + wave * 4 + i]
-#define LLMI_ATT_STAMP(K, I)                                                                      \
-    if (a.trace && (threadIdx.x & 63) == 0)                                                       \
-        a.trace[((size_t)(K) * 4096 + blockIdx.y * gridDim.x + blockIdx.x) * 64 + (threadIdx.x >> 6) * 4 + (I)] = \
-            __builtin_amdgcn_s_memrealtime();
-#else
-#define LLMI_ATT_STAMP(K, I)
-#endif
+
 // Split attention, phase 1: grid (HK, kv_bound/64), 256 threads; thread (t, qd) dots
 // quarter qd of K row t with the G f16-rounded query heads of its group (G independent
 // double chains of D/4), then a 4-lane butterfly; K rows are read straight from HBM,
@@ -623,186 +615,12 @@ __global__ __launch_bounds__(256) void k_attn_pv_split(AttnArgs a, int kvb) {
     LLMI_ATT_STAMP(1, 3)
 }
 
-// Split attention v2, phase 1: grid (HK, kv_bound/32), 256 threads; thread (t, qd)
-// dots 1/8 of K row t (D/8 dims) with the G f16-rounded query heads (G independent
-// double chains of D/8), 8-lane butterfly; K loads issued before the position is
-// known.  Also writes the tile's per-head score maximum (tmax) so phase 2 needs no
-// pass over the scores to find the row maximum (max is exact in any order).
+// Split attention v2 (bodies in mv_device.h: attn_scores8_body / attn_pv16_body, shared
+// with the batched decode's per-sequence launches in batch.hip).
 template <int D, int G>
-__global__ __launch_bounds__(256) void k_attn_scores8(AttnArgs a) {
-    LLMI_ATT_STAMP(0, 0)
-    const int g = blockIdx.x, tile = blockIdx.y, t0 = tile * 32;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int DQ = D / 8;  // 16 (D=128) or 8 (D=64) dims per lane
-    const int t = t0 + (tid >> 3), qd = tid & 7;
-    const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
-    u32x4 kv[DQ / 8];
-#pragma unroll
-    for (int i = 0; i < DQ / 8; ++i) kv[i] = __builtin_nontemporal_load((const u32x4*)(kr + 8 * i));  // K read once
-    // q rounded to f16 as upstream's KQ mul_mat does, held as double: every k*q product
-    // of two f16 values is exact, so fma(k, q, acc) == acc + (double)(k * q)
-    __shared__ __attribute__((aligned(16))) double qs[G][D];
-    __shared__ float wmax[4][G];
-    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = (double)h2f(f2h(a.q[(size_t)g * G * D + i]));
-    const int n_kv = a.st->pos + 1;
-    __syncthreads();
-    LLMI_ATT_STAMP(0, 1)
-    if (t0 >= n_kv) return;
-    double acc[G];
-#pragma unroll
-    for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
-#pragma unroll
-    for (int i = 0; i < DQ / 8; ++i) {
-        const int d = qd * DQ + 8 * i;
-        double k[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            k[2 * j] = (double)h2f((uint16_t)kv[i][j]);
-            k[2 * j + 1] = (double)h2f((uint16_t)(kv[i][j] >> 16));
-        }
-#pragma unroll
-        for (int hh = 0; hh < G; ++hh)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[hh] = __builtin_fma(k[j], qs[hh][d + j], acc[hh]);
-    }
-#pragma unroll
-    for (int hh = 0; hh < G; ++hh) {
-        acc[hh] += xor_partner_d<1>(acc[hh]);
-        acc[hh] += xor_partner_d<2>(acc[hh]);
-        acc[hh] += xor_partner_d<4>(acc[hh]);
-        const float sc = (float)acc[hh] * a.scale;
-        if (t < n_kv && qd == (hh & 7)) a.scores[(size_t)(g * G + hh) * a.n_ctx + t] = sc;
-        // tile max: 8 positions per wave (lanes xor 8, 16, 32), then the 4 waves
-        float m = t < n_kv ? sc : -INFINITY;
-        m = fmaxf(m, xor_partner<8>(m));
-        m = fmaxf(m, xor_partner<16>(m));
-        m = fmaxf(m, xor_partner<32>(m));
-        if (lane == 0) wmax[wave][hh] = m;
-    }
-    __syncthreads();
-    if (tid < G)
-        a.tmax[(size_t)(g * G + tid) * (a.n_ctx / 32) + tile] =
-            fmaxf(fmaxf(wmax[0][tid], wmax[1][tid]), fmaxf(wmax[2][tid], wmax[3][tid]));
-    LLMI_ATT_STAMP(0, 3)
-}
-
-// Split attention v2, phase 2: grid (HK, D/16), 512 threads.  Softmax of the group's G
-// heads by 8/G waves each: row max from the tile maxima, e = expf(s - max) with a
-// double sum (waves combined in fixed order), p = f16(e / sum) exactly as upstream's
-// non-FA path, in LDS as f32 (scores -> e -> p in place); then PV for 16
-// output dims: 32 lanes per dim, lane sl takes positions 4*sl + 128*k (8-B V loads, a
-// 1024-position window in flight, issued before the position is known),
-// fma(v, p, acc) in double (f16 x f16 products are exact; p read as conflict-free
-// float4 per 4 positions), 32-lane butterfly.
+__global__ __launch_bounds__(256) void k_attn_scores8(AttnArgs a) { attn_scores8_body<D, G>(a); }
 template <int D, int G>
-__global__ __launch_bounds__(512) void k_attn_pv16(AttnArgs a, int kvb) {
-    LLMI_ATT_STAMP(1, 0)
-    extern __shared__ __attribute__((aligned(16))) float spd[];  // [G][kvb]
-    __shared__ float redm[8];
-    __shared__ double reds[8];
-    constexpr int WPH = 8 / G;  // waves per head
-    const int g = blockIdx.x, dc = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int d = dc * 16 + (tid >> 5), sl = tid & 31;
-    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
-    // 1. stage the G score rows (all kv_bound positions; those past n_kv are never used)
-    const int n4 = kvb >> 2;
-#pragma unroll
-    for (int hh = 0; hh < G; ++hh) {
-        const float4* src = (const float4*)(a.scores + (size_t)(g * G + hh) * a.n_ctx);
-        float4* dst = (float4*)(spd + hh * kvb);
-        for (int j = tid; j < n4; j += 512) dst[j] = src[j];
-    }
-    // V window issued after the score staging (loads return in order: the staging
-    // must not queue behind it), in flight during the softmax
-    constexpr int NV = 8;  // 8-B V loads in flight per lane: a 1024-position window
-    u32x2 vv[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(4 * sl + 128 * k, kvb - 4)));
-    const int n_kv = a.st->pos + 1;
-    const int hh = wave / WPH, wi = wave % WPH;
-    {   // row max from the tile maxima (all kv_bound/32 tiles loaded without waiting for
-        // the position; tiles past n_kv masked afterwards)
-        const float* tm = a.tmax + (size_t)(g * G + hh) * (a.n_ctx / 32);
-        const int nt_all = kvb >> 5;
-        float mt[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) mt[u] = tm[min(wi * 64 + lane + u * WPH * 64, nt_all - 1)];
-        const int ntile = (n_kv + 31) >> 5;
-        float m = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (wi * 64 + lane + u * WPH * 64 < ntile) m = fmaxf(m, mt[u]);
-        for (int i = wi * 64 + lane + 4 * WPH * 64; i < ntile; i += WPH * 64) m = fmaxf(m, tm[i]);
-        m = wave_max(m);
-        if (lane == 0) redm[wave] = m;
-    }
-    __syncthreads();
-    LLMI_ATT_STAMP(1, 1)
-    float mx = redm[hh * WPH];
-#pragma unroll
-    for (int i = 1; i < WPH; ++i) mx = fmaxf(mx, redm[hh * WPH + i]);
-    // 2. e and the double sum, then p
-    float* sp = spd + hh * kvb;
-    double sum = 0.0;
-    for (int t = wi * 64 + lane; t < n_kv; t += WPH * 64) {
-        const float e = llmi_expf(sp[t] - mx);
-        sp[t] = e;
-        sum += (double)e;
-    }
-    sum = wave_sum_d(sum);
-    if (lane == 0) reds[wave] = sum;
-    __syncthreads();
-    double tot = reds[hh * WPH];
-#pragma unroll
-    for (int i = 1; i < WPH; ++i) tot += reds[hh * WPH + i];
-    const float inv = (float)(1.0 / tot);
-    for (int t = wi * 64 + lane; t < n_kv; t += WPH * 64) sp[t] = h2f(f2h(sp[t] * inv));
-    for (int t = n_kv + wi * 64 + lane; t < ((n_kv + 3) & ~3); t += WPH * 64) sp[t] = 0.f;
-    __syncthreads();
-    LLMI_ATT_STAMP(1, 2)
-    // 3. PV
-    double acc[G];
-#pragma unroll
-    for (int h = 0; h < G; ++h) acc[h] = 0.0;
-    for (int t0 = 4 * sl;;) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            const int tb = t0 + 128 * k;
-            if (tb < n_kv) {
-                double v[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float f = h2f((uint16_t)((j < 2 ? vv[k].x : vv[k].y) >> (16 * (j & 1))));
-                    v[j] = tb + j < n_kv ? (double)f : 0.0;
-                }
-#pragma unroll
-                for (int h = 0; h < G; ++h) {
-                    const float4 p = *(const float4*)(spd + h * kvb + tb);
-                    acc[h] = __builtin_fma(v[0], (double)p.x, acc[h]);
-                    acc[h] = __builtin_fma(v[1], (double)p.y, acc[h]);
-                    acc[h] = __builtin_fma(v[2], (double)p.z, acc[h]);
-                    acc[h] = __builtin_fma(v[3], (double)p.w, acc[h]);
-                }
-            }
-        }
-        t0 += 128 * NV;
-        if (t0 >= n_kv) break;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) vv[k] = __builtin_nontemporal_load((const u32x2*)(vr + min(t0 + 128 * k, kvb - 4)));
-    }
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-        double v = acc[h];
-        v += xor_partner_d<1>(v);
-        v += xor_partner_d<2>(v);
-        v += xor_partner_d<4>(v);
-        v += xor_partner_d<8>(v);
-        v += xor_partner_d<16>(v);
-        if (sl == 0) a.out[(size_t)(g * G + h) * D + d] = (float)v;
-    }
-    LLMI_ATT_STAMP(1, 3)
-}
+__global__ __launch_bounds__(512) void k_attn_pv16(AttnArgs a, int kvb) { attn_pv16_body<D, G>(a, kvb); }
 
 // One-launch exchange attention for short contexts (kv_bound <= kXAttnMaxKV): grid
 // (HK, D/16), 512 threads.  Workgroup (g, j) computes the scores of position tile j

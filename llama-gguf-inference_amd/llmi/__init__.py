@@ -150,23 +150,34 @@ class Model:
 class Context:
     """llama_init_from_model: KV cache + scratch + step graphs on the model's device."""
 
-    def __init__(self, model: Model, n_ctx: int = 0, use_graphs: bool = True):
+    def __init__(self, model: Model, n_ctx: int = 0, use_graphs: bool = True, n_seq: int = 1):
         L = lib()
         p = L.llama_context_default_params()
         p.n_ctx = n_ctx
         p.use_graphs = use_graphs
+        p.n_seq_max = n_seq
+        self.n_seq = n_seq
         self._h = L.llama_init_from_model(model._h, p)
         if not self._h:
             raise LlmiError(last_error())
         self.model = model
         self.n_ctx = int(L.llama_n_ctx(self._h))
 
-    def decode(self, tokens: Sequence[int], pos: Optional[Sequence[int]] = None, logits_all: bool = False) -> int:
-        """llama_decode: returns 0 ok, 1 no KV slot, <0 error (same codes as upstream)."""
+    def decode(self, tokens: Sequence[int], pos: Optional[Sequence[int]] = None, logits_all: bool = False,
+               seq: Optional[Sequence[int]] = None) -> int:
+        """llama_decode: returns 0 ok, 1 no KV slot, <0 error (same codes as upstream).
+        seq: per-token sequence id (llama_batch.seq_id[i][0]); None = sequence 0."""
         n = len(tokens)
         toks = (C.c_int32 * n)(*tokens)
         b = lib().llama_batch_get_one(toks, n)
         keep = [toks]
+        if seq is not None:
+            ids = [(C.c_int32 * 1)(int(s)) for s in seq]
+            ptrs = (C.POINTER(C.c_int32) * n)(*[C.cast(a, C.POINTER(C.c_int32)) for a in ids])
+            nsi = (C.c_int32 * n)(*([1] * n))
+            b.seq_id = C.cast(ptrs, C.POINTER(C.POINTER(C.c_int32)))
+            b.n_seq_id = C.cast(nsi, C.POINTER(C.c_int32))
+            keep += [ids, ptrs, nsi]
         if pos is not None:
             pa = (C.c_int32 * n)(*pos)
             b.pos = C.cast(pa, C.POINTER(C.c_int32))
@@ -202,6 +213,24 @@ class Context:
         if r != n:
             raise LlmiError(f"llmi_generate_greedy returned {r}: {last_error()}")
         return list(out)
+
+    def generate_greedy_batch(self, seqs: Sequence[int], first: Sequence[int], pos0: Sequence[int], n: int) -> list[list[int]]:
+        """llmi_generate_greedy_batch: sequences seqs advance together, one batched step
+        per token (continuous batching); returns each sequence's n tokens."""
+        k = len(seqs)
+        sa, fa, pa = (C.c_int32 * k)(*seqs), (C.c_int32 * k)(*first), (C.c_int32 * k)(*pos0)
+        out = (C.c_int32 * (k * n))()
+        r = lib().llmi_generate_greedy_batch(self._h, k, sa, fa, pa, int(n), out)
+        if r != n:
+            raise LlmiError(f"llmi_generate_greedy_batch returned {r}: {last_error()}")
+        return [list(out[i * n:(i + 1) * n]) for i in range(k)]
+
+    def seq_rm(self, seq: int, p0: int = 0, p1: int = -1) -> bool:
+        """llama_kv_self_seq_rm (tail removal)."""
+        return bool(lib().llama_kv_self_seq_rm(self._h, int(seq), int(p0), int(p1)))
+
+    def seq_pos_max(self, seq: int) -> int:
+        return int(lib().llmi_seq_pos_max(self._h, int(seq)))
 
     def stats(self) -> tuple[float, float]:
         b, u = C.c_double(), C.c_double()

@@ -87,6 +87,10 @@ SIGNATURES = {
     "llmi_device_count": (C.c_int32, []),
     "llmi_greedy_ith": (C.c_int32, [_P, C.c_int32]),
     "llmi_generate_greedy": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
+    "llmi_generate_greedy_batch": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_int32)]),
+    "llama_kv_self_seq_rm": (C.c_bool, [_P, C.c_int32, C.c_int32, C.c_int32]),
+    "llmi_seq_pos_max": (C.c_int32, [_P, C.c_int32]),
     "llmi_last_step_stats": (None, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "llmi_test_option": (C.c_int32, [C.c_char_p, C.c_int32]),
     "llmi_step_path": (C.c_int32, [_P, C.c_int32]),
