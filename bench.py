@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=20)
     ap.add_argument("--cpu-sample-tokens", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--batch-seqs", default="2,4,8",
+                    help="continuous-batching leg: sequence counts to time (comma list, '' to skip)")
+    ap.add_argument("--batch-steps", type=int, default=64)
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r02"),
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
     return ap.parse_args(argv)
@@ -181,6 +184,43 @@ class LlmiEngine:
         """Per-class kernel time at the current position (consumes no tokens)."""
         return self.ctx.profile_kernels(self.next, self.pos, n)
 
+    def batched(self, counts: list[int], steps: int) -> dict:
+        """Continuous-batching leg (reported beside `value`, never as it): k sequences of one
+        context (the same 128-token prompt length, different prompts) advance together
+        through batched steps (llmi_generate_greedy_batch); aggregate tokens/s = k *
+        steps / time of `steps` steps after 8 warmup steps."""
+        import numpy as np
+
+        llmi = self.llmi
+        kmax = max(counts)
+        n_ctx = ((self.args.prompt + steps + 8 + 2 + 255) // 256) * 256
+        ctx = llmi.Context(self.model, n_ctx=n_ctx, n_seq=kmax)
+        rng = np.random.default_rng(40)
+        bos = self.model.bos if self.model.bos >= 0 else 1
+        prompts = [[bos] + [int(t) for t in rng.integers(0, min(128000, self.model.n_vocab), self.args.prompt - 1)]
+                   for _ in range(kmax)]
+        firsts = []
+        for s, p in enumerate(prompts):
+            assert ctx.decode(p, seq=[s] * len(p)) == 0
+            firsts.append(ctx.greedy(-1))
+        out = {}
+        for k in counts:
+            seqs = list(range(k))
+            for s in seqs:
+                ctx.seq_rm(s, len(prompts[s]), -1)
+            pos = [len(prompts[s]) for s in seqs]
+            g = ctx.generate_greedy_batch(seqs, firsts[:k], pos, 8)
+            nxt = [t[-1] for t in g]
+            pos = [q + 8 for q in pos]
+            self.sync()
+            t0 = time.perf_counter()
+            ctx.generate_greedy_batch(seqs, nxt, pos, steps)
+            self.sync()
+            dt = time.perf_counter() - t0
+            out[str(k)] = {"tok_s": round(k * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4)}
+        ctx.close()
+        return out
+
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -269,6 +309,13 @@ def main(argv=None):
     # end-to-end roofline: algorithmic bytes of the timed tokens / time (this rank)
     e2e_gbps = eng.bytes / (eng.us * 1e-6) / 1e9 if eng.us > 0 else 0.0
     prof = eng.profile(args.profile_steps) if args.profile_steps > 0 else {}
+    counts = [int(x) for x in args.batch_seqs.split(",") if x.strip()]
+    batched = None
+    if counts:
+        try:
+            batched = eng.batched(counts, args.batch_steps)
+        except Exception as e:  # reported beside the metric, never required
+            log(f"batched leg failed: {e}")
     result = None
     if dist.rank == 0:
         k = prof.get(DOMINANT, {"us": 0.0, "bytes": 0.0})
@@ -319,6 +366,11 @@ def main(argv=None):
                         "ttft_ms": round(eng.prefill_warm_s * 1e3, 2),
                         "tok_per_s": round(args.prompt / max(eng.prefill_warm_s, 1e-9), 1)},
             "fanout_s": round(eng.fanout_s, 3),
+            "continuous_batching": {"sequences": batched,
+                                    "note": "k sequences per replica in batched steps (one weight stream per step), "
+                                            f"{args.prompt}-token prompts, {args.batch_steps} timed steps; "
+                                            "aggregate tokens/s of this rank; not the metric's value"}
+            if batched else None,
             "cpu_baseline": cpu,
             "env": knobs,
         }

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Turn tools/bench_profile.sh's two rocprofv3 passes into the committed roofline evidence:
+<out>/traffic_<preset>.json (dominant kernel: FETCH_SIZE bytes per launch, corrected x2
+on gfx950 per MI355X_MICROARCH.md §HBM; rocprof average duration) and
+<out>/kernel_stats.csv (the --stats summary)."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+out, preset = sys.argv[1], sys.argv[2]
+DOM = "k_matvec<0, true, 3,"  # fused ffn_gate+ffn_up + SwiGLU (bench.py DOMINANT)
+stats = glob.glob(os.path.join(out, "stats", "**", "*kernel_stats.csv"), recursive=True)
+pmc = glob.glob(os.path.join(out, "pmc", "**", "*counter_collection.csv"), recursive=True)
+assert stats and pmc, (stats, pmc)
+rows = list(csv.DictReader(open(stats[0])))
+dom = [r for r in rows if DOM in r["Name"]]
+assert len(dom) == 1, [r["Name"] for r in dom]
+us = float(dom[0]["AverageNs"]) / 1e3
+vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(pmc[0]))
+        if r["Counter_Name"] == "FETCH_SIZE" and DOM in r["Kernel_Name"]]
+assert vals
+fetch_kib = sum(vals) / len(vals)
+res = {
+    "preset": preset,
+    "kernel": dom[0]["Name"],
+    "rocprof_us": round(us, 3),
+    "rocprof_calls": int(dom[0]["Calls"]),
+    "fetch_size_kib_mean": fetch_kib,
+    "hbm_bytes_per_launch": round(fetch_kib * 1024 * 2),
+    "launches_counted": len(vals),
+    "correction": "bytes = 2 * 1024 * FETCH_SIZE (gfx950 counts wide streaming reads at half, MI355X_MICROARCH.md §HBM)",
+    "source": f"rocprofv3 --pmc FETCH_SIZE over bench.py --preset {preset} (tools/bench_profile.sh); "
+              "duration from the separate --kernel-trace --stats pass",
+}
+json.dump(res, open(os.path.join(out, f"traffic_{preset}.json"), "w"), indent=1)
+shutil.copy(stats[0], os.path.join(out, "kernel_stats.csv"))
+print(json.dumps(res, indent=1))
