@@ -17,7 +17,8 @@ constexpr int kMVThreads = LLMI_MV_THREADS;  // matvec workgroup; each wave owns
 constexpr int kMVWaves = kMVThreads / 64;
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
 constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
-constexpr int kXAttnMaxKV = 1024;  // one-launch exchange attention (k_attn_x) up to this KV bound
+constexpr int kXAttnMaxKV = 1024;
+constexpr int kRegAttnMaxKV = 512;  // register-prefetched one-launch attention (k_attn_r) up to this KV bound  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
 extern int g_pf_attn_simple, g_pf_max_kv, g_xspin_limit, g_xtag_skew;

@@ -843,6 +843,7 @@ __global__ __launch_bounds__(512) void k_attn_x(AttnArgs a, int kvb) {
 // so 3 of 4 K/V reads hit that XCD's L2).  Same numerics as the two-kernel path above.
 template <int D>
 __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) {
+    LLMI_ATT_STAMP(0, 0)
     extern __shared__ __attribute__((aligned(16))) float sp_lds[];
     __shared__ float qs[D];
     __shared__ double redd[16];
@@ -872,6 +873,7 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
         sp_lds[t] = w;
         mx = fmaxf(mx, w);
     }
+    LLMI_ATT_STAMP(0, 1)
     mx = wave_max(mx);
     if (lane == 0) redf[wave] = mx;
     __syncthreads();
@@ -889,6 +891,7 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
     const float inv = (float)(1.0 / tot);
     for (int t = tid; t < n_kv; t += 1024) sp_lds[t] = h2f(f2h(llmi_expf(sp_lds[t] - mx) * inv));
     __syncthreads();
+    LLMI_ATT_STAMP(0, 2)
     // PV over the transposed V cache: SL threads per output dim, 8 positions (16 B) each
     constexpr int SL = 1024 / D;
     const int d = tid / SL, sl = tid % SL;
@@ -913,6 +916,125 @@ __global__ __launch_bounds__(1024) void k_attn_fused(AttnArgs a, int G, int HK) 
     if constexpr (SL >= 16) acc += xor_partner_d<8>(acc);
     static_assert(SL == 8 || SL == 16, "head_dim 64 or 128");
     if (sl == 0) a.out[(size_t)h * D + d] = (float)acc;
+    LLMI_ATT_STAMP(0, 3)
+}
+
+// Register-prefetched one-launch attention for short contexts (kv_bound <= 64*P <= 512):
+// one 512-thread workgroup per query head.  Every global load of the launch — the step
+// position, the head's q slice, all kv_bound K rows and the V window — is issued at
+// entry (addresses clamped into the bucket, never gated on the position), so one memory
+// latency covers the launch; the rest is the dependent compute chain:
+//   scores  8 lanes x D/8 dims per position (exact f16 products summed in double, 3-step
+//           butterfly), P passes of 64 positions; scores to LDS, row max per wave
+//   softmax e = expf(s - max), double sum over the workgroup (fixed order), p =
+//           f16(e * (float)(1/sum)) in LDS as f32 — the formulas of k_attn_fused
+//   PV      512/D lanes per output dim, double fma of exact f16 products, butterfly.
+// Same numerics as the other paths (the double sums are exact in practice; the paths
+// are checked bit-identical against each other and the oracle).
+template <int D, int P>
+__global__ __launch_bounds__(512) void k_attn_r(AttnArgs a, int G, int kvb) {
+    constexpr int DQ = D / 8;          // score dims per lane
+    constexpr int SLV = 512 / D;       // PV lanes per output dim (4 or 8)
+    constexpr int NVL = 64 * P / (8 * SLV);  // 16-B V loads per lane (8 positions each)
+    __shared__ __attribute__((aligned(16))) float sp[64 * P + 8];
+    __shared__ float redm[8];
+    __shared__ double reds[8];
+    LLMI_ATT_STAMP(0, 0)
+    const int h = blockIdx.x, g = h / G;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qd = tid & 7, pp = tid >> 3;
+    // 1. every load up front: position, q slice, K rows of all passes, V window
+    const int pos = a.st->pos;
+    float4 qv[DQ / 4];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; ++i) qv[i] = *(const float4*)(a.q + (size_t)h * D + qd * DQ + 4 * i);
+    u32x4 kv[P][DQ / 8];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int t = min(64 * p + pp, kvb - 1);
+        const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = __builtin_nontemporal_load((const u32x4*)(kr + 8 * i));
+    }
+    const int d = tid / SLV, sl = tid % SLV;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    u32x4 vv[NVL];
+#pragma unroll
+    for (int u = 0; u < NVL; ++u) vv[u] = __builtin_nontemporal_load((const u32x4*)(vr + min(8 * sl + 8 * SLV * u, kvb - 8)));
+    const int n_kv = pos + 1;
+    // 2. scores (q rounded to f16 as upstream's KQ mul_mat does; f16 x f16 products exact)
+    double q[DQ];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; ++i) {
+        q[4 * i + 0] = (double)h2f(f2h(qv[i].x)); q[4 * i + 1] = (double)h2f(f2h(qv[i].y));
+        q[4 * i + 2] = (double)h2f(f2h(qv[i].z)); q[4 * i + 3] = (double)h2f(f2h(qv[i].w));
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                acc = __builtin_fma((double)h2f((uint16_t)kv[p][i][jj]), q[8 * i + 2 * jj], acc);
+                acc = __builtin_fma((double)h2f((uint16_t)(kv[p][i][jj] >> 16)), q[8 * i + 2 * jj + 1], acc);
+            }
+        acc += xor_partner_d<1>(acc);
+        acc += xor_partner_d<2>(acc);
+        acc += xor_partner_d<4>(acc);
+        const int t = 64 * p + pp;
+        const float sc = (float)acc * a.scale;
+        if (qd == 0) sp[t] = sc;
+        if (t < n_kv) m = fmaxf(m, sc);
+    }
+    LLMI_ATT_STAMP(0, 1)
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
+    __syncthreads();
+    float mx = redm[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) mx = fmaxf(mx, redm[w]);
+    // 3. softmax: thread t owns position t (64*P <= 512 positions)
+    float e = 0.f;
+    double s = 0.0;
+    if (tid < n_kv && tid < 64 * P) {
+        e = llmi_expf(sp[tid] - mx);
+        s = (double)e;
+    }
+    s = wave_sum_d(s);
+    if (lane == 0) reds[wave] = s;
+    __syncthreads();
+    double tot = reds[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) tot += reds[w];
+    const float inv = (float)(1.0 / tot);
+    if (tid < 64 * P) sp[tid] = tid < n_kv ? h2f(f2h(e * inv)) : 0.f;
+    __syncthreads();
+    LLMI_ATT_STAMP(0, 2)
+    // 4. PV: lane sl covers positions 8*sl + 8*SLV*u + j; two double chains
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NVL; ++u) {
+        const int tb = 8 * sl + 8 * SLV * u;
+        if (tb < n_kv) {
+            const float4 p0 = *(const float4*)(sp + tb), p1 = *(const float4*)(sp + tb + 4);
+            const float pr[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float f = h2f((uint16_t)(vv[u][j >> 1] >> (16 * (j & 1))));
+                const double v = tb + j < n_kv ? (double)f : 0.0;
+                if (j & 1) acc1 = __builtin_fma(v, (double)pr[j], acc1);
+                else acc0 = __builtin_fma(v, (double)pr[j], acc0);
+            }
+        }
+    }
+    double acc = acc0 + acc1;
+    acc += xor_partner_d<1>(acc);
+    acc += xor_partner_d<2>(acc);
+    if constexpr (SLV == 8) acc += xor_partner_d<4>(acc);
+    if (sl == 0) a.out[(size_t)h * D + d] = (float)acc;
+    LLMI_ATT_STAMP(0, 3)
 }
 
 // ----------------------------------------------------------------------------------
@@ -1336,6 +1458,7 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     const bool fused_ok = kv_bound <= kFusedAttnMaxKV;
     (void)n_head;
     if (g_attn_mode == 4 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
+    if (g_attn_mode == 5 && kv_bound <= kRegAttnMaxKV) return 5;
     if (g_attn_mode == 1 && fused_ok) return 1;
     if (g_attn_mode == 2 && split_ok) return 2;
     if (g_attn_mode == 3) return 3;
@@ -1345,7 +1468,10 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     //                             split beyond (640: 10.8 vs 12.9 exchange)
     //   G=8, D=128 (70B): fused <= 640 (128: 8.1 vs 16.3 exchange), split beyond
     //   G=8, D=64 (TinyLlama): fused <= 2048 (128: 6.2 vs 9.7; 1280: 15.9 vs 20.9)
+    //   G=8, D=64: register-prefetched k_attn_r <= 256 (5.5-5.9 vs 6.2-6.7 fused); for
+    //              D=128 it loses to fused (one CU pulls 64 KB+ per head: per-CU bandwidth)
     if (g_attn_mode == 0) {
+        if (g == 8 && head_dim == 64 && kv_bound <= 256) return 5;
         if (g == 8 && fused_ok && kv_bound <= (head_dim == 64 ? 2048 : 640)) return 1;
         if (g == 4 && fused_ok && kv_bound <= 256) return 1;
         if (g == 4 && split_ok && kv_bound > 512) return 2;
@@ -1363,6 +1489,15 @@ hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int h
     int path = attn_path(n_head, n_head_kv, kv_bound, head_dim);
     if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254))
         path = attn_path(n_head, n_head_kv, kXAttnMaxKV + 256, head_dim);
+    if (path == 5) {
+        const int p = kv_bound <= 64 ? 1 : kv_bound <= 128 ? 2 : kv_bound <= 256 ? 4 : 8;
+#define LLMI_ATTR(D_, P_) \
+        if (head_dim == D_ && p == P_) { launch_k(k_attn_r<D_, P_>, dim3(n_head), dim3(512), 0, s, true, true, a, g, kv_bound); return hipGetLastError(); }
+        LLMI_ATTR(128, 1) LLMI_ATTR(128, 2) LLMI_ATTR(128, 4) LLMI_ATTR(128, 8)
+        LLMI_ATTR(64, 1) LLMI_ATTR(64, 2) LLMI_ATTR(64, 4) LLMI_ATTR(64, 8)
+#undef LLMI_ATTR
+        return hipErrorInvalidValue;
+    }
     if (path == 4) {
         if (head_dim == 128 && attn_x_np(128, kv_bound)) return attn_x_g<128>(a, g, n_head_kv, kv_bound, s);
         if (head_dim == 64 && attn_x_np(64, kv_bound)) return attn_x_g<64>(a, g, n_head_kv, kv_bound, s);

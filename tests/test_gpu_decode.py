@@ -178,11 +178,12 @@ def test_profile_kernels_leaves_state(gpu, tiny_models):
     assert np.array_equal(ref.logits(-1), c.logits(-1))
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
 def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
     """Each attention path (1 fused one-WG-per-head, 2 split scores+PV over 16-dim
     slices, 3 long-context two-kernel, 4 one-launch exchange: score tiles handed off
-    as tagged granules) reproduces the oracle's logits bit for bit
+    as tagged granules, 5 register-prefetched one-WG-per-head) reproduces the oracle's
+    logits bit for bit
     (LLMI_ATTN_MODE is read when a context is created)."""
     monkeypatch.setenv("LLMI_ATTN_MODE", str(mode))
     rng = np.random.default_rng(5 + mode)
@@ -192,6 +193,23 @@ def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
         assert g == o
     monkeypatch.setenv("LLMI_ATTN_MODE", "0")
     llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode
+
+
+@pytest.mark.parametrize("mode", ["5", "0"])
+def test_register_attention_all_buckets(gpu, tiny_models, monkeypatch, mode):
+    """k_attn_r (mode 5) over every KV bucket it takes (64..512 positions: 1, 2, 4, 8
+    passes): a 300-token prompt then decode steps to position 330, bit-identical to the
+    oracle; auto (0) for comparison on the same run."""
+    monkeypatch.setenv("LLMI_ATTN_MODE", mode)
+    rng = np.random.default_rng(77)
+    try:
+        for preset in ("tiny-mixed", "tiny-mixed-d128"):
+            prompt = [1] + list(rng.integers(3, 700, 299))
+            worst, g, o, *_ = run_parity(tiny_models[preset], prompt, 30, n_ctx=512, exact=True)
+            assert g == o
+    finally:
+        monkeypatch.setenv("LLMI_ATTN_MODE", "0")
+        llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode
 
 
 def test_golden_greedy16_on_gpu(gpu):
