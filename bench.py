@@ -47,6 +47,8 @@ def parse(argv=None):
     ap.add_argument("--batch-seqs", default="2,4,8",
                     help="continuous-batching leg: sequence counts to time (comma list, '' to skip)")
     ap.add_argument("--batch-steps", type=int, default=64)
+    ap.add_argument("--eager", action="store_true",
+                    help="launch the step kernels one by one instead of replaying HIP graphs (PMC passes)")
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r02"),
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
     return ap.parse_args(argv)
@@ -117,6 +119,18 @@ def timed_decode(engine, dist: Dist, steps: int, warmup: int) -> tuple[float, fl
     return dt, dist.max(dt)
 
 
+def replica_fanout(model, dist: Dist, rccl_unique_id) -> float:
+    """Rank 0's weight arena to every rank's replica: rank 0 makes the
+    RCCL unique id, the torch.distributed group broadcasts it, and every rank joins the
+    one RCCL broadcast over xGMI (llmi_model_fanout).  Returns this rank's seconds."""
+    if dist.world <= 1:
+        return 0.0
+    uid = dist.bcast_bytes(rccl_unique_id() if dist.rank == 0 else None)
+    t = time.perf_counter()
+    model.fanout(uid, dist.world, dist.rank)
+    return time.perf_counter() - t
+
+
 class LlmiEngine:
     """One replica on this rank's GPU driven through the C ABI (libllmi.so)."""
 
@@ -141,14 +155,9 @@ class LlmiEngine:
         t = time.perf_counter()
         self.model = llmi.Model(path, main_gpu=dist.local_rank, no_upload=dist.rank != 0)
         self.load_s = time.perf_counter() - t
-        self.fanout_s = 0.0
-        if dist.world > 1:
-            uid = dist.bcast_bytes(llmi.rccl_unique_id() if dist.rank == 0 else None)
-            t = time.perf_counter()
-            self.model.fanout(uid, dist.world, dist.rank)
-            self.fanout_s = time.perf_counter() - t
+        self.fanout_s = replica_fanout(self.model, dist, llmi.rccl_unique_id)
         n_ctx = ((args.prompt + args.warmup + args.steps + args.profile_steps + 2 + 255) // 256) * 256
-        self.ctx = llmi.Context(self.model, n_ctx=n_ctx)
+        self.ctx = llmi.Context(self.model, n_ctx=n_ctx, use_graphs=not args.eager)
         rng = np.random.default_rng(4 + dist.rank)
         bos = self.model.bos if self.model.bos >= 0 else 1
         self.prompt = [bos] + [int(t) for t in rng.integers(0, min(128000, self.model.n_vocab), args.prompt - 1)]
@@ -373,6 +382,7 @@ def main(argv=None):
             if batched else None,
             "cpu_baseline": cpu,
             "env": knobs,
+            "eager": bool(args.eager),
         }
         print(json.dumps(result), flush=True)
     dist.close()

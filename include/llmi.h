@@ -146,7 +146,7 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
  * n_seq_max >= 2 advance together, one batched step per token (every weight byte read
  * once per step for all of them).  Sequence k starts from first[k] at pos0[k];
  * out[k * n_gen + j] = its token after step j, bit-identical to llmi_generate_greedy of
- * that sequence alone.  Returns n_gen or < 0 on error. */
+ * that sequence alone (n = 1 runs the single-sequence step).  Returns n_gen or < 0 on error. */
 int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const int32_t* seqs, const llama_token* first,
                                    const int32_t* pos0, int32_t n_gen, llama_token* out);
 /* Roofline accounting of the last llama_decode / llmi_generate_greedy call:

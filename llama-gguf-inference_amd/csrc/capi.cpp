@@ -459,6 +459,10 @@ int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const i
         if (pos0[k] < 0 || pos0[k] + n_gen > c.n_ctx) { set_err("llmi_generate_greedy_batch: exceeds n_ctx"); return 1; }
         max_end = std::max(max_end, pos0[k] + n_gen);
     }
+    if (n == 1) {  // one sequence: the single-sequence step (k_matvec path, its own graphs)
+        context_select_seq(c, seqs[0]);
+        return llmi_generate_greedy(ctx, first[0], pos0[0], n_gen, out);
+    }
     (void)hipSetDevice(c.m->device);
     (void)hipGetLastError();
     std::string err;

@@ -14,13 +14,19 @@ module answers that contract:
   Authorization: Bearer <key> required on every route but /health when a key is
   configured (401 otherwise; llama-server's public endpoints are /health and /v1/health)
 
+  GET /health adds per-replica serving metrics: active/queued requests, generated
+  tokens, tok/s over decode time, HBM GB/s of the last decode call (the gateway passes
+  the body through, scripts/gateway.py:360-363)
+
 Decoding is greedy (temperature is accepted and ignored: the north star's workload is
 greedy); `ignore_eos` and `n_predict` follow llama-server.  Every GPU replica is one
-llmi Context driven by one thread; requests take the least-loaded free replica.
+llmi Context with `--parallel` sequences (llama-server's slots) driven by one scheduler
+thread: requests go to the least-loaded replica and are decoded there together, one
+batched step per token for up to 8 sequences (continuous batching).
 
-Text handling is the §8f "next" item: token-id prompts are exact; text is tokenized
-by greedy longest match over the GGUF vocabulary (exact for the synthetic vocab, an
-approximation of BPE/SPM for real vocabularies) and detokenized by piece concatenation.
+Text: the GGUF's own tokenizer (SPM or byte-level BPE from tokenizer.ggml.*) and chat
+template (tokenizer.chat_template, sandboxed Jinja2), llmi/tokenizer.py; streamed text
+holds incomplete UTF-8 sequences back until their last byte.
 """
 from __future__ import annotations
 
@@ -39,9 +45,23 @@ VERSION = "llmi-server 0.1 (libllmi, gfx950)"
 
 
 # --------------------------------------------------------------------------------------
-# vocabulary: detokenize + greedy longest-match tokenizer
+# text codecs: the GGUF's tokenizer + chat template (llmi/tokenizer.py), or the legacy
+# greedy Vocab (kept for stand-in engines)
 # --------------------------------------------------------------------------------------
+class _SimpleStream:
+    def __init__(self, v):
+        self.v = v
+
+    def push(self, t: int) -> str:
+        return self.v.detokenize([t])
+
+    def flush(self) -> str:
+        return ""
+
+
 class Vocab:
+    """Greedy longest match over token texts (stand-in engines and synthetic vocabularies)."""
+
     def __init__(self, pieces: list[str], bos: int, eos: int):
         self.bos, self.eos = bos, eos
         self.text = [self._surface(p) for p in pieces]
@@ -50,6 +70,11 @@ class Vocab:
             if t and not (pieces[i].startswith("<") and pieces[i].endswith(">")):
                 self.by_text.setdefault(t, i)
         self.max_len = max((len(t) for t in self.by_text), default=1)
+        self.eog = {eos}
+
+    @property
+    def n_vocab(self) -> int:
+        return len(self.text)
 
     @staticmethod
     def _surface(p: str) -> str:
@@ -77,10 +102,16 @@ class Vocab:
                 i += 1  # no piece covers this character: skipped
         return out
 
+    def chat_ids(self, messages: list[dict]) -> list[int]:
+        return self.tokenize(chat_prompt(messages, self), add_bos=True)
+
+    def stream(self):
+        return _SimpleStream(self)
+
 
 def chat_prompt(messages: list[dict], vocab: Vocab) -> str:
     """Llama-3 header template when the vocabulary has its special tokens, else a
-    plain role-prefixed transcript ending with the assistant turn."""
+    plain role-prefixed transcript ending with the assistant turn (legacy Vocab only)."""
     if "<|start_header_id|>" in vocab.by_text or any(t == "<|start_header_id|>" for t in vocab.text):
         s = ""
         for m in messages:
@@ -89,73 +120,303 @@ def chat_prompt(messages: list[dict], vocab: Vocab) -> str:
     return "".join(f"{m.get('role', 'user')}: {m.get('content', '')}\n" for m in messages) + "assistant:"
 
 
-# --------------------------------------------------------------------------------------
-# engine: replicas of one GGUF, one llmi Context each
-# --------------------------------------------------------------------------------------
-class Engine:
-    """Owns the GPU replicas.  generate() runs on a free replica (least loaded first)."""
+class TextCodec:
+    """The GGUF's own tokenizer (SPM / byte-level BPE / greedy for synthetic vocabularies)
+    and chat template (tokenizer.chat_template; llama.cpp's chatml default), as
+    llama-server applies them: prompts tokenized with parse_special, BOS added unless the
+    rendered chat already starts with it, generation stops at any end-of-generation token."""
 
-    def __init__(self, path: str, n_ctx: int, n_gpu_layers: int, devices: list[int]):
+    EOG_TEXTS = ("<|eot_id|>", "<|eom_id|>", "<|end_of_text|>", "<|im_end|>", "<|endoftext|>", "</s>", "<|end|>")
+
+    def __init__(self, tok, template: Optional[str]):
+        from . import tokenizer as T
+
+        self.T = T
+        self.tok = tok
+        self.template = template
+        self.bos, self.eos = tok.bos, tok.eos
+        self.bos_text = tok.tokens[tok.bos] if 0 <= tok.bos < tok.n_vocab else ""
+        self.eos_text = tok.tokens[tok.eos] if 0 <= tok.eos < tok.n_vocab else ""
+        self.eog = {tok.eos} | {tok.by_text[t] for t in self.EOG_TEXTS
+                                if t in tok.by_text and tok.types[tok.by_text[t]] == T.CONTROL}
+        self.eog.discard(-1)
+
+    @property
+    def n_vocab(self) -> int:
+        return self.tok.n_vocab
+
+    def tokenize(self, s: str, add_bos: bool = True) -> list[int]:
+        return self.tok.tokenize(s, add_special=add_bos, parse_special=True)
+
+    def detokenize(self, ids: Iterable[int]) -> str:
+        return self.tok.detokenize(ids)
+
+    def chat_ids(self, messages: list[dict]) -> list[int]:
+        for m in messages:
+            if not isinstance(m, dict) or not isinstance(m.get("content", ""), str):
+                raise ValueError("each message must be an object with string 'content'")
+        try:
+            text = self.T.render_chat(self.template, messages, self.bos_text, self.eos_text)
+        except self.T.TemplateError as e:
+            raise ValueError(str(e)) from e
+        add_bos = not (self.bos_text and text.startswith(self.bos_text))
+        return self.tokenize(text, add_bos=add_bos)
+
+    def stream(self):
+        return self.tok.stream()
+
+
+# --------------------------------------------------------------------------------------
+# engine: replicas of one GGUF; each replica = one llmi Context with `slots` sequences,
+# driven by one scheduler thread (continuous batching, SURVEY.md §8f row 3)
+# --------------------------------------------------------------------------------------
+class Request:
+    """One generation: prompt ids in, token lists out through `q` (None terminates)."""
+
+    def __init__(self, prompt: list[int], max_tokens: int, ignore_eos: bool):
+        self.prompt, self.max_tokens, self.ignore_eos = list(prompt), max_tokens, ignore_eos
+        self.out: list[int] = []
+        self.q: "queue.Queue" = queue.Queue()
+        self.finish: Optional[str] = None
+        self.error: Optional[str] = None
+        self.t_submit = time.perf_counter()
+        self.t_first: Optional[float] = None
+        self.replica = -1
+        # scheduler state
+        self.seq = -1
+        self.last = -1
+        self.pos = 0
+
+    def emit(self, toks: list[int]) -> None:
+        if toks:
+            if self.t_first is None:
+                self.t_first = time.perf_counter()
+            self.out += toks
+            self.q.put(list(toks))
+
+    def done(self, finish: str) -> None:
+        self.finish = finish
+        self.q.put(None)
+
+    def fail(self, err: str) -> None:
+        self.error = err
+        self.q.put(None)
+
+
+class Replica:
+    """One context (device) serving up to `slots` requests at once.  Its thread admits
+    queued requests into free sequences (prefill through llama_decode with their seq id)
+    and advances all active ones together with llmi_generate_greedy_batch (one weight
+    stream per step for up to 8 sequences), `chunk` tokens per call."""
+
+    def __init__(self, idx: int, ctx, slots: int, eog: set, chunk: int, n_ctx: int, device: int = 0):
+        self.idx, self.ctx, self.slots, self.eog, self.chunk, self.n_ctx = idx, ctx, slots, eog, chunk, n_ctx
+        self.device = device
+        self.pending: "queue.Queue[Request]" = queue.Queue()
+        self.active: list[Request] = []
+        self.free = list(range(slots))
+        self.lock = threading.Lock()
+        self.n_queued = 0
+        self.tokens = 0          # generated tokens served
+        self.busy_s = 0.0        # time inside decode calls
+        self.last_gbps = 0.0     # HBM GB/s of the last decode call (algorithmic bytes / device time)
+        self.requests = 0
+        self.stop = False
+        self.th = threading.Thread(target=self._run, name=f"llmi-replica-{idx}", daemon=True)
+        self.th.start()
+
+    def load(self) -> int:
+        with self.lock:
+            return self.n_queued + len(self.active)
+
+    def submit(self, r: Request) -> None:
+        with self.lock:
+            self.n_queued += 1
+            self.requests += 1
+        r.replica = self.idx
+        self.pending.put(r)
+
+    def _stats(self) -> None:
+        try:
+            b, us = self.ctx.stats()
+            if us > 0:
+                self.last_gbps = b / (us * 1e-6) / 1e9
+        except Exception:
+            pass
+
+    # -- admission: prefill into a free sequence, emit the first token
+    def _admit(self, r: Request) -> None:
+        with self.lock:
+            self.n_queued -= 1
+        seq = self.free.pop()
+        try:
+            c = self.ctx
+            c.seq_rm(seq)
+            max_tokens = r.max_tokens
+            if len(r.prompt) + max_tokens > self.n_ctx:
+                max_tokens = max(0, self.n_ctx - len(r.prompt))
+            r.max_tokens = max_tokens
+            if not r.prompt or max_tokens <= 0:
+                self.free.append(seq)
+                r.done("length")
+                return
+            t0 = time.perf_counter()
+            rc = c.decode(r.prompt, seq=[seq] * len(r.prompt))
+            self.busy_s += time.perf_counter() - t0
+            if rc != 0:
+                raise RuntimeError(f"llama_decode returned {rc}")
+            first = c.greedy(-1)
+            r.seq, r.pos = seq, len(r.prompt)
+            if self._take(r, [first]):
+                self.free.append(seq)
+            else:
+                r.last = first
+                self.active.append(r)
+        except Exception as e:  # this request fails; the replica keeps serving
+            self.free.append(seq)
+            r.fail(str(e))
+
+    def _take(self, r: Request, toks: list[int]) -> bool:
+        """Emit generated tokens up to EOS / max_tokens; True when the request is done."""
+        emit = []
+        for t in toks:
+            if t in self.eog and not r.ignore_eos:
+                r.emit(emit)
+                self.tokens += len(emit)
+                r.done("stop")
+                return True
+            emit.append(t)
+            if len(r.out) + len(emit) >= r.max_tokens:
+                break
+        r.emit(emit)
+        self.tokens += len(emit)
+        if len(r.out) >= r.max_tokens:
+            r.done("length")
+            return True
+        return False
+
+    def _step(self) -> None:
+        batch = self.active[:8]
+        k = max(1, min(self.chunk, min(r.max_tokens - len(r.out) for r in batch)))
+        c = self.ctx
+        t0 = time.perf_counter()
+        try:
+            outs = c.generate_greedy_batch([r.seq for r in batch], [r.last for r in batch], [r.pos for r in batch], k)
+        except Exception:
+            # not batchable here (e.g. a context past the batched attention's bound):
+            # one sequence at a time, same results
+            outs = [c.generate_greedy_batch([r.seq], [r.last], [r.pos], k)[0] for r in batch]
+        self.busy_s += time.perf_counter() - t0
+        self._stats()
+        done = []
+        for r, toks in zip(batch, outs):
+            r.pos += k
+            r.last = toks[-1]
+            if self._take(r, toks):
+                done.append(r)
+        for r in done:
+            self.active.remove(r)
+            self.free.append(r.seq)
+        # rotate so more than 8 active requests share the steps fairly
+        if len(self.active) > 8:
+            self.active = self.active[len(batch):] + self.active[:len(batch)]
+
+    def _run(self) -> None:
+        while not self.stop:
+            try:
+                while self.free and (not self.pending.empty() or not self.active):
+                    r = self.pending.get(timeout=0.5 if not self.active else None) if not self.active else \
+                        self.pending.get_nowait()
+                    self._admit(r)
+            except queue.Empty:
+                pass
+            if not self.active:
+                continue
+            try:
+                self._step()
+            except Exception as e:  # the context failed: every active request fails
+                for r in self.active:
+                    r.fail(str(e))
+                    self.free.append(r.seq)
+                self.active = []
+
+
+class Engine:
+    """Owns the GPU replicas.  Requests go to the least-loaded replica (active + queued;
+    ties to the lowest index) and are served there with continuous batching."""
+
+    def __init__(self, path: str, n_ctx: int, n_gpu_layers: int, devices: list[int], slots: int = 4,
+                 chunk: int = 8, contexts=None):
         self.path, self.n_ctx, self.ngl, self.devices = path, n_ctx, n_gpu_layers, devices
+        self.slots, self.chunk = max(1, slots), max(1, chunk)
         self.ready = False
         self.error: Optional[str] = None
-        self.vocab: Optional[Vocab] = None
+        self.vocab = None
         self.model_id = os.path.basename(path)
-        self._free: "queue.Queue[int]" = queue.Queue()
-        self._ctxs = []
+        self.replicas: list[Replica] = []
         self._models = []
+        self._contexts = contexts  # test hook: (list of context-like objects, codec)
+        self.t_ready: Optional[float] = None
+        self.load_s = 0.0
 
     def load(self) -> None:
+        t0 = time.perf_counter()
         try:
-            import llmi
+            if self._contexts is not None:
+                ctxs, self.vocab = self._contexts
+            else:
+                import llmi
+                from . import tokenizer as T
 
-            m0 = llmi.Model(self.path, n_gpu_layers=self.ngl, main_gpu=self.devices[0])
-            models = [m0] + (m0.replicate(self.devices[1:]) if len(self.devices) > 1 else [])
-            self._models = models
-            self._ctxs = [llmi.Context(m, n_ctx=self.n_ctx) for m in models]
-            self.n_ctx = self._ctxs[0].n_ctx
-            self.vocab = Vocab([m0.token_text(i) for i in range(m0.n_vocab)], m0.bos, m0.eos)
-            for i in range(len(self._ctxs)):
-                self._free.put(i)
+                m0 = llmi.Model(self.path, n_gpu_layers=self.ngl, main_gpu=self.devices[0])
+                models = [m0] + (m0.replicate(self.devices[1:]) if len(self.devices) > 1 else [])
+                self._models = models
+                ctxs = [llmi.Context(m, n_ctx=self.n_ctx, n_seq=self.slots) for m in models]
+                self.n_ctx = ctxs[0].n_ctx
+                meta = T.read_gguf_meta(self.path)
+                tok = T.make_tokenizer(meta, tokens=[m0.token_text(i) for i in range(m0.n_vocab)],
+                                       bos=m0.bos, eos=m0.eos) if not meta.get("tokenizer.ggml.tokens") \
+                    else T.make_tokenizer(meta)
+                self.vocab = TextCodec(tok, meta.get("tokenizer.chat_template"))
+            eog = getattr(self.vocab, "eog", {self.vocab.eos})
+            self.replicas = [Replica(i, c, self.slots, eog, self.chunk, self.n_ctx,
+                                     self.devices[i] if i < len(self.devices) else i) for i, c in enumerate(ctxs)]
+            self.load_s = time.perf_counter() - t0
+            self.t_ready = time.perf_counter()
             self.ready = True
         except Exception as e:  # reported by /health
             self.error = str(e)
 
+    def submit(self, prompt: list[int], max_tokens: int, ignore_eos: bool) -> Request:
+        r = Request(prompt, max_tokens, ignore_eos)
+        rep = min(self.replicas, key=lambda x: (x.load(), x.idx))
+        rep.submit(r)
+        return r
+
     def generate(self, prompt: list[int], max_tokens: int, ignore_eos: bool, on_tokens: Callable[[list[int]], None],
                  chunk: int = 8) -> tuple[list[int], str]:
-        i = self._free.get()
-        try:
-            c = self._ctxs[i]
-            c.kv_clear()
-            if len(prompt) + max_tokens > self.n_ctx:
-                max_tokens = max(0, self.n_ctx - len(prompt))
-            if not prompt or max_tokens <= 0:
-                return [], "length"
-            rc = c.decode(prompt)
-            if rc != 0:
-                raise RuntimeError(f"llama_decode returned {rc}")
-            # generate_greedy(t, pos, k) decodes t at pos and returns the k tokens after it
-            out: list[int] = []
-            pending, pos = [c.greedy(-1)], len(prompt)
-            while True:
-                emit = []
-                for t in pending:
-                    if t == self.vocab.eos and not ignore_eos:
-                        if emit:
-                            on_tokens(emit)
-                        return out + emit, "stop"
-                    emit.append(t)
-                    if len(out) + len(emit) >= max_tokens:
-                        break
-                out += emit
-                on_tokens(emit)
-                if len(out) >= max_tokens:
-                    return out, "length"
-                k = min(chunk, max_tokens - len(out))
-                pending = c.generate_greedy(out[-1], pos, k)
-                pos += k
-        finally:
-            self._free.put(i)
+        r = self.submit(prompt, max_tokens, ignore_eos)
+        while True:
+            toks = r.q.get()
+            if toks is None:
+                break
+            on_tokens(toks)
+        if r.error:
+            raise RuntimeError(r.error)
+        return r.out, r.finish or "length"
+
+    def health(self) -> dict:
+        """Per-replica serving metrics for /health (kept well under the gateway's 4 KB read,
+        scripts/gateway.py:350)."""
+        up = max(1e-9, time.perf_counter() - (self.t_ready or time.perf_counter()))
+        reps = []
+        for r in self.replicas:
+            reps.append({"id": r.idx, "device": r.device, "active": len(r.active), "queued": r.n_queued,
+                         "tokens": r.tokens, "tok_s": round(r.tokens / max(r.busy_s, 1e-9), 1) if r.tokens else 0.0,
+                         "hbm_gbps": round(r.last_gbps, 1), "busy": round(r.busy_s / up, 3)})
+        busy = sum(len(r.active) for r in self.replicas)
+        return {"slots_idle": self.slots * len(self.replicas) - busy, "slots_processing": busy,
+                "load_s": round(self.load_s, 2), "replicas": reps[:16]}
 
 
 # --------------------------------------------------------------------------------------
@@ -210,7 +471,10 @@ class Handler(BaseHTTPRequestHandler):
                 return self._send_json(500, {"status": "error", "error": eng.error})
             if not eng.ready:
                 return self._send_json(503, _error(503, "Loading model", "unavailable_error"))
-            return self._send_json(200, {"status": "ok"})
+            h = {"status": "ok"}
+            if hasattr(eng, "health"):
+                h.update(eng.health())
+            return self._send_json(200, h)
         if not self._authorized(route):
             return self._send_json(401, _error(401, "Invalid API Key", "authentication_error"))
         if route == "/v1/models":
@@ -237,12 +501,12 @@ class Handler(BaseHTTPRequestHandler):
                 msgs = req.get("messages")
                 if not isinstance(msgs, list) or not msgs:
                     raise ValueError("'messages' must be a non-empty list")
-                prompt = v.tokenize(chat_prompt(msgs, v), add_bos=True)
+                prompt = v.chat_ids(msgs)
             else:
                 p = req.get("prompt", "")
                 if isinstance(p, list) and all(isinstance(t, int) for t in p):
                     prompt = list(p)
-                    if not prompt or not (0 <= min(prompt) and max(prompt) < len(v.text)):
+                    if not prompt or not (0 <= min(prompt) and max(prompt) < v.n_vocab):
                         raise ValueError("token ids out of range")
                 elif isinstance(p, str):
                     prompt = v.tokenize(p, add_bos=True)
@@ -288,15 +552,24 @@ class Handler(BaseHTTPRequestHandler):
             event({"id": rid, "object": cobj, "created": created, "model": eng.model_id,
                    "choices": [{"index": 0, "delta": {"role": "assistant"}, "finish_reason": None}]})
 
+        sd = v.stream()
+
         def on_tokens(ts: list[int]) -> None:
             for t in ts:
-                piece = v.detokenize([t])
+                piece = sd.push(t)
+                if not piece:
+                    continue  # an incomplete UTF-8 sequence: held until its last byte
                 ch = ({"index": 0, "delta": {"content": piece}, "finish_reason": None} if chat
                       else {"index": 0, "text": piece, "logprobs": None, "finish_reason": None})
                 event({"id": rid, "object": cobj, "created": created, "model": eng.model_id, "choices": [ch]})
 
         try:
             ids, finish = eng.generate(prompt, max_tokens, ignore_eos, on_tokens, chunk=4)
+            tail = sd.flush()
+            if tail:
+                ch = ({"index": 0, "delta": {"content": tail}, "finish_reason": None} if chat
+                      else {"index": 0, "text": tail, "logprobs": None, "finish_reason": None})
+                event({"id": rid, "object": cobj, "created": created, "model": eng.model_id, "choices": [ch]})
             last = ({"index": 0, "delta": {}, "finish_reason": finish} if chat
                     else {"index": 0, "text": "", "logprobs": None, "finish_reason": finish})
             event({"id": rid, "object": cobj, "created": created, "model": eng.model_id, "choices": [last],
@@ -333,6 +606,9 @@ def parse_args(argv=None):
     ap.add_argument("-t", "--threads", type=int, default=0)
     ap.add_argument("--replicas", type=int, default=int(os.environ.get("LLMI_REPLICAS", "1")),
                     help="GPU replicas (devices 0..N-1), one context each")
+    ap.add_argument("-np", "--parallel", type=int, default=int(os.environ.get("LLMI_SLOTS", "4")),
+                    help="sequences (slots) per replica decoded together (continuous batching)")
+    ap.add_argument("--decode-chunk", type=int, default=8, help="tokens per batched decode call")
     args, extra = ap.parse_known_args(argv)
     return args, extra
 
@@ -350,7 +626,8 @@ def main(argv=None) -> int:
     key = args.api_key
     if args.api_key_file:
         key = open(args.api_key_file).read().strip()
-    eng = Engine(args.model, args.ctx_size, args.ngl, list(range(max(1, args.replicas))))
+    eng = Engine(args.model, args.ctx_size, args.ngl, list(range(max(1, args.replicas))), slots=args.parallel,
+                 chunk=args.decode_chunk)
     srv = make_server(eng, args.host, args.port, key)
     threading.Thread(target=eng.load, daemon=True).start()
     print(f"[llmi-server] listening on {args.host}:{args.port}", file=sys.stderr, flush=True)

@@ -70,3 +70,53 @@ def test_two_rank_timed_region_gloo():
     assert max0 >= 0.02  # the slower rank's 20 ms dominates the job time
     assert runs0 == runs1 == [("warmup", 3), ("run", 7)]
     assert uid0 == uid1 == b"unique-id-from-rank0"
+
+
+class StubModel:
+    """Records the llmi_model_fanout call a replica makes (no GPU, no RCCL)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def fanout(self, uid, nranks, rank):
+        self.calls.append((uid, nranks, rank))
+
+
+def _fanout_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import bench
+
+    d = bench.Dist("gloo")
+    made = []
+
+    def uid_fn():
+        made.append(rank)
+        return b"rccl-uid-" + bytes([7] * 8)
+
+    m = StubModel()
+    s = bench.replica_fanout(m, d, uid_fn)
+    q.put((rank, made, m.calls, s >= 0))
+    d.close()
+
+
+@pytest.mark.timeout(120)
+def test_replica_fanout_call_sequence_gloo():
+    """bench.py's weight fan-out at world size 2: only rank 0 creates the RCCL unique id,
+    both ranks receive the same bytes over the process group and call llmi_model_fanout
+    once with (uid, nranks=2, their rank)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fanout_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (r0, made0, calls0, ok0), (r1, made1, calls1, ok1) = res
+    assert made0 == [0] and made1 == []
+    uid = b"rccl-uid-" + bytes([7] * 8)
+    assert calls0 == [(uid, 2, 0)] and calls1 == [(uid, 2, 1)] and ok0 and ok1
