@@ -371,6 +371,7 @@ def main(argv=None):
             "kernels": {k2: {"us": round(v["us"], 3), "GBps": round(v["GBps"], 1),
                              "per_step": v["launches_per_step"]} for k2, v in prof.items()},
             "load_s": round(eng.load_s, 2),
+            "upload_s": round(eng.model.upload_s, 3),
             "prefill": {"tokens": args.prompt, "path": "mfma" if eng.model.prefill_supported else "decode-steps",
                         "ttft_ms": round(eng.prefill_warm_s * 1e3, 2),
                         "tok_per_s": round(args.prompt / max(eng.prefill_warm_s, 1e-9), 1)},

@@ -149,6 +149,9 @@ int32_t llmi_generate_greedy(struct llama_context* ctx, llama_token first, int32
  * that sequence alone (n = 1 runs the single-sequence step).  Returns n_gen or < 0 on error. */
 int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const int32_t* seqs, const llama_token* first,
                                    const int32_t* pos0, int32_t n_gen, llama_token* out);
+/* seconds the weight upload took in llama_model_load_from_file (chunked pinned H2D,
+ * double-buffered against the on-device repack; file reads included) */
+double llmi_model_upload_s(const struct llama_model* model);
 /* Roofline accounting of the last llama_decode / llmi_generate_greedy call:
  * algorithmic HBM bytes it streamed and its device time in microseconds. */
 void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec);
@@ -214,7 +217,9 @@ int64_t llmi_synth_write_gguf(const char* path, const char* preset, uint64_t see
 
 /* Debug taps of the last decode step (host copy, synchronous): 1 residual x after the
  * last layer (n_embd), 2 roped q (n_head*head_dim), 3 attention output, 4 SwiGLU output
- * (n_ff) — the last layer's.  Mirrors the oracle's or_tap.  0 on success. */
+ * (n_ff) — the last layer's.  Mirrors the oracle's or_tap.  7/8: the last layer's raw
+ * f16 K/V cache.  11-15: the last batched step's buffers, 8 slot rows each: x, q,
+ * attention output, SwiGLU output, logits.  0 on success. */
 int32_t llmi_debug_tap(struct llama_context* ctx, int32_t which, float* out);
 
 /* ---------- kernel-level entry points (tests and microbenchmarks) ----------

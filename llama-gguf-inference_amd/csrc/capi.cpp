@@ -633,6 +633,15 @@ int32_t llmi_debug_tap(struct llama_context* ctx, int32_t which, float* out) {
         if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
         return 0;
     }
+    if (which >= 11 && which <= 15) {  // batched-step buffers, kMaxBatch rows each
+        const float* b = which == 11 ? c.bx : which == 12 ? c.bq : which == 13 ? c.batt : which == 14 ? c.bh : c.blogits;
+        const size_t per = which == 11 ? hp.n_embd : which == 14 ? hp.n_ff : which == 15 ? hp.n_vocab
+                                                                                     : (size_t)hp.n_head * hp.head_dim;
+        if (!b) { set_err("llmi_debug_tap: no batched step ran"); return -1; }
+        hipError_t e = hipMemcpy(out, b, per * kMaxBatch * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+        return 0;
+    }
     const float* src = which == 1 ? c.x : which == 2 ? c.q : which == 3 ? c.att : which == 4 ? c.h : nullptr;
     const size_t n = which == 1 ? hp.n_embd : which == 4 ? hp.n_ff : (size_t)hp.n_head * hp.head_dim;
     if (!src) { set_err("llmi_debug_tap: unknown tap"); return -1; }
@@ -642,6 +651,8 @@ int32_t llmi_debug_tap(struct llama_context* ctx, int32_t which, float* out) {
     if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
     return 0;
 }
+
+double llmi_model_upload_s(const struct llama_model* model) { return model ? model->m.upload_s : -1.0; }
 
 int32_t llmi_prefill_supported(const struct llama_model* model) {
     return model && prefill_supported(model->m) ? 1 : 0;

@@ -7,6 +7,10 @@
 // on the device (argmax key -> k_embed), so greedy generation needs no host round trip.
 #include "engine.h"
 
+#include <chrono>
+#include <cstring>
+#include <thread>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -211,28 +215,102 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
         add(p + "attn_v.weight", &L.wv); add(p + "attn_output.weight", &L.wo); add(p + "ffn_norm.weight", &L.ffn_norm);
         add(p + "ffn_gate.weight", &L.wg); add(p + "ffn_up.weight", &L.wu); add(p + "ffn_down.weight", &L.wd);
     }
-    size_t stage_bytes = 0;
-    for (const Item& it : items)
-        if (needs_repack(it.m->type)) stage_bytes = std::max(stage_bytes, it.t->nbytes);
-    uint8_t* stage = nullptr;
-    if (stage_bytes) HIPC(hipMalloc(&stage, stage_bytes));
+    // Chunked, double-buffered upload: host threads copy a chunk of whole rows from the
+    // mmap into a pinned buffer (page faults of a cold file taken in parallel) while the
+    // previous chunk's DMA and on-device repack run on the upload stream.
+    constexpr size_t kChunk = 64u << 20;
+    uint8_t* pin[2] = {nullptr, nullptr};
+    uint8_t* dstage[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    hipStream_t us = nullptr;
     bool ok = true;
+    auto cleanup = [&]() {
+        if (us) (void)hipStreamSynchronize(us);
+        for (int k = 0; k < 2; ++k) {
+            if (pin[k]) (void)hipHostFree(pin[k]);
+            if (dstage[k]) (void)hipFree(dstage[k]);
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+        }
+        if (us) (void)hipStreamDestroy(us);
+    };
+    hipError_t e = hipStreamCreateWithFlags(&us, hipStreamNonBlocking);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+        e = hipHostMalloc((void**)&pin[k], kChunk, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(&dstage[k], kChunk);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        err = "upload buffers: " + hip_err(e);
+        cleanup();
+        return false;
+    }
+    const unsigned nthr = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    auto host_copy = [&](uint8_t* dst, const uint8_t* src, size_t n) {
+        if (n < (4u << 20) || nthr == 1) { memcpy(dst, src, n); return; }
+        std::vector<std::thread> th;
+        const size_t per = (n + nthr - 1) / nthr;
+        for (unsigned t = 0; t < nthr; ++t) {
+            const size_t o = t * per;
+            if (o >= n) break;
+            th.emplace_back([=] { memcpy(dst + o, src + o, std::min(per, n - o)); });
+        }
+        for (auto& x : th) x.join();
+    };
+    int slot = 0;
+    auto next_slot = [&]() -> hipError_t {
+        if (used[slot]) {
+            hipError_t e2 = hipEventSynchronize(ev[slot]);
+            if (e2 != hipSuccess) return e2;
+        }
+        return hipSuccess;
+    };
+    const auto t_up = std::chrono::steady_clock::now();
     for (const Item& it : items) {
-        hipError_t e;
-        if (needs_repack(it.m->type)) {
-            e = hipMemcpy(stage, it.t->data, it.t->nbytes, hipMemcpyHostToDevice);
-            if (e == hipSuccess) {
-                const int64_t nblk = it.m->rows * (it.m->cols / block_elems(it.m->type));
-                e = launch_repack(it.m->type, stage, M.arena + it.m->off_a, M.arena + it.m->off_h, M.arena + it.m->off_s,
-                                  M.arena + it.m->off_d, nblk, it.m->cols, nullptr);
-                if (e == hipSuccess) e = hipDeviceSynchronize();
+        const DevMat& m = *it.m;
+        const uint8_t* src = (const uint8_t*)it.t->data;
+        e = hipSuccess;
+        if (needs_repack(m.type)) {
+            const int64_t bpr = m.cols / block_elems(m.type);  // blocks per row
+            const size_t row_raw = (size_t)bpr * block_bytes(m.type);
+            const int64_t rows_per = std::max<int64_t>(1, (int64_t)(kChunk / row_raw));
+            const size_t pa = m.type == T_Q8_0 ? 32 : 128, ph = m.type == T_Q5_K ? 32 : m.type == T_Q6_K ? 64 : 0,
+                         ps = m.type == T_Q8_0 ? 0 : 16, pd = (m.type == T_Q6_K || m.type == T_Q8_0) ? 2 : 0;
+            for (int64_t r0 = 0; r0 < m.rows && e == hipSuccess; r0 += rows_per) {
+                const int64_t nr = std::min(rows_per, m.rows - r0);
+                const size_t n = (size_t)nr * row_raw;
+                const size_t b0 = (size_t)r0 * bpr;
+                e = next_slot();
+                if (e != hipSuccess) break;
+                host_copy(pin[slot], src + (size_t)r0 * row_raw, n);
+                e = hipMemcpyAsync(dstage[slot], pin[slot], n, hipMemcpyHostToDevice, us);
+                if (e == hipSuccess)
+                    e = launch_repack(m.type, dstage[slot], M.arena + m.off_a + b0 * pa, M.arena + m.off_h + b0 * ph,
+                                      M.arena + m.off_s + b0 * ps, M.arena + m.off_d + b0 * pd, nr * bpr, m.cols, us);
+                if (e == hipSuccess) e = hipEventRecord(ev[slot], us);
+                used[slot] = true;
+                slot ^= 1;
             }
         } else {
-            e = hipMemcpy(M.arena + it.m->off_a, it.t->data, it.t->nbytes, hipMemcpyHostToDevice);
+            for (size_t o = 0; o < it.t->nbytes && e == hipSuccess; o += kChunk) {
+                const size_t n = std::min(kChunk, it.t->nbytes - o);
+                e = next_slot();
+                if (e != hipSuccess) break;
+                host_copy(pin[slot], src + o, n);
+                e = hipMemcpyAsync(M.arena + m.off_a + o, pin[slot], n, hipMemcpyHostToDevice, us);
+                if (e == hipSuccess) e = hipEventRecord(ev[slot], us);
+                used[slot] = true;
+                slot ^= 1;
+            }
         }
         if (e != hipSuccess) { err = "upload of " + it.t->name + ": " + hip_err(e); ok = false; break; }
     }
-    if (stage) (void)hipFree(stage);
+    if (ok) {
+        e = hipStreamSynchronize(us);
+        if (e != hipSuccess) { err = "upload: " + hip_err(e); ok = false; }
+    }
+    M.upload_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_up).count();
+    cleanup();
     return ok;
 }
 
@@ -351,10 +429,10 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, int n_seq, Context& c, s
         HIPC(hipMalloc(&c.step_mv, tab2.size() * sizeof(MVArgs)));
         HIPC(hipMemcpy(c.step_mv, tab2.data(), tab2.size() * sizeof(MVArgs), hipMemcpyHostToDevice));
         HIPC(hipMalloc(&c.step_bar, kStepBarWords * 4));
-        HIPC(hipMemset(c.step_bar, 0, kStepBarWords * 4));
+        HIPC(hipMemsetAsync(c.step_bar, 0, kStepBarWords * 4, c.stream));
 #if defined(LLMI_EXP_TRACE)
         HIPC(hipMalloc(&c.step_trace, (size_t)1024 * 512 * 2 * 8));
-        HIPC(hipMemset(c.step_trace, 0, (size_t)1024 * 512 * 2 * 8));
+        HIPC(hipMemsetAsync(c.step_trace, 0, (size_t)1024 * 512 * 2 * 8, c.stream));
 #endif
     }
     context_clear(c);
@@ -653,12 +731,15 @@ static bool balloc(Context& c, std::string& err) {
     HIPC(hipMalloc(&c.bscores, B * attn_scratch_floats(hp.n_head, c.n_ctx) * 4));
     HIPC(hipMalloc(&c.btpos, B * 4));
     HIPC(hipMalloc(&c.btseq, B * 4));
-    // padded slots read these rows: finite (zeros); their positions 0
-    HIPC(hipMemset(c.bx, 0, B * E * 4));
-    HIPC(hipMemset(c.batt, 0, B * QD * 4));
-    HIPC(hipMemset(c.bh, 0, B * F * 4));
-    HIPC(hipMemset(c.btpos, 0, B * 4));
-    HIPC(hipMemset(c.btseq, 0, B * 4));
+    // padded slots read these rows: finite (zeros); their positions 0.  On the context
+    // stream (a null-stream memset is not ordered with it: it could land after the slot
+    // map upload that follows and point every slot at sequence 0)
+    HIPC(hipMemsetAsync(c.bx, 0, B * E * 4, c.stream));
+    HIPC(hipMemsetAsync(c.batt, 0, B * QD * 4, c.stream));
+    HIPC(hipMemsetAsync(c.bh, 0, B * F * 4, c.stream));
+    HIPC(hipMemsetAsync(c.btpos, 0, B * 4, c.stream));
+    HIPC(hipMemsetAsync(c.btseq, 0, B * 4, c.stream));
+    HIPC(hipStreamSynchronize(c.stream));
     return true;
 }
 

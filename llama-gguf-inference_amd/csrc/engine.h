@@ -38,6 +38,7 @@ struct Model {
     std::vector<std::string> vocab;
     int bos = -1, eos = -1;
     std::vector<float> rope_freq_host;  // rope_freqs.weight, if present
+    double upload_s = 0;                 // chunked pinned upload + repack time (model_load)
     ~Model();
 };
 

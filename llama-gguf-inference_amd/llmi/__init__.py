@@ -108,6 +108,11 @@ class Model:
         s = lib().llama_vocab_get_text(self._vocab, int(t))
         return s.decode("utf-8", "replace") if s is not None else ""
 
+    @property
+    def upload_s(self) -> float:
+        """Seconds of the weight upload (chunked pinned H2D + on-device repack)."""
+        return float(lib().llmi_model_upload_s(self._h))
+
     def bytes_per_token(self, n_kv: int) -> float:
         return float(lib().llmi_bytes_per_token(self._h, int(n_kv)))
 

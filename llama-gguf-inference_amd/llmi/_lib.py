@@ -91,6 +91,7 @@ SIGNATURES = {
                                                C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_int32)]),
     "llama_kv_self_seq_rm": (C.c_bool, [_P, C.c_int32, C.c_int32, C.c_int32]),
     "llmi_seq_pos_max": (C.c_int32, [_P, C.c_int32]),
+    "llmi_model_upload_s": (C.c_double, [_P]),
     "llmi_last_step_stats": (None, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "llmi_test_option": (C.c_int32, [C.c_char_p, C.c_int32]),
     "llmi_step_path": (C.c_int32, [_P, C.c_int32]),
