@@ -184,6 +184,97 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     return best;
 }
 
+// 3-deep register ring (experiment build -DLLMI_MV_RING=1; off by default): the same
+// items in the same order with the same arithmetic as mv_body (bit-identical, tested),
+// but each wave keeps the NEXT TWO items' weights in flight while it reduces one.
+// Buffers A, B, C are reloaded in place (the loop is unrolled by 3), so no register copy
+// forces a wait on a load just issued.  Measured (profiles/r02/matvec_ring.md): output
+// head 80.0 -> 76-77 us, gate+up 17.0 -> 16.8 us, but QKV 5.8 -> 8.3 and attn_output
+// 5.4 -> 7.6 us (the dummy ring loads of single-round launches delay their prologue);
+// end to end 604 -> 553 tok/s.  Per-wave stamps show the matvec is bound by the
+// dispatch ramp (waves start over 1.9 us), the 2.4 us prologue and a 3 us exit spread,
+// not by the in-flight depth.
+#ifndef LLMI_MV_RING
+#define LLMI_MV_RING 0
+#endif
+template <int ACT, bool NORM, int EPI, int T, int NP>
+__device__ __forceinline__ unsigned long long mv_body3(const MVArgs& A, const Lds& L, int p0, int G, int pbeg, int pend) {
+    int pos = 0;
+    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
+    unsigned long long best = 0;
+    const int lane = threadIdx.x & 63;
+    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+    const uint8_t* xb = (const uint8_t*)A.x;
+    const RowPtr dummy{xb, xb, xb, xb};
+    ProRegs<NORM, NP> R;
+    mv_prologue_issue<NORM, NP>(A, R);  // activation loads first (see mv_body)
+    if (pend - pbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // load cursor (pl, jl) and compute cursor (pc, jc); pstop = first pair of this wave
+    // that is not of type T (it and the pairs after it go to the generic loop below)
+    int pl = p0, jl = 0, pc = p0, jc = 0, pstop = pend;
+    float acc_a = 0.f, acc_b = 0.f;
+#define MV_LOAD(X)                                                                     \
+    {                                                                                  \
+        PairRows<T> rows_;                                                             \
+        rows_.a = rows_.b = dummy;                                                     \
+        int jj_ = 0;                                                                   \
+        if (pl < pstop) {                                                              \
+            const PairRef r_ = pair_ref<EPI>(A, pl);                                   \
+            if (r_.type == T) {                                                        \
+                rows_ = pair_rows<T>(r_, A.cols);                                      \
+                jj_ = jl;                                                              \
+            } else {                                                                   \
+                pstop = pl;                                                            \
+            }                                                                          \
+        }                                                                              \
+        X = load_item<T>(rows_, lane + 64 * jj_, nch);                                 \
+        if (pl < pstop) {                                                              \
+            if (++jl == NJ) { jl = 0; pl += G; }                                       \
+        }                                                                              \
+    }
+#define MV_STEP(X)                                                                     \
+    {                                                                                  \
+        if (pc < pstop) {                                                              \
+            const int ch_ = lane + 64 * jc;                                            \
+            const int chc_ = ch_ < nch ? ch_ : nch - 1;                                \
+            const Act act_ = load_act<ACT>(L, chc_, nch);                              \
+            const float va_ = dot_chunk<T>(X.a, act_, chc_), vb_ = dot_chunk<T>(X.b, act_, chc_); \
+            acc_a += ch_ < nch ? va_ : 0.f;                                            \
+            acc_b += ch_ < nch ? vb_ : 0.f;                                            \
+            if (jc == NJ - 1) {                                                        \
+                epilogue<EPI>(A, pair_ref<EPI>(A, pc), pc, reduce_pair(acc_a, acc_b), pos, best); \
+                acc_a = acc_b = 0.f;                                                   \
+                jc = 0;                                                                \
+                pc += G;                                                               \
+            } else {                                                                   \
+                ++jc;                                                                  \
+            }                                                                          \
+        }                                                                              \
+        MV_LOAD(X);                                                                    \
+    }
+    PairRaw<T> bA, bB, bC;
+    MV_LOAD(bA);  // the first three items in flight during the prologue
+    MV_LOAD(bB);
+    MV_LOAD(bC);
+    mv_prologue_finish<ACT, NORM, NP>(A, L, R);
+    __syncthreads();
+    while (pc < pstop) {
+        MV_STEP(bA);
+        MV_STEP(bB);
+        MV_STEP(bC);
+    }
+#undef MV_STEP
+#undef MV_LOAD
+    // pairs of other types (mixed-type segments): one at a time
+    for (int p = pc; p < pend; p += G) {
+        const PairRef r = pair_ref<EPI>(A, p);
+        const float a = generic_row_any<ACT>(r.sa.type, r.sa, r.ra, A.cols, L);
+        const float b = r.vb ? generic_row_any<ACT>(r.sb.type, r.sb, r.rb, A.cols, L) : 0.f;
+        epilogue<EPI>(A, r, p, reduce_pair(a, b), pos, best);
+    }
+    return best;
+}
+
 // A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
 // split by workgroup: workgroups [0, split_wgs) run the pairs of type T, the rest the
 // pairs of type T2, each group pipelined in its own type (no divergence in a workgroup).
@@ -194,16 +285,22 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     unsigned long long best;
+#if LLMI_MV_RING && !defined(LLMI_EXP_TRACE)
+#define MV_BODY mv_body3
+#else
+#define MV_BODY mv_body
+#endif
     if constexpr (T2 == T) {
-        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.npairs);
+        best = MV_BODY<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.npairs);
     } else {
         if ((int)blockIdx.x < A.split_wgs)
-            best = mv_body<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
+            best = MV_BODY<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
                                                   A.split_pairs);
         else
-            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, A.split_pairs + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
+            best = MV_BODY<ACT, NORM, EPI, T2, NP>(A, L, A.split_pairs + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
                                                    (gridDim.x - A.split_wgs) * kMVWaves, A.split_pairs, A.npairs);
     }
+#undef MV_BODY
     if constexpr (EPI == EPI_LOGITS) {
         // workgroup max of the waves' keys, then one atomic into this workgroup's slot
         const int cur_pos = A.st->pos;
