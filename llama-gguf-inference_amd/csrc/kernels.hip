@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
 }
 
 // K-split matvec for rows longer than one 64-chunk item (NJ = ceil(cols/4096) >= 2:
-// ffn_down, 70B-wide inputs).  A workgroup's 4 waves form 4/KS pair slots of KS waves;
+// ffn_down, 70B-wide inputs).  A workgroup's 16 waves form 16/KS pair slots of KS waves;
 // the waves of a slot split the pair's items (wave sub takes items sub, sub+KS, ...),
 // so every item of the first pair is in flight during the prologue, instead of one
 // item per wave with the rest fetched serially after it.  Per-lane item values go to

@@ -108,8 +108,9 @@ def gpu_matvec(qtype, raw, rows, cols, x, nw=None, eps=1e-5):
     return yd.cpu().numpy()
 
 
-# cols > 4096 take the K-split kernel (KS=2 for 2-3 items per row, KS=4 for >= 4;
-# 28672 also exercises the prologue's tail loop beyond the register-held sub-blocks)
+# cols > 4096 take the K-split kernel (KS=2 below 6 items per row, KS=1 from 6 items when
+# its part buffer fits LDS; 28672 also exercises the prologue's tail loop beyond the
+# register-held sub-blocks)
 SHAPES = [(2, 256), (7, 512), (130, 1024), (1024, 4096), (333, 14336), (4096, 4096), (64, 8192), (130, 5632),
           (5, 28672), (2048, 14336)]
 
@@ -126,6 +127,24 @@ def test_matvec_vs_oracle(gpu, qtype, rows, cols):
     tol = 1e-5 * float(np.abs(ref).max())
     err = float(np.abs(got - ref).max())
     assert err <= tol, f"max |err| vs generic order {err:.3g} > {tol:.3g}"
+    po.set_dot_order(po.DEVICE_ORDER)
+    try:
+        exact = po.matvec(qtype, raw, rows, cols, x)
+    finally:
+        po.set_dot_order(po.GENERIC)
+    assert np.array_equal(got, exact), "not bit-exact vs device-order oracle"
+
+
+@pytest.mark.parametrize("qtype", [12, 14], ids=["q4_K", "q6_K"])
+def test_matvec_ks1_multi_round(gpu, qtype):
+    """K-split width 1 past one round: 4224 pairs of 28672-column rows exceed the 16 pair
+    slots x 256 resident workgroups, so slots take a second round and the double-buffered
+    part buffer (buf ^= 1) is reused; bit-exact vs the device-order oracle."""
+    rows, cols = 8448, 28672
+    rng = np.random.default_rng(91 + qtype)
+    raw = random_blocks(qtype, rows, cols, rng)
+    x = rng.standard_normal(cols).astype(np.float32)
+    got = gpu_matvec(qtype, raw, rows, cols, x)
     po.set_dot_order(po.DEVICE_ORDER)
     try:
         exact = po.matvec(qtype, raw, rows, cols, x)
