@@ -318,20 +318,42 @@ static hipError_t mvn_epi(const MVArgs& a, int epi, int nt, int mb, hipStream_t 
     }
 }
 
-hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
-    if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0 || nt < 1 || nt > kMaxBatch) return hipErrorInvalidValue;
-    const int t = a.seg[0].type;
-    for (int i = 1; i < a.nseg; ++i)
-        if (a.seg[i].type != t) return hipErrorInvalidValue;  // callers group segments by type
-    // the padded token count (3 -> 4, 5..7 -> 8) reads rows of the batch buffers past nt:
-    // the caller keeps kMaxBatch rows allocated and finite
-    switch (t) {
+static hipError_t mvn_type(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
+    switch (a.seg[0].type) {
         case T_Q4_K: return mvn_epi<0, T_Q4_K>(a, epi, nt, max_blocks, s);
         case T_Q5_K: return mvn_epi<0, T_Q5_K>(a, epi, nt, max_blocks, s);
         case T_Q6_K: return mvn_epi<0, T_Q6_K>(a, epi, nt, max_blocks, s);
         case T_Q8_0: return mvn_epi<1, T_Q8_0>(a, epi, nt, max_blocks, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+static int mvn_pad(int nt) { return nt <= 1 ? 1 : nt == 2 ? 2 : nt <= 4 ? 4 : 8; }
+
+hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
+    if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0 || nt < 1 || nt > kMaxBatch) return hipErrorInvalidValue;
+    const int t = a.seg[0].type;
+    for (int i = 1; i < a.nseg; ++i)
+        if (a.seg[i].type != t) return hipErrorInvalidValue;  // callers group segments by type
+    // the padded token count (3 -> 4, 5..7 -> 8) reads rows of the batch buffers past nt:
+    // the caller keeps kMaxBatch rows allocated and finite.  Rows too long for NT LDS
+    // images (70B ffn_down: 28672 columns, 32 KB per token) run as several launches of
+    // fewer tokens each (each streams the weights again; results per token unchanged).
+    const int act = t == T_Q8_0 ? 1 : 0;
+    int group = mvn_pad(nt);
+    while (group > 1 && mvn_lds_bytes(act, a.cols, group) > 160 * 1024) group >>= 1;
+    if (mvn_lds_bytes(act, a.cols, group) > 160 * 1024) return hipErrorInvalidValue;
+    for (int t0 = 0; t0 < nt; t0 += group) {
+        MVArgs b = a;
+        const int n = nt - t0 < group ? nt - t0 : group;
+        b.x += (size_t)t0 * a.x_stride;
+        b.y += (size_t)t0 * a.y_stride;
+        if (a.tpos) b.tpos += t0;
+        if (a.tseq) b.tseq += t0;
+        const hipError_t e = mvn_type(b, epi, n, max_blocks, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s) {

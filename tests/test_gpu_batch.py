@@ -10,7 +10,8 @@ sequences at different positions (different KV lengths and RoPE angles in one st
 a step whose sequences straddle a 256-position KV bucket, llama_decode batches with
 several seq_ids (single-token sequences batched, longer ones prefilled), sequence
 removal and reuse, and the real widths (Llama-3-8B Q4_K_M, Mistral Q5_K_M / Q6_K,
-TinyLlama Q8_0 shapes at 2 layers).
+TinyLlama Q8_0, Llama-3-70B Q4_K_M shapes at 2 layers; 70B's 28672-column ffn_down runs
+as two 4-token launches, its LDS images of 8 tokens exceeding 160 KB).
 """
 from __future__ import annotations
 
@@ -164,7 +165,7 @@ def test_mixed_gate_up_types_fall_back(gpu, tiny_models):
 
 
 @pytest.mark.parametrize("preset,n_vocab", [("llama3-8b-q4km", 0), ("mistral7b-q5km", 0), ("mistral7b-q6k", 0),
-                                            ("tinyllama-q8_0", 0)])
+                                            ("tinyllama-q8_0", 0), ("llama3-70b-q4km", 32000)])
 def test_batched_real_widths(gpu, synth_dir, preset, n_vocab):
     path = str(synth_dir / f"{preset}-batch-L2.gguf")
     llmi.write_synthetic_gguf(path, preset, seed=11, n_layer=2, n_vocab=n_vocab)
@@ -175,3 +176,26 @@ def test_batched_real_widths(gpu, synth_dir, preset, n_vocab):
     for s in range(8):
         assert np.array_equal(got_lg[s], want_lg[s]), f"seq {s}: prompt logits differ"
         assert got[s] == want[s], f"seq {s}"
+
+
+def test_batched_past_attention_lds_bound_falls_back(gpu, synth_dir):
+    """TinyLlama shapes (GQA 8): the batched attention holds 8 heads x kv_bound scores in
+    LDS (<= 4096 positions).  Past it llmi_generate_greedy_batch reports the limit and
+    llama_decode runs those sequences one at a time — same tokens as single decode."""
+    path = str(synth_dir / "tinyllama-q8_0-batch-L2.gguf")
+    llmi.write_synthetic_gguf(path, "tinyllama-q8_0", seed=11, n_layer=2)
+    rng = np.random.default_rng(8)
+    prompts = [[1] + [int(t) for t in rng.integers(3, 30000, 4150)], [1] + [int(t) for t in rng.integers(3, 30000, 20)]]
+    want, want_lg = _single_reference(path, prompts, 3, 4352)
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=4352, n_seq=2)
+    firsts = []
+    for s, p in enumerate(prompts):
+        assert c.decode(p, seq=[s] * len(p)) == 0
+        assert np.array_equal(c.logits(-1), want_lg[s])
+        firsts.append(c.greedy(-1))
+    with pytest.raises(llmi.LlmiError):
+        c.generate_greedy_batch([0, 1], firsts, [len(p) for p in prompts], 2)
+    # llama_decode with one token per sequence: not batchable here, still exact
+    assert c.decode(firsts, pos=[len(p) for p in prompts], seq=[0, 1], logits_all=True) == 0
+    assert [c.greedy(0), c.greedy(1)] == [want[0][1], want[1][1]]
