@@ -120,6 +120,56 @@ __device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t) {
     return B;
 }
 
+// v of lane L ^ O for any values (not only butterfly-uniform ones): DPP quad_perm for 1
+// and 2, ds_swizzle bit mode within 32 lanes for 4 and 8, permlane swaps for 16 and 32
+template <int O>
+__device__ __forceinline__ float xor_any(float v) {
+    if constexpr (O == 1 || O == 2 || O == 16 || O == 32) return xor_partner<O>(v);
+    else return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (O << 10)));
+}
+
+// One reduce-scatter level over lane bit O: each lane keeps half of its H values (the
+// lower half when bit O is clear) and adds the partner's copy of the same half.  The
+// additions are the butterfly's (block sums of the two O-halves), so every value's
+// total is the single-token matvec's tree exactly; only which lane holds it changes.
+template <int O, int H>
+__device__ __forceinline__ void scatter_level(float (&v)[16]) {
+    const bool hi = (threadIdx.x & O) != 0;
+#pragma unroll
+    for (int j = 0; j < H / 2; ++j) {
+        const float send = hi ? v[j] : v[j + H / 2];
+        const float keep = hi ? v[j + H / 2] : v[j];
+        v[j] = keep + xor_any<O>(send);
+    }
+}
+
+// 2*NT per-lane partial sums (v[2t] row a, v[2t+1] row b of token t) -> the full 64-lane
+// sum of value idx(lane) in every lane: reduce-scatter over the low log2(2NT) lane bits,
+// then the butterfly over the rest.  idx = sum over scatter levels of (bit set ? H/2 : 0).
+template <int NT>
+__device__ __forceinline__ float reduce_scatter(float (&v)[16]) {
+    scatter_level<1, 2 * NT>(v);
+    if constexpr (NT >= 2) scatter_level<2, NT>(v);
+    if constexpr (NT >= 4) scatter_level<4, NT / 2>(v);
+    if constexpr (NT >= 8) scatter_level<8, NT / 4>(v);
+    float x = v[0];
+    if constexpr (NT < 2) x += xor_any<2>(x);
+    if constexpr (NT < 4) x += xor_any<4>(x);
+    if constexpr (NT < 8) x += xor_any<8>(x);
+    x += xor_any<16>(x);
+    x += xor_any<32>(x);
+    return x;
+}
+// the value index a lane holds after reduce_scatter<NT>: bits read from the lane from
+// the first scatter level (weight NT) down to the last (weight 1)
+template <int NT>
+__device__ __forceinline__ int scatter_idx(int lane) {
+    int idx = 0;
+#pragma unroll
+    for (int k = 0, w = NT; w >= 1; ++k, w >>= 1) idx += ((lane >> k) & 1) ? w : 0;
+    return idx;
+}
+
 }  // namespace
 
 template <int ACT, bool NORM, int EPI, int T, int NT>
@@ -131,12 +181,14 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
     const int G = gridDim.x * kBW;
-    int pos[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) pos[t] = A.tpos ? A.tpos[t] : 0;
-    unsigned long long best[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) best[t] = 0;
+    // after the reduce-scatter, lane L holds row (idx & 1) of token idx >> 1; lanes
+    // 0..15 holding row a run their token's epilogue (one token per lane)
+    constexpr int RB = NT;  // lane bit (as a mask) that selects row a / row b
+    const int my_idx = scatter_idx<NT>(lane);
+    const int my_t = my_idx >> 1;
+    const bool ep_lane = lane < 2 * NT && (my_idx & 1) == 0;
+    const int my_pos = A.tpos ? A.tpos[my_t < NT ? my_t : 0] : 0;
+    unsigned long long best = 0;
     bprologue<ACT, NORM, NT>(A, smem, img, red);
 
     int p = blockIdx.x * kBW + wave;
@@ -173,11 +225,18 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
                 acc_b[t] += ch < nch ? vb : 0.f;
             }
             if (j == NJ - 1) {
+                float v[16];
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
-                    const MVArgs B = token_view(A, t);
-                    epilogue<EPI>(B, r, p, reduce_pair(acc_a[t], acc_b[t]), pos[t], best[t]);
+                    v[2 * t] = acc_a[t];
+                    v[2 * t + 1] = acc_b[t];
                     acc_a[t] = acc_b[t] = 0.f;
+                }
+                const float mine = reduce_scatter<NT>(v);
+                const float other = xor_any<RB>(mine);  // the same token's other row
+                if (ep_lane) {
+                    const MVArgs B = token_view(A, my_t);
+                    epilogue<EPI, false, MVArgs, true>(B, r, p, PairSum{mine, other}, my_pos, best);
                 }
             }
             if (!has_next) break;
@@ -189,25 +248,21 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
         }
     }
     if constexpr (EPI == EPI_LOGITS) {
-        // per token: workgroup max of the waves' keys, one atomic into the slot of its
-        // sequence's StepState; workgroup 0 advances the sequence's next position
-        unsigned long long* wred = (unsigned long long*)red;
-        for (int t = 0; t < NT; ++t) {
-            __syncthreads();
-            unsigned long long bt = 0;
-#pragma unroll
-            for (int u = 0; u < NT; ++u)
-                if (u == t) bt = best[u];
-            if (lane == 0) wred[wave] = bt;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                unsigned long long b = wred[0];
-                for (int w = 1; w < kBW; ++w) b = wred[w] > b ? wred[w] : b;
-                StepState* st = A.st + (A.tseq ? A.tseq[t] : 0);
-                const int pt = A.tpos[t];
-                if (b) atomicMax(&st->key[pt & 1][blockIdx.x % kArgSlots], b);
-                if (blockIdx.x == 0) st->pos_next = pt + 1;
-            }
+        // per token: workgroup max of the waves' keys (each held by the token's epilogue
+        // lane), one atomic into the slot of its sequence's StepState; workgroup 0
+        // advances the sequence's next position
+        unsigned long long* wred = (unsigned long long*)red;  // [kBW][NT]
+        __syncthreads();
+        if (ep_lane) wred[wave * NT + my_t] = best;
+        __syncthreads();
+        if ((int)threadIdx.x < NT) {
+            const int t = threadIdx.x;
+            unsigned long long b = wred[t];
+            for (int w = 1; w < kBW; ++w) b = wred[w * NT + t] > b ? wred[w * NT + t] : b;
+            StepState* st = A.st + (A.tseq ? A.tseq[t] : 0);
+            const int pt = A.tpos[t];
+            if (b) atomicMax(&st->key[pt & 1][blockIdx.x % kArgSlots], b);
+            if (blockIdx.x == 0) st->pos_next = pt + 1;
         }
     }
 }

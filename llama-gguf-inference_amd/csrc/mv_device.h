@@ -645,12 +645,13 @@ __device__ __forceinline__ void st_u16(uint16_t* p, uint16_t v) {
 }
 
 // Epilogue of one finished pair (every lane holds both row sums; lane 0 writes).
-template <int EPI, bool WT = false, class MA>
+// (ANY_LANE: the calling lane writes; the batched matvec runs one token per lane)
+template <int EPI, bool WT = false, class MA, bool ANY_LANE = false>
 __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, PairSum v, int pos,
                                          unsigned long long& best) {
     const int lane = threadIdx.x & 63;
     const float va = v.a, vb = v.b;
-    if (lane != 0) return;
+    if (!ANY_LANE && lane != 0) return;
     if constexpr (EPI == EPI_STORE) {
         st_f32<WT>(A.y + r.sa.row0 + r.ra, va);
         if (r.vb) st_f32<WT>(A.y + r.sa.row0 + r.rb, vb);
