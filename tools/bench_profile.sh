@@ -11,6 +11,7 @@ mkdir -p "$OUT"; export TMPDIR=/tmp
 ARGS="--preset $PRESET --no-cpu-baseline --batch-seqs= --steps 100 --warmup 16 --profile-steps 0"
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/stats" -o run -- \
     python3 "$ROOT/bench.py" $ARGS > "$ROOT/$OUT/stats.json" 2> "$ROOT/$OUT/stats.err" ) || exit $?
+# counters on eager launches (graph replays under --pmc crashed the profiler's host side)
 ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$ROOT/$OUT/pmc" -o run -- \
-    python3 "$ROOT/bench.py" $ARGS > "$ROOT/$OUT/pmc.json" 2> "$ROOT/$OUT/pmc.err" ) || exit $?
+    python3 "$ROOT/bench.py" $ARGS --eager --steps 20 > "$ROOT/$OUT/pmc.json" 2> "$ROOT/$OUT/pmc.err" ) || exit $?
 python3 tools/make_traffic.py "$OUT" "$PRESET"
