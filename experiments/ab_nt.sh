@@ -9,7 +9,7 @@ for lib in libllmi libllmi_nt0; do
 done
 for r in 1 2; do
   for lib in libllmi libllmi_nt0; do
-    LLMI_LIB=$L/$lib.so timeout -k 10 300 python3 bench.py --no-cpu-baseline --batch-seqs 8 \
+    LLMI_LIB=$L/$lib.so timeout -k 10 300 python3 bench.py --no-cpu-baseline --batch-seqs "" --steps 256 \
       > "$OUT/bench_${lib}_$r.json" 2> "$OUT/bench_${lib}_$r.err" || exit $?
   done
 done
