@@ -18,6 +18,7 @@ constexpr int kMVWaves = kMVThreads / 64;
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
 constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
 constexpr int kXAttnMaxKV = 1024;
+constexpr int kDimAttnMaxKV = 1024;  // dim-split one-launch attention (k_attn_d) up to this KV bound
 constexpr int kRegAttnMaxKV = 512;  // register-prefetched one-launch attention (k_attn_r) up to this KV bound  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
@@ -191,6 +192,7 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
 // (group, 16-dim slice) workgroups), 3 two-kernel long-context path, 4 one-launch
 // exchange (k_attn_x: scores tiles + granule hand-off + PV, kv_bound <= kXAttnMaxKV)
 int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim);
+int attn_d_slices(int n_head, int head_dim);
 // arm (or with nullptrs disarm) per-op kernel timing events for this thread's launches
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);

@@ -1134,6 +1134,139 @@ __global__ __launch_bounds__(512) void k_attn_r(AttnArgs a, int G, int kvb) {
     LLMI_ATT_STAMP(0, 3)
 }
 
+// Dim-split one-launch attention (path 6, kv_bound <= 64*P <= 1024): H*S workgroups of
+// 512 threads.  Workgroup b serves query head h of KV group g = b % HK and the DS = D/S
+// output dims of slice b / H.  Each workgroup recomputes its head's scores and softmax
+// in full (no cross-workgroup hand-off) and splits only the PV, so a head's K rows are
+// read by S workgroups and its V rows once in total.  Placement: the G*S workgroups of a
+// KV group have equal b % HK, i.e. one XCD under round-robin dispatch (HK = 8), so a K
+// row comes from HBM once and from that XCD's L2 for the others (default cache policy
+// on K and V for that reason).  Every global load is issued at entry, as in k_attn_r;
+// numerics are k_attn_r's (exact f16 products summed in double, p = f16(e * (float)(1 /
+// sum)), double PV); the per-position work and the PV lane split differ only in how the
+// exact double sums are associated.
+template <int D, int P, int S>
+__global__ __launch_bounds__(512) void k_attn_d(AttnArgs a, int G, int HK, int kvb) {
+    constexpr int DQ = D / 8;                    // score dims per lane
+    constexpr int DS = D / S;                    // output dims of this workgroup
+    constexpr int SLV = 512 / DS;                // PV lanes per output dim (<= 64)
+    constexpr int NVL = (64 * P + 8 * SLV - 1) / (8 * SLV);  // 16-B V loads per lane
+    static_assert(SLV <= 64 && (SLV & (SLV - 1)) == 0, "PV lanes of a dim stay in one wave");
+    __shared__ __attribute__((aligned(16))) float sp[64 * P + 8];
+    __shared__ float redm[8];
+    __shared__ double reds[8];
+    LLMI_ATT_STAMP(0, 0)
+    const int b = blockIdx.x, H = HK * G;
+    const int g = b % HK, h = g * G + (b / HK) % G, ds = b / H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qd = tid & 7, pp = tid >> 3;
+    // 1. every load up front: position, q slice, the K rows of all passes, the V slice
+    const int pos = a.st->pos;
+    float4 qv[DQ / 4];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; ++i) qv[i] = *(const float4*)(a.q + (size_t)h * D + qd * DQ + 4 * i);
+    u32x4 kv[P][DQ / 8];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int t = min(64 * p + pp, kvb - 1);
+        const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = *(const u32x4*)(kr + 8 * i);
+    }
+    const int d = ds * DS + tid / SLV, sl = tid % SLV;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    u32x4 vv[NVL];
+#pragma unroll
+    for (int u = 0; u < NVL; ++u) vv[u] = *(const u32x4*)(vr + min(8 * sl + 8 * SLV * u, kvb - 8));
+    const int n_kv = pos + 1;
+    // 2. scores (q rounded to f16 as upstream's KQ mul_mat does; f16 x f16 products exact)
+    double q[DQ];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; ++i) {
+        q[4 * i + 0] = (double)h2f(f2h(qv[i].x)); q[4 * i + 1] = (double)h2f(f2h(qv[i].y));
+        q[4 * i + 2] = (double)h2f(f2h(qv[i].z)); q[4 * i + 3] = (double)h2f(f2h(qv[i].w));
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                acc = __builtin_fma((double)h2f((uint16_t)kv[p][i][jj]), q[8 * i + 2 * jj], acc);
+                acc = __builtin_fma((double)h2f((uint16_t)(kv[p][i][jj] >> 16)), q[8 * i + 2 * jj + 1], acc);
+            }
+        acc += xor_partner_d<1>(acc);
+        acc += xor_partner_d<2>(acc);
+        acc += xor_partner_d<4>(acc);
+        const int t = 64 * p + pp;
+        const float sc = (float)acc * a.scale;
+        if (qd == 0) sp[t] = sc;
+        if (t < n_kv) m = fmaxf(m, sc);
+    }
+    LLMI_ATT_STAMP(0, 1)
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
+    __syncthreads();
+    float mx = redm[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) mx = fmaxf(mx, redm[w]);
+    // 3. softmax: thread t owns positions t, t + 512
+    constexpr int NE = (64 * P + 511) / 512;
+    float e[NE];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int t = tid + 512 * k;
+        e[k] = 0.f;
+        if (t < n_kv && t < 64 * P) {
+            e[k] = llmi_expf(sp[t] - mx);
+            s += (double)e[k];
+        }
+    }
+    s = wave_sum_d(s);
+    if (lane == 0) reds[wave] = s;
+    __syncthreads();
+    double tot = reds[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) tot += reds[w];
+    const float inv = (float)(1.0 / tot);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int t = tid + 512 * k;
+        if (t < 64 * P) sp[t] = t < n_kv ? h2f(f2h(e[k] * inv)) : 0.f;
+    }
+    __syncthreads();
+    LLMI_ATT_STAMP(0, 2)
+    // 4. PV of this workgroup's DS dims: lane sl covers positions 8*sl + 8*SLV*u + j
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NVL; ++u) {
+        const int tb = 8 * sl + 8 * SLV * u;
+        if (tb < n_kv) {
+            const float4 p0 = *(const float4*)(sp + tb), p1 = *(const float4*)(sp + tb + 4);
+            const float pr[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float f = h2f((uint16_t)(vv[u][j >> 1] >> (16 * (j & 1))));
+                const double v = tb + j < n_kv ? (double)f : 0.0;
+                if (j & 1) acc1 = __builtin_fma(v, (double)pr[j], acc1);
+                else acc0 = __builtin_fma(v, (double)pr[j], acc0);
+            }
+        }
+    }
+    double acc = acc0 + acc1;
+    if constexpr (SLV >= 2) acc += xor_partner_d<1>(acc);
+    if constexpr (SLV >= 4) acc += xor_partner_d<2>(acc);
+    if constexpr (SLV >= 8) acc += xor_partner_d<4>(acc);
+    if constexpr (SLV >= 16) acc += xor_partner_d<8>(acc);
+    if constexpr (SLV >= 32) acc += xor_partner_d<16>(acc);
+    if constexpr (SLV >= 64) acc += xor_partner_d<32>(acc);
+    if (sl == 0) a.out[(size_t)h * D + d] = (float)acc;
+    LLMI_ATT_STAMP(0, 3)
+}
+
 // ----------------------------------------------------------------------------------
 // Step entry: choose the token, advance pos, dequantize its embedding row
 // (upstream ggml_get_rows + dequantize_row_*; bit-exact).
@@ -1547,8 +1680,20 @@ int g_xspin_limit = kXSpinLimit;        // k_attn_x bounded-wait polls before it
 int g_xtag_skew = 0;                    // k_attn_x consumers expect tag + skew (1: never matches)
 int pf_max_kv() { return g_pf_max_kv; }
 
+// dim slices of k_attn_d: about 256 workgroups (one per CU), 2..8, at least 8 dims each
+static int g_attn_s = 0;  // LLMI_ATTN_S (A/B only): force 2, 4 or 8 slices
+int attn_d_slices(int n_head, int head_dim) {
+    const int s = g_attn_s ? g_attn_s : n_head >= 128 ? 2 : n_head >= 64 ? 4 : 8;
+    return head_dim / s >= 8 ? s : head_dim / 8;
+}
+
 static int g_attn_mode = 0;  // 0 auto, 1 fused, 2 split, 3 two-kernel, 4 exchange (experiments: LLMI_ATTN_MODE)
-void set_attn_mode(int mode) { g_attn_mode = mode; }
+void set_attn_mode(int mode) {
+    g_attn_mode = mode;
+    const char* e = getenv("LLMI_ATTN_S");
+    const int v = e ? atoi(e) : 0;
+    g_attn_s = (v == 2 || v == 4 || v == 8) ? v : 0;
+}
 int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     const int g = n_head / n_head_kv;
     const bool split_ok = (size_t)g * kv_bound * 4 <= kSplitAttnMaxLds;
@@ -1556,6 +1701,7 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     (void)n_head;
     if (g_attn_mode == 4 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
     if (g_attn_mode == 5 && kv_bound <= kRegAttnMaxKV) return 5;
+    if (g_attn_mode == 6 && kv_bound <= kDimAttnMaxKV) return 6;
     if (g_attn_mode == 1 && fused_ok) return 1;
     if (g_attn_mode == 2 && split_ok) return 2;
     if (g_attn_mode == 3) return 3;
@@ -1567,7 +1713,11 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     //   G=8, D=64 (TinyLlama): fused <= 2048 (128: 6.2 vs 9.7; 1280: 15.9 vs 20.9)
     //   G=8, D=64: register-prefetched k_attn_r <= 256 (5.5-5.9 vs 6.2-6.7 fused); for
     //              D=128 it loses to fused (one CU pulls 64 KB+ per head: per-CU bandwidth)
+    //   k_attn_d (dim-split, scores recomputed per slice, round 2) beats all of the above
+    //   up to 1024 positions on every shape (tools/attnbench.py, profiles/r02/attn_dim_split.md):
+    //   G=4 D=128 128: 5.2 vs 8.1 fused, 512: 7.0 vs 10.0 exchange, 1024: 10.8 vs 12.7 split
     if (g_attn_mode == 0) {
+        if (g <= 8 && kv_bound <= kDimAttnMaxKV && attn_d_slices(n_head, head_dim) >= 2) return 6;
         if (g == 8 && head_dim == 64 && kv_bound <= 256) return 5;
         if (g == 8 && fused_ok && kv_bound <= (head_dim == 64 ? 2048 : 640)) return 1;
         if (g == 4 && fused_ok && kv_bound <= 256) return 1;
@@ -1593,6 +1743,18 @@ hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int h
         LLMI_ATTR(128, 1) LLMI_ATTR(128, 2) LLMI_ATTR(128, 4) LLMI_ATTR(128, 8)
         LLMI_ATTR(64, 1) LLMI_ATTR(64, 2) LLMI_ATTR(64, 4) LLMI_ATTR(64, 8)
 #undef LLMI_ATTR
+        return hipErrorInvalidValue;
+    }
+    if (path == 6) {
+        const int p = kv_bound <= 64 ? 1 : kv_bound <= 128 ? 2 : kv_bound <= 256 ? 4 : kv_bound <= 512 ? 8
+                    : kv_bound <= 768 ? 12 : 16;
+        const int sdim = attn_d_slices(n_head, head_dim);
+#define LLMI_ATTD(D_, P_, S_) \
+        if (head_dim == D_ && p == P_ && sdim == S_) { launch_k(k_attn_d<D_, P_, S_>, dim3(n_head * S_), dim3(512), 0, s, true, true, a, g, n_head_kv, kv_bound); return hipGetLastError(); }
+#define LLMI_ATTD_P(D_, S_) LLMI_ATTD(D_, 1, S_) LLMI_ATTD(D_, 2, S_) LLMI_ATTD(D_, 4, S_) LLMI_ATTD(D_, 8, S_) LLMI_ATTD(D_, 12, S_) LLMI_ATTD(D_, 16, S_)
+        LLMI_ATTD_P(128, 2) LLMI_ATTD_P(128, 4) LLMI_ATTD_P(128, 8) LLMI_ATTD_P(64, 2) LLMI_ATTD_P(64, 4) LLMI_ATTD_P(64, 8)
+#undef LLMI_ATTD_P
+#undef LLMI_ATTD
         return hipErrorInvalidValue;
     }
     if (path == 4) {

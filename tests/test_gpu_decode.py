@@ -178,11 +178,12 @@ def test_profile_kernels_leaves_state(gpu, tiny_models):
     assert np.array_equal(ref.logits(-1), c.logits(-1))
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5, 6])
 def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
     """Each attention path (1 fused one-WG-per-head, 2 split scores+PV over 16-dim
     slices, 3 long-context two-kernel, 4 one-launch exchange: score tiles handed off
-    as tagged granules, 5 register-prefetched one-WG-per-head) reproduces the oracle's
+    as tagged granules, 5 register-prefetched one-WG-per-head, 6 dim-split one-launch:
+    scores recomputed per output-dim slice) reproduces the oracle's
     logits bit for bit
     (LLMI_ATTN_MODE is read when a context is created)."""
     monkeypatch.setenv("LLMI_ATTN_MODE", str(mode))
@@ -195,11 +196,11 @@ def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
     llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode
 
 
-@pytest.mark.parametrize("mode", ["5", "0"])
+@pytest.mark.parametrize("mode", ["5", "6", "0"])
 def test_register_attention_all_buckets(gpu, tiny_models, monkeypatch, mode):
-    """k_attn_r (mode 5) over every KV bucket it takes (64..512 positions: 1, 2, 4, 8
-    passes): a 300-token prompt then decode steps to position 330, bit-identical to the
-    oracle; auto (0) for comparison on the same run."""
+    """k_attn_r (mode 5) / k_attn_d (mode 6) over the KV buckets up to 512 positions (1,
+    2, 4, 8 passes): a 300-token prompt then decode steps to position 330, bit-identical
+    to the oracle; auto (0) for comparison on the same run."""
     monkeypatch.setenv("LLMI_ATTN_MODE", mode)
     rng = np.random.default_rng(77)
     try:
@@ -207,6 +208,22 @@ def test_register_attention_all_buckets(gpu, tiny_models, monkeypatch, mode):
             prompt = [1] + list(rng.integers(3, 700, 299))
             worst, g, o, *_ = run_parity(tiny_models[preset], prompt, 30, n_ctx=512, exact=True)
             assert g == o
+    finally:
+        monkeypatch.setenv("LLMI_ATTN_MODE", "0")
+        llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode
+
+
+@pytest.mark.parametrize("preset", ["tiny-mixed", "tiny-mixed-d128"])
+def test_dim_split_attention_long_buckets(gpu, tiny_models, monkeypatch, preset):
+    """k_attn_d (mode 6) in its 768- and 1024-position buckets (12 and 16 K passes, two
+    softmax positions per thread): a 700-token prompt, decode steps across position 768
+    to 800, bit-identical to the oracle."""
+    monkeypatch.setenv("LLMI_ATTN_MODE", "6")
+    rng = np.random.default_rng(78)
+    try:
+        prompt = [1] + list(rng.integers(3, 700, 699))
+        worst, g, o, *_ = run_parity(tiny_models[preset], prompt, 100, n_ctx=1024, exact=True)
+        assert g == o
     finally:
         monkeypatch.setenv("LLMI_ATTN_MODE", "0")
         llmi.Context(llmi.Model(tiny_models["tiny-mixed"]), n_ctx=32).close()  # reset the global mode
