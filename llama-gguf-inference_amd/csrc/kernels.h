@@ -26,10 +26,16 @@ extern int g_pf_attn_simple, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
 int pf_max_kv();  // llama_decode hands prompt runs reaching past this KV length to decode steps
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
 // + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
-inline size_t attn_gran_off(int n_head, int n_ctx) {
+__host__ __device__ inline size_t attn_gran_off(int n_head, int n_ctx) {
     return ((size_t)n_head * n_ctx + (size_t)n_head * (n_ctx / 32 + 1) + 3) & ~(size_t)3;
 }
-inline size_t attn_scratch_floats(int n_head, int n_ctx) { return attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV + 4; }
+// + the long-context path's (k_attl_*) per-256-position tile sums [H][n_ctx/256] and PV
+// partials [H][n_ctx/256][<= 128 dims], both double
+constexpr int kLongTile = 256;
+__host__ __device__ inline size_t attn_long_off(int n_head, int n_ctx) { return attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV + 4; }
+inline size_t attn_scratch_floats(int n_head, int n_ctx) {
+    return attn_long_off(n_head, n_ctx) + 2 * (size_t)n_head * ((n_ctx + kLongTile - 1) / kLongTile) * 129;
+}
 
 enum Epi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_LOGITS = 4,
                  EPI_SWIGLU_UP = 5 };  // prefill: y = silu(y) * up (gate/up of different types)

@@ -1134,6 +1134,245 @@ __global__ __launch_bounds__(512) void k_attn_r(AttnArgs a, int G, int kvb) {
     LLMI_ATT_STAMP(0, 3)
 }
 
+// Long-context attention (path 7): every phase spread over position tiles so the K and V
+// streams use the whole chip, in four launches (a softmax over a whole row cannot be
+// formed piecewise bit-exactly: p = f16(e / sum) needs the row's max and sum first).
+//   1. k_attn_scores8 (split path phase 1): scores of the G heads per 32-position tile,
+//      K read once, plus per-tile maxima
+//   2. k_attl_exp    grid (H, tiles of kLongTile): row max from the tile maxima, e =
+//      expf(s - max) in place, the tile's double sum of e
+//   3. k_attl_pv     grid (HK, tiles): row sum = the tile sums in fixed order, p =
+//      f16(e * (float)(1 / sum)), PV of the tile's positions for all D dims of the G
+//      heads (V read once), double partial per (head, tile, dim)
+//   4. k_attl_sum    grid H: out = the partials summed over tiles in fixed order
+// The double sums are exact in practice, as on every other path (tests compare with the
+// oracle and the other paths bit for bit).
+__device__ __forceinline__ double* attl_tsum(const AttnArgs& a, int n_head) {
+    return (double*)(a.scores + attn_long_off(n_head, a.n_ctx));
+}
+__device__ __forceinline__ double* attl_part(const AttnArgs& a, int n_head) {
+    return attl_tsum(a, n_head) + (size_t)n_head * ((a.n_ctx + kLongTile - 1) / kLongTile);
+}
+
+// phase 1 for long contexts: k_attn_scores8 with NP 32-position passes per workgroup (the
+// q staging amortised over 32*NP positions, every K load issued at entry); same per-pass
+// arithmetic, scores and tile maxima as attn_scores8_body
+template <int D, int G, int NP>
+__global__ __launch_bounds__(256) void k_attl_scores(AttnArgs a) {
+    constexpr int DQ = D / 8;
+    __shared__ __attribute__((aligned(16))) double qs[G][D];
+    __shared__ float wmax[NP][4][G];
+    const int g = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qd = tid & 7;
+    const int tb0 = blockIdx.y * 32 * NP;
+    const int kvb = a.n_ctx;
+    u32x4 kv[NP][DQ / 8];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int t = min(tb0 + 32 * p + (tid >> 3), kvb - 1);
+        const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = __builtin_nontemporal_load((const u32x4*)(kr + 8 * i));
+    }
+    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = (double)h2f(f2h(a.q[(size_t)g * G * D + i]));
+    const int n_kv = a.st->pos + 1;
+    __syncthreads();
+    if (tb0 >= n_kv) return;  // uniform
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int t = tb0 + 32 * p + (tid >> 3);
+        double acc[G];
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) {
+            const int d = qd * DQ + 8 * i;
+            double k[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                k[2 * j] = (double)h2f((uint16_t)kv[p][i][j]);
+                k[2 * j + 1] = (double)h2f((uint16_t)(kv[p][i][j] >> 16));
+            }
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[hh] = __builtin_fma(k[j], qs[hh][d + j], acc[hh]);
+        }
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            acc[hh] += xor_partner_d<1>(acc[hh]);
+            acc[hh] += xor_partner_d<2>(acc[hh]);
+            acc[hh] += xor_partner_d<4>(acc[hh]);
+            const float sc = (float)acc[hh] * a.scale;
+            if (t < n_kv && qd == (hh & 7)) a.scores[(size_t)(g * G + hh) * a.n_ctx + t] = sc;
+            float m = t < n_kv ? sc : -INFINITY;
+            m = fmaxf(m, xor_partner<8>(m));
+            m = fmaxf(m, xor_partner<16>(m));
+            m = fmaxf(m, xor_partner<32>(m));
+            if (lane == 0) wmax[p][wave][hh] = m;
+        }
+    }
+    __syncthreads();
+    if (tid < NP * G) {
+        const int p = tid / G, hh = tid % G;
+        if (tb0 + 32 * p < n_kv)
+            a.tmax[(size_t)(g * G + hh) * (a.n_ctx / 32) + (tb0 >> 5) + p] =
+                fmaxf(fmaxf(wmax[p][0][hh], wmax[p][1][hh]), fmaxf(wmax[p][2][hh], wmax[p][3][hh]));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_attl_exp(AttnArgs a, int n_head, int kvb) {
+    __shared__ float redm[4];
+    __shared__ double reds[4];
+    const int h = blockIdx.x, tile = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // loads before the position is known: this position's score, the head's tile maxima
+    const int t = tile * kLongTile + tid;
+    float* srow = a.scores + (size_t)h * a.n_ctx;
+    const float s = srow[min(t, kvb - 1)];
+    const float* tm = a.tmax + (size_t)h * (a.n_ctx / 32);
+    const int ntm_all = kvb >> 5;
+    constexpr int NM = 32768 / 32 / 256;  // tile maxima per thread up to a 32768-position bound
+    float mt[NM];
+#pragma unroll
+    for (int k = 0; k < NM; ++k) mt[k] = tm[min(tid + 256 * k, ntm_all - 1)];
+    const int n_kv = a.st->pos + 1;
+    const int ntl = (a.n_ctx + kLongTile - 1) / kLongTile;
+    double* tsum = attl_tsum(a, n_head) + (size_t)h * ntl;
+    if (tile * kLongTile >= n_kv) {  // uniform: tiles past the position
+        if (tid == 0) tsum[tile] = 0.0;
+        return;
+    }
+    const int ntm = (n_kv + 31) >> 5;
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+        if (tid + 256 * k < ntm) m = fmaxf(m, mt[k]);
+    for (int i = tid + 256 * NM; i < ntm; i += 256) m = fmaxf(m, tm[i]);
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
+    __syncthreads();
+    const float mx = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    double sum = 0.0;
+    if (t < n_kv) {
+        const float e = llmi_expf(s - mx);
+        srow[t] = e;
+        sum = (double)e;
+    }
+    sum = wave_sum_d(sum);
+    if (lane == 0) reds[wave] = sum;
+    __syncthreads();
+    if (tid == 0) tsum[tile] = ((reds[0] + reds[1]) + reds[2]) + reds[3];
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(512) void k_attl_pv(AttnArgs a, int n_head, int kvb) {
+    constexpr int SL = 512 / D;                  // lanes per output dim (4 or 8)
+    constexpr int NV = kLongTile / (8 * SL);     // 16-B V loads per lane (8 positions each)
+    __shared__ __attribute__((aligned(16))) float sp[G][kLongTile];
+    __shared__ float sinv[G];
+    const int g = blockIdx.x, tile = blockIdx.y, t0 = tile * kLongTile;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_kv = a.st->pos + 1;
+    if (t0 >= n_kv) return;  // uniform
+    const int ntl = (a.n_ctx + kLongTile - 1) / kLongTile;
+    // V rows of this tile first (independent of everything else)
+    const int d = tid / SL, sl = tid % SL;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    u32x4 vv[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) vv[u] = __builtin_nontemporal_load((const u32x4*)(vr + min(t0 + 8 * sl + 8 * SL * u, kvb - 8)));
+    // this tile's e values (k_attl_exp) of the G heads, also before the row sums
+    constexpr int NE = (G * kLongTile + 511) / 512;
+    float ev[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int i = min(tid + 512 * k, G * kLongTile - 1);
+        ev[k] = a.scores[(size_t)(g * G + i / kLongTile) * a.n_ctx + min(t0 + i % kLongTile, kvb - 1)];
+    }
+    // row sums: wave hh < G adds its head's tile sums (lanes, then the fixed butterfly)
+    const int ntv = (n_kv + kLongTile - 1) / kLongTile;
+    if (wave < G) {
+        const double* ts = attl_tsum(a, n_head) + (size_t)(g * G + wave) * ntl;
+        constexpr int NS = 32768 / kLongTile / 64;  // tile sums per lane up to 32768 positions
+        double tv[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) tv[k] = ts[min(lane + 64 * k, ntl - 1)];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (lane + 64 * k < ntv) s += tv[k];
+        for (int i = lane + 64 * NS; i < ntv; i += 64) s += ts[i];
+        s = wave_sum_d(s);
+        if (lane == 0) sinv[wave] = (float)(1.0 / s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int i = tid + 512 * k;
+        if (i < G * kLongTile) {
+            const int hh = i / kLongTile, t = t0 + i % kLongTile;
+            sp[hh][i % kLongTile] = t < n_kv ? h2f(f2h(ev[k] * sinv[hh])) : 0.f;
+        }
+    }
+    __syncthreads();
+    double acc[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int tb = 8 * sl + 8 * SL * u;  // within the tile
+        if (t0 + tb < n_kv) {
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float f = h2f((uint16_t)(vv[u][j >> 1] >> (16 * (j & 1))));
+                v[j] = t0 + tb + j < n_kv ? (double)f : 0.0;
+            }
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh) {
+                const float4 p0 = *(const float4*)&sp[hh][tb], p1 = *(const float4*)&sp[hh][tb + 4];
+                acc[hh] = __builtin_fma(v[0], (double)p0.x, acc[hh]);
+                acc[hh] = __builtin_fma(v[1], (double)p0.y, acc[hh]);
+                acc[hh] = __builtin_fma(v[2], (double)p0.z, acc[hh]);
+                acc[hh] = __builtin_fma(v[3], (double)p0.w, acc[hh]);
+                acc[hh] = __builtin_fma(v[4], (double)p1.x, acc[hh]);
+                acc[hh] = __builtin_fma(v[5], (double)p1.y, acc[hh]);
+                acc[hh] = __builtin_fma(v[6], (double)p1.z, acc[hh]);
+                acc[hh] = __builtin_fma(v[7], (double)p1.w, acc[hh]);
+            }
+        }
+    }
+    double* part = attl_part(a, n_head);
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        double v = acc[hh];
+        v += xor_partner_d<1>(v);
+        v += xor_partner_d<2>(v);
+        if constexpr (SL == 8) v += xor_partner_d<4>(v);
+        if (sl == 0) part[((size_t)(g * G + hh) * ntl + tile) * D + d] = v;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void k_attl_sum(AttnArgs a, int n_head) {
+    const int h = blockIdx.x, d = threadIdx.x;
+    const int n_kv = a.st->pos + 1;
+    const int ntl = (a.n_ctx + kLongTile - 1) / kLongTile, ntv = (n_kv + kLongTile - 1) / kLongTile;
+    const double* part = attl_part(a, n_head) + (size_t)h * ntl * D + d;
+    // batches of 16 loads in flight, summed in tile order
+    double s = 0.0;
+    for (int j0 = 0; j0 < ntv; j0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = part[(size_t)min(j0 + k, ntl - 1) * D];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (j0 + k < ntv) s += v[k];
+    }
+    a.out[(size_t)h * D + d] = (float)s;
+}
+
 // Dim-split one-launch attention (path 6, kv_bound <= 64*P <= 1024): H*S workgroups of
 // 512 threads.  Workgroup b serves query head h of KV group g = b % HK and the DS = D/S
 // output dims of slice b / H.  Each workgroup recomputes its head's scores and softmax
@@ -1702,6 +1941,7 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     if (g_attn_mode == 4 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
     if (g_attn_mode == 5 && kv_bound <= kRegAttnMaxKV) return 5;
     if (g_attn_mode == 6 && kv_bound <= kDimAttnMaxKV) return 6;
+    if (g_attn_mode == 7 && g <= 8) return 7;
     if (g_attn_mode == 1 && fused_ok) return 1;
     if (g_attn_mode == 2 && split_ok) return 2;
     if (g_attn_mode == 3) return 3;
@@ -1716,8 +1956,12 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     //   k_attn_d (dim-split, scores recomputed per slice, round 2) beats all of the above
     //   up to 1024 positions on every shape (tools/attnbench.py, profiles/r02/attn_dim_split.md):
     //   G=4 D=128 128: 5.2 vs 8.1 fused, 512: 7.0 vs 10.0 exchange, 1024: 10.8 vs 12.7 split
+    //   long-context four-launch path 7 (profiles/r02/attn_long.md): G=4 D=128 beyond 2048
+    //   (4096: 25.4 vs 31.2 split, 16384: 62 vs 628 two-kernel), G=8 beyond 1024
     if (g_attn_mode == 0) {
         if (g <= 8 && kv_bound <= kDimAttnMaxKV && attn_d_slices(n_head, head_dim) >= 2) return 6;
+        if (g == 8 && kv_bound > 1024) return 7;
+        if (g <= 4 && kv_bound > 2048) return 7;
         if (g == 8 && head_dim == 64 && kv_bound <= 256) return 5;
         if (g == 8 && fused_ok && kv_bound <= (head_dim == 64 ? 2048 : 640)) return 1;
         if (g == 4 && fused_ok && kv_bound <= 256) return 1;
@@ -1743,6 +1987,24 @@ hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int h
         LLMI_ATTR(128, 1) LLMI_ATTR(128, 2) LLMI_ATTR(128, 4) LLMI_ATTR(128, 8)
         LLMI_ATTR(64, 1) LLMI_ATTR(64, 2) LLMI_ATTR(64, 4) LLMI_ATTR(64, 8)
 #undef LLMI_ATTR
+        return hipErrorInvalidValue;
+    }
+    if (path == 7) {
+        const int ntile = (kv_bound + kLongTile - 1) / kLongTile;
+        const int np = kv_bound > 4096 ? 4 : 1;  // 32-position passes per scores workgroup
+        const dim3 gs(n_head_kv, (kv_bound + 32 * np - 1) / (32 * np));
+#define LLMI_ATTL(D_, G_)                                                                                   \
+        if (head_dim == D_ && g == G_) {                                                                    \
+            if (np == 4) launch_k(k_attl_scores<D_, G_, 4>, gs, dim3(256), 0, s, true, false, a);          \
+            else launch_k(k_attl_scores<D_, G_, 1>, gs, dim3(256), 0, s, true, false, a);                  \
+            launch_k(k_attl_exp, dim3(n_head, ntile), dim3(256), 0, s, false, false, a, n_head, kv_bound); \
+            launch_k(k_attl_pv<D_, G_>, dim3(n_head_kv, ntile), dim3(512), 0, s, false, false, a, n_head, kv_bound); \
+            launch_k(k_attl_sum<D_>, dim3(n_head), dim3(D_), 0, s, false, true, a, n_head);                \
+            return hipGetLastError();                                                                       \
+        }
+        LLMI_ATTL(128, 1) LLMI_ATTL(128, 2) LLMI_ATTL(128, 4) LLMI_ATTL(128, 8)
+        LLMI_ATTL(64, 1) LLMI_ATTL(64, 2) LLMI_ATTL(64, 4) LLMI_ATTL(64, 8)
+#undef LLMI_ATTL
         return hipErrorInvalidValue;
     }
     if (path == 6) {

@@ -178,12 +178,13 @@ def test_profile_kernels_leaves_state(gpu, tiny_models):
     assert np.array_equal(ref.logits(-1), c.logits(-1))
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5, 6, 7])
 def test_attention_paths_bit_exact(gpu, tiny_models, monkeypatch, mode):
     """Each attention path (1 fused one-WG-per-head, 2 split scores+PV over 16-dim
     slices, 3 long-context two-kernel, 4 one-launch exchange: score tiles handed off
     as tagged granules, 5 register-prefetched one-WG-per-head, 6 dim-split one-launch:
-    scores recomputed per output-dim slice) reproduces the oracle's
+    scores recomputed per output-dim slice, 7 long-context four-launch: exp and PV
+    partials per 256-position tile) reproduces the oracle's
     logits bit for bit
     (LLMI_ATTN_MODE is read when a context is created)."""
     monkeypatch.setenv("LLMI_ATTN_MODE", str(mode))

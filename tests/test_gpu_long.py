@@ -141,11 +141,12 @@ def _long_oracle(path, prompt):
 
 
 @pytest.mark.parametrize("preset,mode", [("tiny-mixed-d128", "0"), ("tiny-mixed-d128", "1"),
-                                         ("tiny-mixed-d128", "3"), ("tiny-mixed", "0")])
+                                         ("tiny-mixed-d128", "3"), ("tiny-mixed-d128", "7"),
+                                         ("tiny-mixed", "0"), ("tiny-mixed", "7")])
 def test_decode_past_4096_positions(gpu, tiny_models, monkeypatch, preset, mode):
     """A 4100-token prompt (batched prefill) and 4 decode steps at positions 4100-4103
-    with the attention path forced (LLMI_ATTN_MODE, read at context creation): 0 auto
-    (split at this length), 1 fused one-workgroup-per-head, 3 two-kernel."""
+    with the attention path forced (LLMI_ATTN_MODE, read at context creation): 0 auto,
+    1 fused one-workgroup-per-head, 3 two-kernel, 7 long-context four-launch."""
     path = tiny_models[preset]
     rng = np.random.default_rng(41)
     prompt = [1] + [int(t) for t in rng.integers(3, 700, 4099)]

@@ -154,13 +154,14 @@ def test_attention_variants_agree_long_context(gpu, tiny_models, monkeypatch):
     rng = np.random.default_rng(9)
     prompt = [1] + [int(t) for t in rng.integers(3, 700, 499)]
     res = []
-    for mode in ("2", "4", "6"):
+    for mode in ("2", "4", "6", "7"):
         monkeypatch.setenv("LLMI_ATTN_MODE", mode)
         _, a = _gpu_prompt_logits(path, prompt, 768, 0, monkeypatch, no_prefill=True)
         res.append(a[0])
     monkeypatch.setenv("LLMI_ATTN_MODE", "0")
     assert np.array_equal(res[0], res[1])
     assert np.array_equal(res[0], res[2])
+    assert np.array_equal(res[0], res[3])
 
 
 def test_prefill_continues_after_past(gpu, tiny_models, monkeypatch):
