@@ -177,6 +177,26 @@ def test_prompt_past_prefill_kv_limit(gpu, tiny_models, monkeypatch):
     _assert_same(got, steps)
 
 
+def test_prefill_attention_past_16k_positions(gpu, tiny_models, monkeypatch):
+    """A 16500-token prompt: both batched-prefill attention kernels (G heads per
+    workgroup, and one head per workgroup) then hold > 64 KiB of scores in LDS (both once
+    failed with "invalid argument" from a refused LDS attribute call).  Prefilled logits and the decode steps after them (long-context
+    decode attention) equal all-decode-step processing of the prompt bit for bit."""
+    path = tiny_models["tiny-mixed-d128"]
+    rng = np.random.default_rng(16)
+    prompt = [1] + [int(t) for t in rng.integers(3, 700, 16499)]
+    _, grouped = _gpu_run(path, prompt, 16640, 2)  # G = 2 heads per workgroup: 130 KiB LDS
+    old = llmi.test_option("pf_attn_simple", 1)
+    try:
+        _, pf = _gpu_run(path, prompt, 16640, 2)
+    finally:
+        llmi.test_option("pf_attn_simple", old)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    _, steps = _gpu_run(path, prompt, 16640, 2)
+    _assert_same(pf, steps)
+    _assert_same(grouped, steps)
+
+
 def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
     """k_attn_x's hand-off waits are bounded; with the bound lowered to 0 polls and the
     consumers waiting for a tag no producer writes (test options, captured into the step
