@@ -16,6 +16,7 @@
 #include "kernels.h"
 #include "mv_device.h"
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -417,12 +418,76 @@ hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// the single-sequence dim-split and long-context attention bodies (mv_device.h) with the
+// batch slot as the last grid dimension
+template <int D, int P, int S>
+__global__ __launch_bounds__(512) void k_battn_d(BAttnArgs b, int G, int HK, int kvb) {
+    attn_d_body<D, P, S>(b.a[blockIdx.y], G, HK, kvb);
+}
+template <int D, int G, int NP>
+__global__ __launch_bounds__(256) void k_battl_scores(BAttnArgs b) { attl_scores_body<D, G, NP>(b.a[blockIdx.z]); }
+__global__ __launch_bounds__(256) void k_battl_exp(BAttnArgs b, int n_head, int kvb) { attl_exp_body(b.a[blockIdx.z], n_head, kvb); }
+template <int D, int G>
+__global__ __launch_bounds__(512) void k_battl_pv(BAttnArgs b, int n_head, int kvb) { attl_pv_body<D, G>(b.a[blockIdx.z], n_head, kvb); }
+template <int D>
+__global__ __launch_bounds__(D) void k_battl_sum(BAttnArgs b, int n_head) { attl_sum_body<D>(b.a[blockIdx.z], n_head); }
+
+// batched attention path: dim split up to 1024 positions for up to 3 slots (8B bench:
+// 2 slots 940 vs 897 tok/s split, 4: 1335 vs 1341, 8: 1746 vs 1823 — at 8 slots its
+// redundant K reads cost more than the split path's second launch), split while its LDS
+// fits up to 2048 (G <= 4) / 1024 positions, long-context beyond; LLMI_BATTN_MODE (A/B
+// only) forces 2 split, 6 dim split or 7 long-context
+static int battn_path(int g, int n_head, int head_dim, int kv_bound, int nt) {
+    const char* e = getenv("LLMI_BATTN_MODE");
+    const int forced = e ? atoi(e) : 0;
+    const bool split_ok = (size_t)g * kv_bound * 4 <= kSplitAttnMaxLds;
+    const bool dim_ok = g <= 8 && kv_bound <= kDimAttnMaxKV && attn_d_slices(n_head, head_dim) >= 2;
+    if (forced == 2 && split_ok) return 2;
+    if (forced == 6 && dim_ok) return 6;
+    if (forced == 7 && g <= 8) return 7;
+    if (dim_ok && nt <= 3) return 6;
+    if (split_ok && (g <= 4 ? kv_bound <= 2048 : kv_bound <= 1024)) return 2;
+    if (dim_ok) return 6;
+    return g <= 8 ? 7 : (split_ok ? 2 : 0);
+}
+
 hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
                              hipStream_t s) {
     if (nt < 1 || nt > kMaxBatch || n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     const int g = n_head / n_head_kv;
+    const int path = battn_path(g, n_head, head_dim, kv_bound, nt);
+    if (path == 6) {
+        const int p = kv_bound <= 64 ? 1 : kv_bound <= 128 ? 2 : kv_bound <= 256 ? 4 : kv_bound <= 512 ? 8
+                    : kv_bound <= 768 ? 12 : 16;
+        const int sd = attn_d_slices(n_head, head_dim);
+#define LLMI_BATTD(D_, P_, S_) \
+        if (head_dim == D_ && p == P_ && sd == S_) { hipLaunchKernelGGL((k_battn_d<D_, P_, S_>), dim3(n_head * S_, nt), dim3(512), 0, s, b, g, n_head_kv, kv_bound); return hipGetLastError(); }
+#define LLMI_BATTD_P(D_, S_) LLMI_BATTD(D_, 1, S_) LLMI_BATTD(D_, 2, S_) LLMI_BATTD(D_, 4, S_) LLMI_BATTD(D_, 8, S_) LLMI_BATTD(D_, 12, S_) LLMI_BATTD(D_, 16, S_)
+        LLMI_BATTD_P(128, 2) LLMI_BATTD_P(128, 4) LLMI_BATTD_P(128, 8) LLMI_BATTD_P(64, 2) LLMI_BATTD_P(64, 4) LLMI_BATTD_P(64, 8)
+#undef LLMI_BATTD_P
+#undef LLMI_BATTD
+        return hipErrorInvalidValue;
+    }
+    if (path == 7) {
+        const int ntile = (kv_bound + kLongTile - 1) / kLongTile;
+        const int np = kv_bound > 4096 ? 4 : 1;
+        const dim3 gs(n_head_kv, (kv_bound + 32 * np - 1) / (32 * np), nt);
+#define LLMI_BATTL(D_, G_)                                                                                        \
+        if (head_dim == D_ && g == G_) {                                                                          \
+            if (np == 4) hipLaunchKernelGGL((k_battl_scores<D_, G_, 4>), gs, dim3(256), 0, s, b);                 \
+            else hipLaunchKernelGGL((k_battl_scores<D_, G_, 1>), gs, dim3(256), 0, s, b);                         \
+            hipLaunchKernelGGL(k_battl_exp, dim3(n_head, ntile, nt), dim3(256), 0, s, b, n_head, kv_bound);       \
+            hipLaunchKernelGGL((k_battl_pv<D_, G_>), dim3(n_head_kv, ntile, nt), dim3(512), 0, s, b, n_head, kv_bound); \
+            hipLaunchKernelGGL((k_battl_sum<D_>), dim3(n_head, 1, nt), dim3(D_), 0, s, b, n_head);               \
+            return hipGetLastError();                                                                             \
+        }
+        LLMI_BATTL(128, 1) LLMI_BATTL(128, 2) LLMI_BATTL(128, 4) LLMI_BATTL(128, 8)
+        LLMI_BATTL(64, 1) LLMI_BATTL(64, 2) LLMI_BATTL(64, 4) LLMI_BATTL(64, 8)
+#undef LLMI_BATTL
+        return hipErrorInvalidValue;
+    }
+    if (path != 2) return hipErrorInvalidValue;
     const size_t lds = (size_t)g * kv_bound * 4;
-    if (lds > kSplitAttnMaxLds) return hipErrorInvalidValue;
 #define LLMI_BATT(D_, G_)                                                                                    \
     if (head_dim == D_ && g == G_) {                                                                         \
         hipLaunchKernelGGL((k_battn_scores8<D_, G_>), dim3(n_head_kv, (kv_bound + 31) / 32, nt), dim3(256), 0, s, b); \

@@ -818,7 +818,10 @@ bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& er
     if (!balloc(c, err)) return false;
     const int bucket = max_pos / 256;
     const int kv_bound = std::min(c.n_ctx, (bucket + 1) * 256);
-    if ((size_t)(hp.n_head / hp.n_head_kv) * kv_bound * 4 > kSplitAttnMaxLds) { err = "batched step: context too long"; return false; }
+    if (hp.n_head / hp.n_head_kv > 8 && (size_t)(hp.n_head / hp.n_head_kv) * kv_bound * 4 > kSplitAttnMaxLds) {
+        err = "batched step: context too long for GQA groups of more than 8 heads";
+        return false;
+    }
     // slot -> sequence map (padded slots -> the dummy sequence n_seq)
     std::vector<int> map((size_t)kMaxBatch, c.n_seq);
     for (int s = 0; s < nt; ++s) map[(size_t)s] = seqs[s];

@@ -966,4 +966,376 @@ __device__ __forceinline__ void attn_pv16_body(const AttnArgs& a, int kvb) {
     LLMI_ATT_STAMP(1, 3)
 }
 
+// Long-context attention (path 7): every phase spread over position tiles so the K and V
+// streams use the whole chip, in four launches (a softmax over a whole row cannot be
+// formed piecewise bit-exactly: p = f16(e / sum) needs the row's max and sum first).
+//   1. k_attn_scores8 (split path phase 1): scores of the G heads per 32-position tile,
+//      K read once, plus per-tile maxima
+//   2. k_attl_exp    grid (H, tiles of kLongTile): row max from the tile maxima, e =
+//      expf(s - max) in place, the tile's double sum of e
+//   3. k_attl_pv     grid (HK, tiles): row sum = the tile sums in fixed order, p =
+//      f16(e * (float)(1 / sum)), PV of the tile's positions for all D dims of the G
+//      heads (V read once), double partial per (head, tile, dim)
+//   4. k_attl_sum    grid H: out = the partials summed over tiles in fixed order
+// The double sums are exact in practice, as on every other path (tests compare with the
+// oracle and the other paths bit for bit).
+__device__ __forceinline__ double* attl_tsum(const AttnArgs& a, int n_head) {
+    return (double*)(a.scores + attn_long_off(n_head, a.n_ctx));
+}
+__device__ __forceinline__ double* attl_part(const AttnArgs& a, int n_head) {
+    return attl_tsum(a, n_head) + (size_t)n_head * ((a.n_ctx + kLongTile - 1) / kLongTile);
+}
+
+// phase 1 for long contexts: k_attn_scores8 with NP 32-position passes per workgroup (the
+// q staging amortised over 32*NP positions, every K load issued at entry); same per-pass
+// arithmetic, scores and tile maxima as attn_scores8_body
+template <int D, int G, int NP>
+__device__ __forceinline__ void attl_scores_body(const AttnArgs& a) {
+    constexpr int DQ = D / 8;
+    __shared__ __attribute__((aligned(16))) double qs[G][D];
+    __shared__ float wmax[NP][4][G];
+    const int g = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qd = tid & 7;
+    const int tb0 = blockIdx.y * 32 * NP;
+    const int kvb = a.n_ctx;
+    u32x4 kv[NP][DQ / 8];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int t = min(tb0 + 32 * p + (tid >> 3), kvb - 1);
+        const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = __builtin_nontemporal_load((const u32x4*)(kr + 8 * i));
+    }
+    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = (double)h2f(f2h(a.q[(size_t)g * G * D + i]));
+    const int n_kv = a.st->pos + 1;
+    __syncthreads();
+    if (tb0 >= n_kv) return;  // uniform
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int t = tb0 + 32 * p + (tid >> 3);
+        double acc[G];
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) {
+            const int d = qd * DQ + 8 * i;
+            double k[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                k[2 * j] = (double)h2f((uint16_t)kv[p][i][j]);
+                k[2 * j + 1] = (double)h2f((uint16_t)(kv[p][i][j] >> 16));
+            }
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[hh] = __builtin_fma(k[j], qs[hh][d + j], acc[hh]);
+        }
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            acc[hh] += xor_partner_d<1>(acc[hh]);
+            acc[hh] += xor_partner_d<2>(acc[hh]);
+            acc[hh] += xor_partner_d<4>(acc[hh]);
+            const float sc = (float)acc[hh] * a.scale;
+            if (t < n_kv && qd == (hh & 7)) a.scores[(size_t)(g * G + hh) * a.n_ctx + t] = sc;
+            float m = t < n_kv ? sc : -INFINITY;
+            m = fmaxf(m, xor_partner<8>(m));
+            m = fmaxf(m, xor_partner<16>(m));
+            m = fmaxf(m, xor_partner<32>(m));
+            if (lane == 0) wmax[p][wave][hh] = m;
+        }
+    }
+    __syncthreads();
+    if (tid < NP * G) {
+        const int p = tid / G, hh = tid % G;
+        if (tb0 + 32 * p < n_kv)
+            a.tmax[(size_t)(g * G + hh) * (a.n_ctx / 32) + (tb0 >> 5) + p] =
+                fmaxf(fmaxf(wmax[p][0][hh], wmax[p][1][hh]), fmaxf(wmax[p][2][hh], wmax[p][3][hh]));
+    }
+}
+
+__device__ __forceinline__ void attl_exp_body(const AttnArgs& a, int n_head, int kvb) {
+    __shared__ float redm[4];
+    __shared__ double reds[4];
+    const int h = blockIdx.x, tile = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // loads before the position is known: this position's score, the head's tile maxima
+    const int t = tile * kLongTile + tid;
+    float* srow = a.scores + (size_t)h * a.n_ctx;
+    const float s = srow[min(t, kvb - 1)];
+    const float* tm = a.tmax + (size_t)h * (a.n_ctx / 32);
+    const int ntm_all = kvb >> 5;
+    constexpr int NM = 32768 / 32 / 256;  // tile maxima per thread up to a 32768-position bound
+    float mt[NM];
+#pragma unroll
+    for (int k = 0; k < NM; ++k) mt[k] = tm[min(tid + 256 * k, ntm_all - 1)];
+    const int n_kv = a.st->pos + 1;
+    const int ntl = (a.n_ctx + kLongTile - 1) / kLongTile;
+    double* tsum = attl_tsum(a, n_head) + (size_t)h * ntl;
+    if (tile * kLongTile >= n_kv) {  // uniform: tiles past the position
+        if (tid == 0) tsum[tile] = 0.0;
+        return;
+    }
+    const int ntm = (n_kv + 31) >> 5;
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+        if (tid + 256 * k < ntm) m = fmaxf(m, mt[k]);
+    for (int i = tid + 256 * NM; i < ntm; i += 256) m = fmaxf(m, tm[i]);
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
+    __syncthreads();
+    const float mx = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    double sum = 0.0;
+    if (t < n_kv) {
+        const float e = llmi_expf(s - mx);
+        srow[t] = e;
+        sum = (double)e;
+    }
+    sum = wave_sum_d(sum);
+    if (lane == 0) reds[wave] = sum;
+    __syncthreads();
+    if (tid == 0) tsum[tile] = ((reds[0] + reds[1]) + reds[2]) + reds[3];
+}
+
+template <int D, int G>
+__device__ __forceinline__ void attl_pv_body(const AttnArgs& a, int n_head, int kvb) {
+    constexpr int SL = 512 / D;                  // lanes per output dim (4 or 8)
+    constexpr int NV = kLongTile / (8 * SL);     // 16-B V loads per lane (8 positions each)
+    __shared__ __attribute__((aligned(16))) float sp[G][kLongTile];
+    __shared__ float sinv[G];
+    const int g = blockIdx.x, tile = blockIdx.y, t0 = tile * kLongTile;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_kv = a.st->pos + 1;
+    if (t0 >= n_kv) return;  // uniform
+    const int ntl = (a.n_ctx + kLongTile - 1) / kLongTile;
+    // V rows of this tile first (independent of everything else)
+    const int d = tid / SL, sl = tid % SL;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    u32x4 vv[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) vv[u] = __builtin_nontemporal_load((const u32x4*)(vr + min(t0 + 8 * sl + 8 * SL * u, kvb - 8)));
+    // this tile's e values (k_attl_exp) of the G heads, also before the row sums
+    constexpr int NE = (G * kLongTile + 511) / 512;
+    float ev[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int i = min(tid + 512 * k, G * kLongTile - 1);
+        ev[k] = a.scores[(size_t)(g * G + i / kLongTile) * a.n_ctx + min(t0 + i % kLongTile, kvb - 1)];
+    }
+    // row sums: wave hh < G adds its head's tile sums (lanes, then the fixed butterfly)
+    const int ntv = (n_kv + kLongTile - 1) / kLongTile;
+    if (wave < G) {
+        const double* ts = attl_tsum(a, n_head) + (size_t)(g * G + wave) * ntl;
+        constexpr int NS = 32768 / kLongTile / 64;  // tile sums per lane up to 32768 positions
+        double tv[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) tv[k] = ts[min(lane + 64 * k, ntl - 1)];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (lane + 64 * k < ntv) s += tv[k];
+        for (int i = lane + 64 * NS; i < ntv; i += 64) s += ts[i];
+        s = wave_sum_d(s);
+        if (lane == 0) sinv[wave] = (float)(1.0 / s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int i = tid + 512 * k;
+        if (i < G * kLongTile) {
+            const int hh = i / kLongTile, t = t0 + i % kLongTile;
+            sp[hh][i % kLongTile] = t < n_kv ? h2f(f2h(ev[k] * sinv[hh])) : 0.f;
+        }
+    }
+    __syncthreads();
+    double acc[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) acc[hh] = 0.0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int tb = 8 * sl + 8 * SL * u;  // within the tile
+        if (t0 + tb < n_kv) {
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float f = h2f((uint16_t)(vv[u][j >> 1] >> (16 * (j & 1))));
+                v[j] = t0 + tb + j < n_kv ? (double)f : 0.0;
+            }
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh) {
+                const float4 p0 = *(const float4*)&sp[hh][tb], p1 = *(const float4*)&sp[hh][tb + 4];
+                acc[hh] = __builtin_fma(v[0], (double)p0.x, acc[hh]);
+                acc[hh] = __builtin_fma(v[1], (double)p0.y, acc[hh]);
+                acc[hh] = __builtin_fma(v[2], (double)p0.z, acc[hh]);
+                acc[hh] = __builtin_fma(v[3], (double)p0.w, acc[hh]);
+                acc[hh] = __builtin_fma(v[4], (double)p1.x, acc[hh]);
+                acc[hh] = __builtin_fma(v[5], (double)p1.y, acc[hh]);
+                acc[hh] = __builtin_fma(v[6], (double)p1.z, acc[hh]);
+                acc[hh] = __builtin_fma(v[7], (double)p1.w, acc[hh]);
+            }
+        }
+    }
+    double* part = attl_part(a, n_head);
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        double v = acc[hh];
+        v += xor_partner_d<1>(v);
+        v += xor_partner_d<2>(v);
+        if constexpr (SL == 8) v += xor_partner_d<4>(v);
+        if (sl == 0) part[((size_t)(g * G + hh) * ntl + tile) * D + d] = v;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void attl_sum_body(const AttnArgs& a, int n_head) {
+    const int h = blockIdx.x, d = threadIdx.x;
+    const int n_kv = a.st->pos + 1;
+    const int ntl = (a.n_ctx + kLongTile - 1) / kLongTile, ntv = (n_kv + kLongTile - 1) / kLongTile;
+    const double* part = attl_part(a, n_head) + (size_t)h * ntl * D + d;
+    // batches of 16 loads in flight, summed in tile order
+    double s = 0.0;
+    for (int j0 = 0; j0 < ntv; j0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = part[(size_t)min(j0 + k, ntl - 1) * D];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (j0 + k < ntv) s += v[k];
+    }
+    a.out[(size_t)h * D + d] = (float)s;
+}
+
+// Dim-split one-launch attention (path 6, kv_bound <= 64*P <= 1024): H*S workgroups of
+// 512 threads.  Workgroup b serves query head h of KV group g = b % HK and the DS = D/S
+// output dims of slice b / H.  Each workgroup recomputes its head's scores and softmax
+// in full (no cross-workgroup hand-off) and splits only the PV, so a head's K rows are
+// read by S workgroups and its V rows once in total.  Placement: the G*S workgroups of a
+// KV group have equal b % HK, i.e. one XCD under round-robin dispatch (HK = 8), so a K
+// row comes from HBM once and from that XCD's L2 for the others (default cache policy
+// on K and V for that reason).  Every global load is issued at entry, as in k_attn_r;
+// numerics are k_attn_r's (exact f16 products summed in double, p = f16(e * (float)(1 /
+// sum)), double PV); the per-position work and the PV lane split differ only in how the
+// exact double sums are associated.
+template <int D, int P, int S>
+__device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, int kvb) {
+    constexpr int DQ = D / 8;                    // score dims per lane
+    constexpr int DS = D / S;                    // output dims of this workgroup
+    constexpr int SLV = 512 / DS;                // PV lanes per output dim (<= 64)
+    constexpr int NVL = (64 * P + 8 * SLV - 1) / (8 * SLV);  // 16-B V loads per lane
+    static_assert(SLV <= 64 && (SLV & (SLV - 1)) == 0, "PV lanes of a dim stay in one wave");
+    __shared__ __attribute__((aligned(16))) float sp[64 * P + 8];
+    __shared__ float redm[8];
+    __shared__ double reds[8];
+    LLMI_ATT_STAMP(0, 0)
+    const int b = blockIdx.x, H = HK * G;
+    const int g = b % HK, h = g * G + (b / HK) % G, ds = b / H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qd = tid & 7, pp = tid >> 3;
+    // 1. every load up front: position, q slice, the K rows of all passes, the V slice
+    const int pos = a.st->pos;
+    float4 qv[DQ / 4];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; ++i) qv[i] = *(const float4*)(a.q + (size_t)h * D + qd * DQ + 4 * i);
+    u32x4 kv[P][DQ / 8];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int t = min(64 * p + pp, kvb - 1);
+        const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = *(const u32x4*)(kr + 8 * i);
+    }
+    const int d = ds * DS + tid / SLV, sl = tid % SLV;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    u32x4 vv[NVL];
+#pragma unroll
+    for (int u = 0; u < NVL; ++u) vv[u] = *(const u32x4*)(vr + min(8 * sl + 8 * SLV * u, kvb - 8));
+    const int n_kv = pos + 1;
+    // 2. scores (q rounded to f16 as upstream's KQ mul_mat does; f16 x f16 products exact)
+    double q[DQ];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; ++i) {
+        q[4 * i + 0] = (double)h2f(f2h(qv[i].x)); q[4 * i + 1] = (double)h2f(f2h(qv[i].y));
+        q[4 * i + 2] = (double)h2f(f2h(qv[i].z)); q[4 * i + 3] = (double)h2f(f2h(qv[i].w));
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < DQ / 8; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                acc = __builtin_fma((double)h2f((uint16_t)kv[p][i][jj]), q[8 * i + 2 * jj], acc);
+                acc = __builtin_fma((double)h2f((uint16_t)(kv[p][i][jj] >> 16)), q[8 * i + 2 * jj + 1], acc);
+            }
+        acc += xor_partner_d<1>(acc);
+        acc += xor_partner_d<2>(acc);
+        acc += xor_partner_d<4>(acc);
+        const int t = 64 * p + pp;
+        const float sc = (float)acc * a.scale;
+        if (qd == 0) sp[t] = sc;
+        if (t < n_kv) m = fmaxf(m, sc);
+    }
+    LLMI_ATT_STAMP(0, 1)
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
+    __syncthreads();
+    float mx = redm[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) mx = fmaxf(mx, redm[w]);
+    // 3. softmax: thread t owns positions t, t + 512
+    constexpr int NE = (64 * P + 511) / 512;
+    float e[NE];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int t = tid + 512 * k;
+        e[k] = 0.f;
+        if (t < n_kv && t < 64 * P) {
+            e[k] = llmi_expf(sp[t] - mx);
+            s += (double)e[k];
+        }
+    }
+    s = wave_sum_d(s);
+    if (lane == 0) reds[wave] = s;
+    __syncthreads();
+    double tot = reds[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) tot += reds[w];
+    const float inv = (float)(1.0 / tot);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int t = tid + 512 * k;
+        if (t < 64 * P) sp[t] = t < n_kv ? h2f(f2h(e[k] * inv)) : 0.f;
+    }
+    __syncthreads();
+    LLMI_ATT_STAMP(0, 2)
+    // 4. PV of this workgroup's DS dims: lane sl covers positions 8*sl + 8*SLV*u + j
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NVL; ++u) {
+        const int tb = 8 * sl + 8 * SLV * u;
+        if (tb < n_kv) {
+            const float4 p0 = *(const float4*)(sp + tb), p1 = *(const float4*)(sp + tb + 4);
+            const float pr[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float f = h2f((uint16_t)(vv[u][j >> 1] >> (16 * (j & 1))));
+                const double v = tb + j < n_kv ? (double)f : 0.0;
+                if (j & 1) acc1 = __builtin_fma(v, (double)pr[j], acc1);
+                else acc0 = __builtin_fma(v, (double)pr[j], acc0);
+            }
+        }
+    }
+    double acc = acc0 + acc1;
+    if constexpr (SLV >= 2) acc += xor_partner_d<1>(acc);
+    if constexpr (SLV >= 4) acc += xor_partner_d<2>(acc);
+    if constexpr (SLV >= 8) acc += xor_partner_d<4>(acc);
+    if constexpr (SLV >= 16) acc += xor_partner_d<8>(acc);
+    if constexpr (SLV >= 32) acc += xor_partner_d<16>(acc);
+    if constexpr (SLV >= 64) acc += xor_partner_d<32>(acc);
+    if (sl == 0) a.out[(size_t)h * D + d] = (float)acc;
+    LLMI_ATT_STAMP(0, 3)
+}
+
 }  // namespace llmi

@@ -178,27 +178,36 @@ def test_batched_real_widths(gpu, synth_dir, preset, n_vocab):
         assert got[s] == want[s], f"seq {s}"
 
 
-def test_batched_past_attention_lds_bound_falls_back(gpu, synth_dir):
-    """TinyLlama shapes (GQA 8): the batched attention holds 8 heads x kv_bound scores in
-    LDS (<= 4096 positions).  Past it llmi_generate_greedy_batch reports the limit and
-    llama_decode runs those sequences one at a time — same tokens as single decode."""
+def test_batched_long_context_gqa8(gpu, synth_dir):
+    """TinyLlama shapes (GQA 8) with one sequence past 4096 positions: the batched step's
+    attention used to hold 8 heads x kv_bound scores in LDS and refused such batches; it
+    now takes the long-context path (per-tile exp / PV partials) and every sequence's
+    tokens and logits equal its single decode."""
     path = str(synth_dir / "tinyllama-q8_0-batch-L2.gguf")
     llmi.write_synthetic_gguf(path, "tinyllama-q8_0", seed=11, n_layer=2)
     rng = np.random.default_rng(8)
     prompts = [[1] + [int(t) for t in rng.integers(3, 30000, 4150)], [1] + [int(t) for t in rng.integers(3, 30000, 20)]]
     want, want_lg = _single_reference(path, prompts, 3, 4352)
-    m = llmi.Model(path)
-    c = llmi.Context(m, n_ctx=4352, n_seq=2)
-    firsts = []
-    for s, p in enumerate(prompts):
-        assert c.decode(p, seq=[s] * len(p)) == 0
-        assert np.array_equal(c.logits(-1), want_lg[s])
-        firsts.append(c.greedy(-1))
-    with pytest.raises(llmi.LlmiError):
-        c.generate_greedy_batch([0, 1], firsts, [len(p) for p in prompts], 2)
-    # llama_decode with one token per sequence: not batchable here, still exact
-    assert c.decode(firsts, pos=[len(p) for p in prompts], seq=[0, 1], logits_all=True) == 0
-    assert [c.greedy(0), c.greedy(1)] == [want[0][1], want[1][1]]
+    got, got_lg, _ = _batched(path, prompts, 3, 4352, n_seq=2)
+    for s in range(2):
+        assert np.array_equal(got_lg[s], want_lg[s]), f"seq {s}: prompt logits differ"
+        assert got[s] == want[s], f"seq {s}: batched {got[s]} single {want[s]}"
+
+
+@pytest.mark.parametrize("mode", ["2", "6", "7"])
+def test_batched_attention_paths(gpu, tiny_models, monkeypatch, mode):
+    """The batched step's attention forced to each path (LLMI_BATTN_MODE: 2 split, 6
+    dim-split, 7 long-context), sequences straddling a KV bucket: tokens equal single
+    decode."""
+    monkeypatch.setenv("LLMI_BATTN_MODE", mode)
+    for preset in ("tiny-mixed-d128",):  # (tiny-mixed: gate/up types differ, not batchable)
+        path = tiny_models[preset]
+        rng = np.random.default_rng(70 + int(mode))
+        prompts = [[1] + [int(t) for t in rng.integers(3, 700, 249)], [1] + [int(t) for t in rng.integers(3, 700, 9)],
+                   [1] + [int(t) for t in rng.integers(3, 700, 120)]]
+        want, _ = _single_reference(path, prompts, 16, 512)
+        got, _, _ = _batched(path, prompts, 16, 512)
+        assert got == want, preset
 
 
 @pytest.mark.parametrize("preset", ["tiny-mixed-d128", "tiny-mixed"])
