@@ -28,7 +28,7 @@ step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output
     python3 bench.py > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" || { tail -20 "$OUT/prof_bench.err"; exit 1; }
 cat "$OUT/prof_bench.json"
 step pmc_bench 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_bench" -o run --output-format csv -- \
-    python3 bench.py --prompt 4 --steps 8 --warmup 2 --profile-steps 0 --no-cpu-baseline \
+    python3 bench.py --prompt 4 --steps 8 --warmup 2 --profile-steps 0 --no-cpu-baseline --eager \
     > "$OUT/pmc_bench.json" 2> "$OUT/pmc_bench.err" || { tail -20 "$OUT/pmc_bench.err"; exit 1; }
 export MV_SHAPES=12:28672x4096 MV_REPS=5
 step pmc_cal 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_cal" -o run \
