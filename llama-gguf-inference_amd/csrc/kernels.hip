@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(D) void k_attl_sum(AttnArgs a, int n_head) { attl_s
 
 // Dim-split one-launch attention (path 6): body in mv_device.h (shared with batch.hip)
 template <int D, int P, int S>
-__global__ __launch_bounds__(512) void k_attn_d(AttnArgs a, int G, int HK, int kvb) { attn_d_body<D, P, S>(a, G, HK, kvb); }
+__global__ __launch_bounds__(512) void k_attn_d(AttnArgs a, int G, int HK, int kvb, int pf) { attn_d_body<D, P, S>(a, G, HK, kvb, pf); }
 
 // ----------------------------------------------------------------------------------
 // Step entry: choose the token, advance pos, dequantize its embedding row
@@ -1562,6 +1562,10 @@ int pf_max_kv() { return g_pf_max_kv; }
 
 // dim slices of k_attn_d: about 256 workgroups (one per CU), 2..8, at least 8 dims each
 static int g_attn_s = 0;  // LLMI_ATTN_S (A/B only): force 2, 4 or 8 slices
+// k_attn_d reads the position before its K/V loads and skips those past it (default;
+// LLMI_ATTN_PF=0 loads the whole KV bucket, A/B only): ties at bucket ends, up to 1.4 us
+// faster mid-bucket (profiles/r02/attn_dim_split.md)
+static int g_attn_pf = 1;
 int attn_d_slices(int n_head, int head_dim) {
     const int s = g_attn_s ? g_attn_s : n_head >= 128 ? 2 : n_head >= 64 ? 4 : 8;
     return head_dim / s >= 8 ? s : head_dim / 8;
@@ -1573,6 +1577,8 @@ void set_attn_mode(int mode) {
     const char* e = getenv("LLMI_ATTN_S");
     const int v = e ? atoi(e) : 0;
     g_attn_s = (v == 2 || v == 4 || v == 8) ? v : 0;
+    const char* f = getenv("LLMI_ATTN_PF");
+    g_attn_pf = f ? atoi(f) : 1;
 }
 int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     const int g = n_head / n_head_kv;
@@ -1653,7 +1659,7 @@ hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int h
                     : kv_bound <= 768 ? 12 : 16;
         const int sdim = attn_d_slices(n_head, head_dim);
 #define LLMI_ATTD(D_, P_, S_) \
-        if (head_dim == D_ && p == P_ && sdim == S_) { launch_k(k_attn_d<D_, P_, S_>, dim3(n_head * S_), dim3(512), 0, s, true, true, a, g, n_head_kv, kv_bound); return hipGetLastError(); }
+        if (head_dim == D_ && p == P_ && sdim == S_) { launch_k(k_attn_d<D_, P_, S_>, dim3(n_head * S_), dim3(512), 0, s, true, true, a, g, n_head_kv, kv_bound, g_attn_pf); return hipGetLastError(); }
 #define LLMI_ATTD_P(D_, S_) LLMI_ATTD(D_, 1, S_) LLMI_ATTD(D_, 2, S_) LLMI_ATTD(D_, 4, S_) LLMI_ATTD(D_, 8, S_) LLMI_ATTD(D_, 12, S_) LLMI_ATTD(D_, 16, S_)
         LLMI_ATTD_P(128, 2) LLMI_ATTD_P(128, 4) LLMI_ATTD_P(128, 8) LLMI_ATTD_P(64, 2) LLMI_ATTD_P(64, 4) LLMI_ATTD_P(64, 8)
 #undef LLMI_ATTD_P

@@ -1217,7 +1217,7 @@ __device__ __forceinline__ void attl_sum_body(const AttnArgs& a, int n_head) {
 // sum)), double PV); the per-position work and the PV lane split differ only in how the
 // exact double sums are associated.
 template <int D, int P, int S>
-__device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, int kvb) {
+__device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, int kvb, int pf = 0) {
     constexpr int DQ = D / 8;                    // score dims per lane
     constexpr int DS = D / S;                    // output dims of this workgroup
     constexpr int SLV = 512 / DS;                // PV lanes per output dim (<= 64)
@@ -1231,8 +1231,11 @@ __device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, in
     const int g = b % HK, h = g * G + (b / HK) % G, ds = b / H;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qd = tid & 7, pp = tid >> 3;
-    // 1. every load up front: position, q slice, the K rows of all passes, the V slice
+    // 1. every load up front: position, q slice, the K rows of all passes, the V slice.
+    // pf (the default): the K passes / V loads past the position are skipped (uniform
+    // branches on the position read first) instead of loading the whole KV bucket
     const int pos = a.st->pos;
+    const int lim = pf ? pos + 1 : kvb;
     float4 qv[DQ / 4];
 #pragma unroll
     for (int i = 0; i < DQ / 4; ++i) qv[i] = *(const float4*)(a.q + (size_t)h * D + qd * DQ + 4 * i);
@@ -1241,14 +1244,22 @@ __device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, in
     for (int p = 0; p < P; ++p) {
         const int t = min(64 * p + pp, kvb - 1);
         const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
+        if (64 * p < lim) {
 #pragma unroll
-        for (int i = 0; i < DQ / 8; ++i) kv[p][i] = *(const u32x4*)(kr + 8 * i);
+            for (int i = 0; i < DQ / 8; ++i) kv[p][i] = *(const u32x4*)(kr + 8 * i);
+        } else {
+#pragma unroll
+            for (int i = 0; i < DQ / 8; ++i) kv[p][i] = u32x4{0u, 0u, 0u, 0u};
+        }
     }
     const int d = ds * DS + tid / SLV, sl = tid % SLV;
     const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
     u32x4 vv[NVL];
 #pragma unroll
-    for (int u = 0; u < NVL; ++u) vv[u] = *(const u32x4*)(vr + min(8 * sl + 8 * SLV * u, kvb - 8));
+    for (int u = 0; u < NVL; ++u) {
+        if (8 * SLV * u < lim) vv[u] = *(const u32x4*)(vr + min(8 * sl + 8 * SLV * u, kvb - 8));
+        else vv[u] = u32x4{0u, 0u, 0u, 0u};
+    }
     const int n_kv = pos + 1;
     // 2. scores (q rounded to f16 as upstream's KQ mul_mat does; f16 x f16 products exact)
     double q[DQ];
@@ -1260,6 +1271,7 @@ __device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, in
     float m = -INFINITY;
 #pragma unroll
     for (int p = 0; p < P; ++p) {
+        if (64 * p >= lim) break;  // uniform: passes past the position (pf only)
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < DQ / 8; ++i)
