@@ -27,6 +27,7 @@
 #include "kernels.h"
 #include "mv_device.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -52,6 +53,8 @@ static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s,
     else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
 }
 
+
+static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_SPLIT_BY_PAIRS")) : 0;  // A/B only
 
 size_t mv_lds_bytes(int act, int cols) { return lds_red_off(act, cols) + kMVWaves * sizeof(double); }
 
@@ -1323,15 +1326,34 @@ static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t 
 }
 
 // Two type groups (pairs [0, split) of type T, [split, npairs) of type T2): the
-// resident grid is dealt to the groups in proportion to their pairs (>= 1 each).
+// resident grid is dealt to the groups so that the largest per-wave byte count (pairs per
+// wave rounded up x bytes per pair) is smallest, >= 1 workgroup each.  (Dealing by pair
+// count left the Q6_K attn_v group of an 8B QKV at 2 pairs = 13.4 KB per wave while the
+// Q4_K waves had 9.2 KB.)  Which wave reduces a pair never changes a result.
+static int split_groups(int wgs, int p1, int p2, double b1, double b2) {
+    int best = 1;
+    double best_cost = 1e300;
+    for (int w1 = 1; w1 < wgs; ++w1) {
+        const int n1 = w1 * kMVWaves, n2 = (wgs - w1) * kMVWaves;
+        const double c = std::max((double)((p1 + n1 - 1) / n1) * b1, (double)((p2 + n2 - 1) / n2) * b2);
+        if (c < best_cost) { best_cost = c; best = w1; }
+    }
+    return best;
+}
 template <int ACT, bool NORM, int T, int T2, int EPI, int NP>
 static hipError_t mv_launch2(const MVArgs& a0, int split_pairs, dim3 grid, size_t lds, hipStream_t s) {
     auto k = k_matvec<ACT, NORM, EPI, T, NP, T2>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
     a.split_pairs = split_pairs;
-    int w1 = (int)(((long long)g.x * split_pairs + a.npairs / 2) / a.npairs);
-    w1 = w1 < 1 ? 1 : w1 > (int)g.x - 1 ? (int)g.x - 1 : w1;
+    int w1;
+    if (g_split_by_pairs) {  // A/B: the round-1 deal by pair count
+        w1 = (int)(((long long)g.x * split_pairs + a.npairs / 2) / a.npairs);
+        w1 = w1 < 1 ? 1 : w1 > (int)g.x - 1 ? (int)g.x - 1 : w1;
+    } else {
+        w1 = split_groups((int)g.x, split_pairs, a.npairs - split_pairs, (double)tensor_bytes(T, 2, a.cols),
+                          (double)tensor_bytes(T2, 2, a.cols));
+    }
     a.split_wgs = w1;
     launch_k(k, g, dim3(kMVThreads), lds, s, true, true, a);
     return hipGetLastError();
