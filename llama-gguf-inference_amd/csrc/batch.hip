@@ -422,7 +422,7 @@ hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s) {
 // batch slot as the last grid dimension
 template <int D, int P, int S>
 __global__ __launch_bounds__(512) void k_battn_d(BAttnArgs b, int G, int HK, int kvb) {
-    attn_d_body<D, P, S>(b.a[blockIdx.y], G, HK, kvb, 1);
+    attn_d_body<D, P, S>(b.a[blockIdx.y], G, HK, kvb, 1, 1);
 }
 template <int D, int G, int NP>
 __global__ __launch_bounds__(256) void k_battl_scores(BAttnArgs b) { attl_scores_body<D, G, NP>(b.a[blockIdx.z]); }

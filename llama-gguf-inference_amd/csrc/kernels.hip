@@ -1148,7 +1148,9 @@ __global__ __launch_bounds__(D) void k_attl_sum(AttnArgs a, int n_head) { attl_s
 
 // Dim-split one-launch attention (path 6): body in mv_device.h (shared with batch.hip)
 template <int D, int P, int S>
-__global__ __launch_bounds__(512) void k_attn_d(AttnArgs a, int G, int HK, int kvb, int pf) { attn_d_body<D, P, S>(a, G, HK, kvb, pf); }
+__global__ __launch_bounds__(512) void k_attn_d(AttnArgs a, int G, int HK, int kvb, int pf) {
+    attn_d_body<D, P, S>(a, G, HK, kvb, pf & 1, (pf >> 1) & 1);
+}
 
 // ----------------------------------------------------------------------------------
 // Step entry: choose the token, advance pos, dequantize its embedding row
@@ -1587,7 +1589,7 @@ static int g_attn_s = 0;  // LLMI_ATTN_S (A/B only): force 2, 4 or 8 slices
 // k_attn_d reads the position before its K/V loads and skips those past it (default;
 // LLMI_ATTN_PF=0 loads the whole KV bucket, A/B only): ties at bucket ends, up to 1.4 us
 // faster mid-bucket (profiles/r02/attn_dim_split.md)
-static int g_attn_pf = 1;
+static int g_attn_pf = 3;
 int attn_d_slices(int n_head, int head_dim) {
     const int s = g_attn_s ? g_attn_s : n_head >= 128 ? 2 : n_head >= 64 ? 4 : 8;
     return head_dim / s >= 8 ? s : head_dim / 8;
@@ -1601,6 +1603,8 @@ void set_attn_mode(int mode) {
     g_attn_s = (v == 2 || v == 4 || v == 8) ? v : 0;
     const char* f = getenv("LLMI_ATTN_PF");
     g_attn_pf = f ? atoi(f) : 1;
+    const char* r = getenv("LLMI_ATTN_ROT");  // rotated K pass order (bit 1 of the word; default on)
+    if (!r || atoi(r)) g_attn_pf |= 2;
 }
 int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     const int g = n_head / n_head_kv;

@@ -1217,7 +1217,7 @@ __device__ __forceinline__ void attl_sum_body(const AttnArgs& a, int n_head) {
 // sum)), double PV); the per-position work and the PV lane split differ only in how the
 // exact double sums are associated.
 template <int D, int P, int S>
-__device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, int kvb, int pf = 0) {
+__device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, int kvb, int pf = 0, int rot_on = 0) {
     constexpr int DQ = D / 8;                    // score dims per lane
     constexpr int DS = D / S;                    // output dims of this workgroup
     constexpr int SLV = 512 / DS;                // PV lanes per output dim (<= 64)
@@ -1236,15 +1236,21 @@ __device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, in
     // branches on the position read first) instead of loading the whole KV bucket
     const int pos = a.st->pos;
     const int lim = pf ? pos + 1 : kvb;
+    // rot_on (the default): the workgroups of one KV group (one XCD) start their K passes
+    // at different positions, so the requests for a K row are spread over the issue window
+    // and the later ones hit that XCD's L2 (3-8 % faster, profiles/r02/attn_dim_split.md);
+    // register pass p holds positions 64 * pb(p) ...
+    const int rot = rot_on ? (b / HK) % P : 0;
+    auto pb = [&](int p) { return p + rot < P ? p + rot : p + rot - P; };
     float4 qv[DQ / 4];
 #pragma unroll
     for (int i = 0; i < DQ / 4; ++i) qv[i] = *(const float4*)(a.q + (size_t)h * D + qd * DQ + 4 * i);
     u32x4 kv[P][DQ / 8];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-        const int t = min(64 * p + pp, kvb - 1);
+        const int t = min(64 * pb(p) + pp, kvb - 1);
         const uint16_t* kr = a.kc + ((size_t)g * a.n_ctx + t) * D + qd * DQ;
-        if (64 * p < lim) {
+        if (64 * pb(p) < lim) {
 #pragma unroll
             for (int i = 0; i < DQ / 8; ++i) kv[p][i] = *(const u32x4*)(kr + 8 * i);
         } else {
@@ -1271,7 +1277,7 @@ __device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, in
     float m = -INFINITY;
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-        if (64 * p >= lim) break;  // uniform: passes past the position (pf only)
+        if (64 * pb(p) >= lim) continue;  // uniform: passes past the position (pf only)
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < DQ / 8; ++i)
@@ -1283,7 +1289,7 @@ __device__ __forceinline__ void attn_d_body(const AttnArgs& a, int G, int HK, in
         acc += xor_partner_d<1>(acc);
         acc += xor_partner_d<2>(acc);
         acc += xor_partner_d<4>(acc);
-        const int t = 64 * p + pp;
+        const int t = 64 * pb(p) + pp;
         const float sc = (float)acc * a.scale;
         if (qd == 0) sp[t] = sc;
         if (t < n_kv) m = fmaxf(m, sc);
