@@ -197,6 +197,27 @@ def test_prefill_attention_past_16k_positions(gpu, tiny_models, monkeypatch):
     _assert_same(grouped, steps)
 
 
+def test_prefill_attention_head_subgroups(gpu, synth_dir, monkeypatch):
+    """Llama-3-8B widths (2 layers, GQA 4), a 10500-token prompt: past ~10k positions the
+    four heads' scores no longer fit in LDS and the batched-prefill attention runs
+    sub-groups of 2 heads per workgroup.  Prefilled logits and the next decode steps equal
+    the one-head-per-workgroup kernel's and all-decode-step processing bit for bit."""
+    path = str(synth_dir / "llama3-8b-q4km-L2-sub.gguf")
+    llmi.write_synthetic_gguf(path, "llama3-8b-q4km", seed=21, n_layer=2)
+    rng = np.random.default_rng(17)
+    prompt = [1] + [int(t) for t in rng.integers(3, 120000, 10499)]
+    _, sub = _gpu_run(path, prompt, 10752, 2)
+    old = llmi.test_option("pf_attn_simple", 1)
+    try:
+        _, simple = _gpu_run(path, prompt, 10752, 2)
+    finally:
+        llmi.test_option("pf_attn_simple", old)
+    _assert_same(sub, simple)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    _, steps = _gpu_run(path, prompt, 10752, 2)
+    _assert_same(sub, steps)
+
+
 def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
     """k_attn_x's hand-off waits are bounded; with the bound lowered to 0 polls and the
     consumers waiting for a tag no producer writes (test options, captured into the step
