@@ -253,9 +253,7 @@ def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
     threads = max(1, min(phys, 16))
     om = po.OracleModel(path, n_ctx=len(prompt) + n_tokens + 2, threads=threads)
     t = time.perf_counter()
-    po.set_dot_order(po.DEVICE_ORDER)  # the fast batched path fills the KV rows (untimed)
-    om.prefill(prompt[:-1])
-    po.set_dot_order(po.GENERIC)
+    om.prefill(prompt[:-1])  # the batched path fills the KV rows (untimed)
     fill_s = time.perf_counter() - t
     lg = om.decode(prompt[-1], len(prompt) - 1)  # first step (page-in), untimed
     tok = int(np.argmax(lg))

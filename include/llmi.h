@@ -167,14 +167,6 @@ void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec
  * output(+argmax).  0 on success. */
 int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps,
                              double* us, double* bytes, int32_t* launches);
-/* 1 when a decode step at `pos` runs as the persistent one-launch step (step.hip: the
- * layer ops as phases of one kernel; opt-in: LLMI_STEP=1 at context creation), 0 when it
- * runs as per-op launches (the default; also past the in-launch attention's KV bound or
- * for shapes the step does not take).  Both give bit-identical results. */
-int32_t llmi_step_path(const struct llama_context* ctx, int32_t pos);
-/* Experiment builds (-DLLMI_EXP_TRACE): copy the persistent step's per-barrier stamps
- * [workgroup][512][arrive, release] (s_memrealtime, 100 MHz) of the last step; -1 otherwise. */
-int32_t llmi_step_trace_copy(struct llama_context* ctx, uint64_t* out, int64_t n);
 /* Test options (tests only; no environment variable reaches these): sets `name` to
  * `value` (value < 0: query) and returns the previous value, -1 for an unknown name.
  *   "pf_attn_simple"  1: batched-prefill attention one head per workgroup (bit-identical)

@@ -5,11 +5,9 @@
 // k_mvn is the matvec (kernels.hip k_matvec) with NT activation vectors: the prologue
 // quantizes the NT inputs into NT LDS images exactly as the single-token prologue does
 // (per-16 sub-block q8_K / q8_0, RMSNorm with a double sum); the main loop loads a row
-// pair's chunk once and forms NT integer dot products against it (the nibble / 6-bit
-// unpacking is shared), each token accumulated per lane in the matvec's order and
-// reduced by the same 64-lane butterfly — so every sequence's results are bit-identical
-// to its own single-token decode.  At NT = 8 the kernel does ~4x the VALU work of the
-// single-token matvec, still under the HBM time of the weight stream.
+// pair's chunk once and forms NT sets of block terms against it, each folded onto its
+// token's chains in ggml's generic order (mv_device.h) — so every sequence's results are
+// bit-identical to its own single-token decode.
 //
 // Attention runs the split kernels' bodies (mv_device.h) with a third grid dimension
 // over the batch slots, each slot reading its own sequence's KV cache.
@@ -121,75 +119,28 @@ __device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t) {
     return B;
 }
 
-// v of lane L ^ O for any values (not only butterfly-uniform ones): DPP quad_perm for 1
-// and 2, ds_swizzle bit mode within 32 lanes for 4 and 8, permlane swaps for 16 and 32
-template <int O>
-__device__ __forceinline__ float xor_any(float v) {
-    if constexpr (O == 1 || O == 2 || O == 16 || O == 32) return xor_partner<O>(v);
-    else return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (O << 10)));
-}
-
-// One reduce-scatter level over lane bit O: each lane keeps half of its H values (the
-// lower half when bit O is clear) and adds the partner's copy of the same half.  The
-// additions are the butterfly's (block sums of the two O-halves), so every value's
-// total is the single-token matvec's tree exactly; only which lane holds it changes.
-template <int O, int H>
-__device__ __forceinline__ void scatter_level(float (&v)[16]) {
-    const bool hi = (threadIdx.x & O) != 0;
-#pragma unroll
-    for (int j = 0; j < H / 2; ++j) {
-        const float send = hi ? v[j] : v[j + H / 2];
-        const float keep = hi ? v[j + H / 2] : v[j];
-        v[j] = keep + xor_any<O>(send);
-    }
-}
-
-// 2*NT per-lane partial sums (v[2t] row a, v[2t+1] row b of token t) -> the full 64-lane
-// sum of value idx(lane) in every lane: reduce-scatter over the low log2(2NT) lane bits,
-// then the butterfly over the rest.  idx = sum over scatter levels of (bit set ? H/2 : 0).
-template <int NT>
-__device__ __forceinline__ float reduce_scatter(float (&v)[16]) {
-    scatter_level<1, 2 * NT>(v);
-    if constexpr (NT >= 2) scatter_level<2, NT>(v);
-    if constexpr (NT >= 4) scatter_level<4, NT / 2>(v);
-    if constexpr (NT >= 8) scatter_level<8, NT / 4>(v);
-    float x = v[0];
-    if constexpr (NT < 2) x += xor_any<2>(x);
-    if constexpr (NT < 4) x += xor_any<4>(x);
-    if constexpr (NT < 8) x += xor_any<8>(x);
-    x += xor_any<16>(x);
-    x += xor_any<32>(x);
-    return x;
-}
-// the value index a lane holds after reduce_scatter<NT>: bits read from the lane from
-// the first scatter level (weight NT) down to the last (weight 1)
-template <int NT>
-__device__ __forceinline__ int scatter_idx(int lane) {
-    int idx = 0;
-#pragma unroll
-    for (int k = 0, w = NT; w >= 1; ++k, w >>= 1) idx += ((lane >> k) & 1) ? w : 0;
-    return idx;
-}
-
 }  // namespace
+
+// fold buffer floats per wave for NT tokens: [NT][2 rows][kFoldRow] + the chain results [NT][18]
+template <int NT>
+__host__ __device__ constexpr int mvn_fold_floats() { return NT * 2 * kFoldRow + ((NT * 18 + 3) & ~3); }
 
 template <int ACT, bool NORM, int EPI, int T, int NT>
 __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const size_t img = img_bytes(ACT, A.cols);
     double* red = (double*)(smem + NT * img);
+    constexpr int NC = ACT ? 1 : 9;   // chains per row
+    constexpr int NF = 2 * NC * NT;   // fold chains of the wave
+    constexpr int NU = (NF + 63) / 64;
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
+    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * mvn_fold_floats<NT>();
+    float* Gr = F + NT * 2 * kFoldRow;  // [NT][2 * NC] chain results
     const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
     const int G = gridDim.x * kBW;
-    // after the reduce-scatter, lane L holds row (idx & 1) of token idx >> 1; lanes
-    // 0..15 holding row a run their token's epilogue (one token per lane)
-    constexpr int RB = NT;  // lane bit (as a mask) that selects row a / row b
-    const int my_idx = scatter_idx<NT>(lane);
-    const int my_t = my_idx >> 1;
-    const bool ep_lane = lane < 2 * NT && (my_idx & 1) == 0;
-    const int my_pos = A.tpos ? A.tpos[my_t < NT ? my_t : 0] : 0;
-    unsigned long long best = 0;
+    const int my_pos = A.tpos ? A.tpos[lane < NT ? lane : 0] : 0;
+    unsigned long long best = 0;  // lane t < NT: token t's LOGITS key
     bprologue<ACT, NORM, NT>(A, smem, img, red);
 
     int p = blockIdx.x * kBW + wave;
@@ -198,9 +149,9 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
         PairRows<T> rows = pair_rows<T>(r, A.cols);
         PairRaw<T> cur = load_item<T>(rows, lane, nch);
         int j = 0;
-        float acc_a[NT], acc_b[NT];
+        float acc[NU];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc_a[t] = acc_b[t] = 0.f;
+        for (int u = 0; u < NU; ++u) acc[u] = 0.f;
         for (;;) {
             int pn = p, jn = j + 1;
             PairRef rn = r;
@@ -221,25 +172,59 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const Act act = load_act<ACT>(carve_t(smem, ACT, A.cols, t, img), chc, nch);
-                const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
-                acc_a[t] += ch < nch ? va : 0.f;
-                acc_b[t] += ch < nch ? vb : 0.f;
+                item_terms<T>(cur.a, act, chc, ch < nch, F + t * 2 * kFoldRow);
+                item_terms<T>(cur.b, act, chc, ch < nch, F + t * 2 * kFoldRow + kFoldRow);
+            }
+            wave_lds_sync();
+            {   // fold chain f = (token, row, chain) onto acc[u] of lane f - 64 u
+                const int nb = item_blocks<ACT>(A.cols, j);
+                constexpr int CS = ACT ? 128 : 16;
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int f = lane + 64 * u;
+                    if (f < NF) {
+                        const int t = f / (2 * NC), rr = f % (2 * NC), row = rr / NC, c = rr % NC;
+                        const float* q = F + t * 2 * kFoldRow + row * kFoldRow + c * CS;
+                        for (int b = 0; b < nb; b += 4) {
+                            const float4 v = *(const float4*)(q + b);
+                            acc[u] += v.x;
+                            if (b + 1 < nb) acc[u] += v.y;
+                            if (b + 2 < nb) acc[u] += v.z;
+                            if (b + 3 < nb) acc[u] += v.w;
+                        }
+                    }
+                }
             }
             if (j == NJ - 1) {
-                float v[16];
+                wave_lds_sync();
 #pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    v[2 * t] = acc_a[t];
-                    v[2 * t + 1] = acc_b[t];
-                    acc_a[t] = acc_b[t] = 0.f;
+                for (int u = 0; u < NU; ++u) {
+                    const int f = lane + 64 * u;
+                    if (f < NF) Gr[f] = acc[u];
+                    acc[u] = 0.f;
                 }
-                const float mine = reduce_scatter<NT>(v);
-                const float other = xor_any<RB>(mine);  // the same token's other row
-                if (ep_lane) {
-                    const MVArgs B = token_view(A, my_t);
-                    epilogue<EPI, false, MVArgs, true>(B, r, p, PairSum{mine, other}, my_pos, best);
+                wave_lds_sync();
+                if (lane < NT) {  // token `lane`: sumf chain + sums[0..7] of both rows, its epilogue
+                    const float* g = Gr + lane * 2 * NC;
+                    PairSum v;
+                    if constexpr (ACT) {
+                        v.a = g[0];
+                        v.b = g[1];
+                    } else {
+                        float sa = g[8], sb = g[17];
+#pragma unroll
+                        for (int l = 0; l < 8; ++l) {
+                            sa += g[l];
+                            sb += g[9 + l];
+                        }
+                        v.a = sa;
+                        v.b = sb;
+                    }
+                    const MVArgs B = token_view(A, lane);
+                    epilogue<EPI, false, MVArgs, true>(B, r, p, v, my_pos, best);
                 }
             }
+            wave_lds_sync();
             if (!has_next) break;
             cur = nxt;
             p = pn;
@@ -249,12 +234,12 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
         }
     }
     if constexpr (EPI == EPI_LOGITS) {
-        // per token: workgroup max of the waves' keys (each held by the token's epilogue
-        // lane), one atomic into the slot of its sequence's StepState; workgroup 0
-        // advances the sequence's next position
+        // per token: workgroup max of the waves' keys (lane t holds token t's), one atomic
+        // into the slot of its sequence's StepState; workgroup 0 advances the sequence's
+        // next position
         unsigned long long* wred = (unsigned long long*)red;  // [kBW][NT]
         __syncthreads();
-        if (ep_lane) wred[wave * NT + my_t] = best;
+        if (lane < NT) wred[wave * NT + lane] = best;
         __syncthreads();
         if ((int)threadIdx.x < NT) {
             const int t = threadIdx.x;
@@ -312,7 +297,10 @@ __global__ __launch_bounds__(512) void k_battn_pv16(BAttnArgs b, int kvb) {
 }
 
 // ---- launchers -----------------------------------------------------------------------------
-size_t mvn_lds_bytes(int act, int cols, int nt) { return (size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8; }
+size_t mvn_lds_bytes(int act, int cols, int nt) {
+    const size_t fold = (size_t)nt * 2 * kFoldRow + (size_t)((nt * 18 + 3) & ~3);
+    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * fold * 4;
+}
 
 template <typename K>
 static int mvn_grid(K kernel, int npairs, size_t lds, int max_blocks) {

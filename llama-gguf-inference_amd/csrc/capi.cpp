@@ -582,24 +582,6 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
     API_CATCH(-5)
 }
 
-int32_t llmi_step_path(const struct llama_context* ctx, int32_t pos) {
-    if (!ctx || pos < 0) return -1;
-    const Context& c = ctx->c;
-    if (!c.use_step) { set_err("persistent step off (LLMI_STEP=0 or mixed gate/up types)"); return 0; }
-    const int kv_bound = std::min(c.n_ctx, (pos / 256 + 1) * 256);
-    std::string why;
-    if (step_supported(step_args(c, kv_bound), c.device, &why)) return 1;
-    set_err("persistent step not taken: " + why);
-    return 0;
-}
-
-int32_t llmi_step_trace_copy(struct llama_context* ctx, uint64_t* out, int64_t n) {
-    if (!ctx || !out || !ctx->c.step_trace) { set_err("llmi_step_trace_copy: not an LLMI_EXP_TRACE build"); return -1; }
-    const int64_t cap = (int64_t)1024 * 512 * 2;
-    (void)hipSetDevice(ctx->c.device);
-    if (hipMemcpy(out, ctx->c.step_trace, (size_t)std::min(n, cap) * 8, hipMemcpyDeviceToHost) != hipSuccess) return -2;
-    return 0;
-}
 
 int32_t llmi_test_option(const char* name, int32_t value) {
     if (!name) return -1;

@@ -52,7 +52,7 @@ Context::~Context() {
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
     void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad,
-                    step_mv, step_bar, step_trace, bx, bq, batt, bh, blogits, bscores, btpos, btseq};
+                    bx, bq, batt, bh, blogits, bscores, btpos, btseq};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -389,52 +389,6 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, int n_seq, Context& c, s
     }
     HIPC(hipMalloc(&c.rope, tab.size() * 4));
     HIPC(hipMemcpy(c.rope, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-    // persistent step: the phase table (the per-op launches' matvec descriptors)
-    {   // the persistent step is an opt-in A/B path: measured slower than the per-op
-        // launches on MI355X ("persistent step"), results bit-identical
-        const char* e = getenv("LLMI_STEP");
-        c.use_step = e && atoi(e) == 1;
-    }
-    {
-        const Model& M = *m;
-        const int E = hp.n_embd, D = hp.head_dim, nq = hp.n_head * D, nk = hp.n_head_kv * D;
-        const size_t kv_layer = (size_t)hp.n_head_kv * c.n_ctx * D;
-        std::vector<MVArgs> tab2((size_t)hp.n_layer * 4 + 1);
-        auto seg = [&](const DevMat& d, int row0) {
-            Seg s;
-            s.a = M.arena + d.off_a; s.h = M.arena + d.off_h; s.s = M.arena + d.off_s; s.d = M.arena + d.off_d;
-            s.type = d.type; s.rows = (int)d.rows; s.row0 = row0;
-            return s;
-        };
-        for (int l = 0; l < hp.n_layer; ++l) {
-            const Layer& L = M.layers[(size_t)l];
-            MVArgs& a = tab2[(size_t)l * 4 + 0];
-            a.seg[0] = seg(L.wq, 0); a.seg[1] = seg(L.wk, nq); a.seg[2] = seg(L.wv, nq + nk); a.nseg = 3;
-            a.cols = E; a.x = c.x; a.nw = (const float*)(M.arena + L.attn_norm.off_a); a.eps = hp.eps; a.y = c.q;
-            a.kc = c.kc + l * kv_layer; a.vc = c.vc + l * kv_layer; a.rope = c.rope; a.st = c.st;
-            a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = nq; a.nk = nk; a.npairs = (nq + 2 * nk) / 2;
-            MVArgs& o = tab2[(size_t)l * 4 + 1];
-            o.seg[0] = seg(L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
-            MVArgs& gu = tab2[(size_t)l * 4 + 2];
-            gu.seg[0] = seg(L.wg, 0); gu.seg[1] = seg(L.wu, 0); gu.nseg = 2; gu.cols = E; gu.x = c.x;
-            gu.nw = (const float*)(M.arena + L.ffn_norm.off_a); gu.eps = hp.eps; gu.y = c.h; gu.npairs = hp.n_ff;
-            MVArgs& dn = tab2[(size_t)l * 4 + 3];
-            dn.seg[0] = seg(L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
-            if (L.wg.type != L.wu.type) c.use_step = false;  // mixed gate/up types: per-op launches
-        }
-        MVArgs& lo = tab2[(size_t)hp.n_layer * 4];
-        lo.seg[0] = seg(M.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
-        lo.nw = (const float*)(M.arena + M.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
-        lo.npairs = (hp.n_vocab + 1) / 2; lo.st = c.st;
-        HIPC(hipMalloc(&c.step_mv, tab2.size() * sizeof(MVArgs)));
-        HIPC(hipMemcpy(c.step_mv, tab2.data(), tab2.size() * sizeof(MVArgs), hipMemcpyHostToDevice));
-        HIPC(hipMalloc(&c.step_bar, kStepBarWords * 4));
-        HIPC(hipMemsetAsync(c.step_bar, 0, kStepBarWords * 4, c.stream));
-#if defined(LLMI_EXP_TRACE)
-        HIPC(hipMalloc(&c.step_trace, (size_t)1024 * 512 * 2 * 8));
-        HIPC(hipMemsetAsync(c.step_trace, 0, (size_t)1024 * 512 * 2 * 8, c.stream));
-#endif
-    }
     context_clear(c);
     HIPC(hipStreamSynchronize(c.stream));
     return true;
@@ -654,51 +608,17 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     return true;
 }
 
-StepArgs step_args(const Context& c, int kv_bound) {
-    const Model& m = *c.m;
-    const HParams& hp = m.hp;
-    StepArgs a;
-    a.mv = c.step_mv; a.n_layer = hp.n_layer;
-    a.out = seg_of(m, m.output, 0); a.onorm = (const float*)(m.arena + m.out_norm.off_a);
-    a.E = hp.n_embd; a.F = hp.n_ff; a.H = hp.n_head; a.HK = hp.n_head_kv; a.D = hp.head_dim; a.n_rot = hp.n_rot;
-    a.n_ctx = c.n_ctx; a.V = hp.n_vocab; a.eps = hp.eps; a.scale = 1.0f / sqrtf((float)hp.head_dim);
-    a.x = c.x; a.q = c.q; a.att = c.att; a.h = c.h; a.logits = c.logits;
-    a.scores = c.scores; a.tmax = c.scores + (size_t)hp.n_head * c.n_ctx;
-    a.kc = c.kc; a.vc = c.vc; a.rope = c.rope; a.st = c.st; a.hist = c.hist;
-    a.bar = c.step_bar; a.fault = c.fault_dev; a.kv_bound = kv_bound; a.trace = c.step_trace;
-    return a;
-}
-
-// one decode step as [k_embed, memset of the barrier shards, k_step] when the persistent
-// step takes this KV bound, else the per-op launches
-static bool step_enqueue_any(Context& c, int kv_bound, std::string& err) {
-    if (c.use_step && c.cur_seq == 0) {
-        const StepArgs a = step_args(c, kv_bound);
-        if (step_supported(a, c.device, nullptr)) {
-            EmbArgs ea;
-            ea.w = seg_of(*c.m, c.m->tok_embd, 0);
-            ea.cols = c.m->hp.n_embd; ea.vocab = c.m->hp.n_vocab; ea.x = c.x; ea.st = c.st; ea.hist = c.hist;
-            ea.n_ctx = c.n_ctx;
-            hipError_t e = launch_embed(ea, c.stream);
-            if (e == hipSuccess) e = launch_step(a, c.stream);
-            if (e != hipSuccess) { err = "persistent step launch: " + hip_err(e); return false; }
-            return true;
-        }
-    }
-    return step_enqueue(c, kv_bound, err);
-}
-
 bool step_run(Context& c, int pos, std::string& err) {
     const int bucket = pos / 256;
     const int kv_bound = std::min(c.n_ctx, (bucket + 1) * 256);
-    if (!c.use_graphs) return step_enqueue_any(c, kv_bound, err);
+    if (!c.use_graphs) return step_enqueue(c, kv_bound, err);
     const int gkey = bucket * 256 + c.cur_seq;
     auto it = c.graphs.find(gkey);
     if (it == c.graphs.end()) {
         hipGraph_t g = nullptr;
         HIPC(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
         std::string e2;
-        const bool ok = step_enqueue_any(c, kv_bound, e2);
+        const bool ok = step_enqueue(c, kv_bound, e2);
         hipError_t ec = hipStreamEndCapture(c.stream, &g);
         if (!ok) { err = "capture: " + e2; if (g) (void)hipGraphDestroy(g); return false; }
         if (ec != hipSuccess) { err = "hipStreamEndCapture: " + hip_err(ec); return false; }

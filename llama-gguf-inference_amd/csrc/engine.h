@@ -83,11 +83,6 @@ struct Context {
     bool use_graphs = true;
     hipStream_t stream = nullptr;
     int max_blocks = 1024;
-    // persistent step (step.hip): one launch per token while the KV bound allows it
-    bool use_step = false;                  // LLMI_STEP=1 at context creation: persistent step
-    MVArgs* step_mv = nullptr;              // device table of the matvec phases
-    unsigned* step_bar = nullptr;           // barrier shards
-    unsigned long long* step_trace = nullptr;  // LLMI_EXP_TRACE builds: per-barrier stamps
     // device
     float *x = nullptr, *q = nullptr, *att = nullptr, *h = nullptr, *logits = nullptr, *scores = nullptr;
     float* rope = nullptr;
@@ -133,8 +128,6 @@ void context_clear_seq(Context& c, int s);
 bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err);
 // enqueue one decode step for a state already set (token_in/pos_next); kv_bound >= pos+1
 bool step_enqueue(Context& c, int kv_bound, std::string& err);
-// the persistent step's arguments for a KV bound (step.hip)
-StepArgs step_args(const Context& c, int kv_bound);
 // run one step via the cached graph of its KV bucket (or eagerly)
 bool step_run(Context& c, int pos, std::string& err);
 double bytes_per_token(const Model& m, int n_kv);

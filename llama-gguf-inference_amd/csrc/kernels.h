@@ -153,33 +153,6 @@ struct PfAttn {
     int n_ctx = 0, pos0 = 0, gqa = 1, max_kv = 0;  // max_kv >= pos0 + T (LDS score space)
     float scale = 0.f;
 };
-// Persistent decode step (step.hip): one launch per token, the layer ops as phases
-// separated by in-launch grid barriers, the next phase's weights in flight across each
-// barrier.  The phases' matvec descriptors are a device-side table built at context
-// creation (the per-op launches' MVArgs, unchanged).
-struct StepArgs {
-    const MVArgs* mv = nullptr;     // device table of the matvec phases: [layer][QKV, O, gate/up, down], output
-    int n_layer = 0;
-    Seg out;                        // output
-    const float* onorm = nullptr;   // output_norm
-    int E = 0, F = 0, H = 0, HK = 0, D = 0, n_rot = 0, n_ctx = 0, V = 0;
-    float eps = 0.f, scale = 0.f;
-    float *x = nullptr, *q = nullptr, *att = nullptr, *h = nullptr, *logits = nullptr;
-    float *scores = nullptr, *tmax = nullptr;
-    uint16_t *kc = nullptr, *vc = nullptr;
-    const float* rope = nullptr;
-    StepState* st = nullptr;
-    int32_t* hist = nullptr;
-    unsigned* bar = nullptr;        // barrier shards [kStepBarWords] u32, zeroed before every launch
-    unsigned* fault = nullptr;      // context fault word (a bounded wait gave up)
-    int kv_bound = 0;
-    unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [workgroup][512][arrive, release]
-};
-constexpr int kStepBarWords = 9 * 16;
-// can the persistent step run this model / KV bound on this device (residency, LDS)?
-bool step_supported(const StepArgs& a, int device, std::string* why);
-hipError_t launch_step(const StepArgs& a, hipStream_t s);
-
 bool pf_gemm_ok(int type, int rows, int cols);
 hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* toks, float* X, int T, int32_t* hist,
                            int pos0, int n_ctx, hipStream_t s);

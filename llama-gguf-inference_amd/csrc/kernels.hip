@@ -56,12 +56,21 @@ static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s,
 
 static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_SPLIT_BY_PAIRS")) : 0;  // A/B only
 
-size_t mv_lds_bytes(int act, int cols) { return lds_red_off(act, cols) + kMVWaves * sizeof(double); }
+// LDS of a matvec workgroup: the activation image, the prologue's reduction slots, then
+// one fold buffer (mv_device.h kFoldFloats) per wave
+__host__ __device__ inline size_t fold_off(int act, int cols, int waves) {
+    return a16(lds_red_off(act, cols) + (size_t)waves * sizeof(double));
+}
+size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + (size_t)kMVWaves * kFoldFloats * 4; }
 
 // The matvec of the pair range [pbeg, pend) by waves starting at pair p0 with stride G
-// (one type group of a launch); returns the wave's LOGITS argmax key.
+// (one type group of a launch); returns the wave's LOGITS argmax key.  Per item (pair
+// p, chunks lane + 64 j): the two rows' block terms into the wave's fold buffer F, the
+// 18 fold lanes add them onto their chains; after the pair's last item both row sums
+// (ggml's generic order, mv_device.h) go to the epilogue.
 template <int ACT, bool NORM, int EPI, int T, int NP>
-__device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, int p0, int G, int pbeg, int pend) {
+__device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int p0, int G, int pbeg,
+                                                      int pend) {
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
@@ -100,17 +109,12 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     }
     PairRaw<T> cur = load_item<T>(rows, lane, nch);
 #if defined(LLMI_EXP_TRACE)
-    // stamp once this wave's activation registers have arrived (forces the wait here)
     asm volatile("" ::"v"(R.x[0][0]), "v"(R.x[0][15]));
     tr_x = __builtin_amdgcn_s_memrealtime();
 #endif
-#if !defined(LLMI_EXP_NOPRO)
     mv_prologue_finish<ACT, NORM, NP>(A, L, R);
 #if defined(LLMI_EXP_TRACE)
     tr_q = __builtin_amdgcn_s_memrealtime();
-#endif
-#else
-    if (R.x[0][0] == 1234.5f) L.d[0] = R.x[0][1];
 #endif
     __syncthreads();
 #if defined(LLMI_EXP_TRACE)
@@ -119,7 +123,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
 
     if (pipe) {
         int j = 0;
-        float acc_a = 0.f, acc_b = 0.f;
+        float acc = 0.f;  // fold lane: its chain of the current pair
         for (;;) {
             // next work item: (p, j+1) or (p+G, 0); uniform control flow
             int pn = p, jn = j + 1;
@@ -139,21 +143,18 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             const int ch = lane + 64 * j;
             const int chc = ch < nch ? ch : nch - 1;
             const Act act = load_act<ACT>(L, chc, nch);
-#if defined(LLMI_EXP_NODOT)
-            const float va = (float)(cur.a.q0.x ^ cur.a.q1.y ^ cur.a.hdr.x), vb = (float)(cur.b.q0.x ^ cur.b.q1.y ^ cur.b.hdr.x);
-            (void)act;
-#else
-            const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
-#endif
-            acc_a += ch < nch ? va : 0.f;
-            acc_b += ch < nch ? vb : 0.f;
+            item_terms<T>(cur.a, act, chc, ch < nch, F);
+            item_terms<T>(cur.b, act, chc, ch < nch, F + kFoldRow);
+            wave_lds_sync();
+            fold_item<ACT>(F, item_blocks<ACT>(A.cols, j), acc);
             if (j == NJ - 1) {
-                epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
-                acc_a = acc_b = 0.f;
+                epilogue<EPI>(A, r, p, fold_final<ACT>(F, acc), pos, best);
+                acc = 0.f;
 #if defined(LLMI_EXP_TRACE)
                 if (tr_items++ == 0) tr2 = __builtin_amdgcn_s_memrealtime();
 #endif
             }
+            wave_lds_sync();  // the fold lanes' reads before the next item's stores
             if (!has_next) {
                 p = pn;
                 break;
@@ -168,9 +169,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     // remaining pairs of other types (or all pairs if the first was not of type T)
     for (; p < pend; p += G) {
         r = pair_ref<EPI>(A, p);
-        const float acc_a = generic_row_any<ACT>(r.sa.type, r.sa, r.ra, A.cols, L);
-        const float acc_b = r.vb ? generic_row_any<ACT>(r.sb.type, r.sb, r.rb, A.cols, L) : 0.f;
-        epilogue<EPI>(A, r, p, reduce_pair(acc_a, acc_b), pos, best);
+        epilogue<EPI>(A, r, p, pair_any<ACT>(r, A.cols, L, F), pos, best);
     }
 #if defined(LLMI_EXP_TRACE)
     if (A.trace && lane == 0) {
@@ -187,97 +186,6 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     return best;
 }
 
-// 3-deep register ring (experiment build -DLLMI_MV_RING=1; off by default): the same
-// items in the same order with the same arithmetic as mv_body (bit-identical, tested),
-// but each wave keeps the NEXT TWO items' weights in flight while it reduces one.
-// Buffers A, B, C are reloaded in place (the loop is unrolled by 3), so no register copy
-// forces a wait on a load just issued.  Measured (profiles/r02/matvec_ring.md): output
-// head 80.0 -> 76-77 us, gate+up 17.0 -> 16.8 us, but QKV 5.8 -> 8.3 and attn_output
-// 5.4 -> 7.6 us (the dummy ring loads of single-round launches delay their prologue);
-// end to end 604 -> 553 tok/s.  Per-wave stamps show the matvec is bound by the
-// dispatch ramp (waves start over 1.9 us), the 2.4 us prologue and a 3 us exit spread,
-// not by the in-flight depth.
-#ifndef LLMI_MV_RING
-#define LLMI_MV_RING 0
-#endif
-template <int ACT, bool NORM, int EPI, int T, int NP>
-__device__ __forceinline__ unsigned long long mv_body3(const MVArgs& A, const Lds& L, int p0, int G, int pbeg, int pend) {
-    int pos = 0;
-    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
-    unsigned long long best = 0;
-    const int lane = threadIdx.x & 63;
-    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
-    const uint8_t* xb = (const uint8_t*)A.x;
-    const RowPtr dummy{xb, xb, xb, xb};
-    ProRegs<NORM, NP> R;
-    mv_prologue_issue<NORM, NP>(A, R);  // activation loads first (see mv_body)
-    if (pend - pbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // load cursor (pl, jl) and compute cursor (pc, jc); pstop = first pair of this wave
-    // that is not of type T (it and the pairs after it go to the generic loop below)
-    int pl = p0, jl = 0, pc = p0, jc = 0, pstop = pend;
-    float acc_a = 0.f, acc_b = 0.f;
-#define MV_LOAD(X)                                                                     \
-    {                                                                                  \
-        PairRows<T> rows_;                                                             \
-        rows_.a = rows_.b = dummy;                                                     \
-        int jj_ = 0;                                                                   \
-        if (pl < pstop) {                                                              \
-            const PairRef r_ = pair_ref<EPI>(A, pl);                                   \
-            if (r_.type == T) {                                                        \
-                rows_ = pair_rows<T>(r_, A.cols);                                      \
-                jj_ = jl;                                                              \
-            } else {                                                                   \
-                pstop = pl;                                                            \
-            }                                                                          \
-        }                                                                              \
-        X = load_item<T>(rows_, lane + 64 * jj_, nch);                                 \
-        if (pl < pstop) {                                                              \
-            if (++jl == NJ) { jl = 0; pl += G; }                                       \
-        }                                                                              \
-    }
-#define MV_STEP(X)                                                                     \
-    {                                                                                  \
-        if (pc < pstop) {                                                              \
-            const int ch_ = lane + 64 * jc;                                            \
-            const int chc_ = ch_ < nch ? ch_ : nch - 1;                                \
-            const Act act_ = load_act<ACT>(L, chc_, nch);                              \
-            const float va_ = dot_chunk<T>(X.a, act_, chc_), vb_ = dot_chunk<T>(X.b, act_, chc_); \
-            acc_a += ch_ < nch ? va_ : 0.f;                                            \
-            acc_b += ch_ < nch ? vb_ : 0.f;                                            \
-            if (jc == NJ - 1) {                                                        \
-                epilogue<EPI>(A, pair_ref<EPI>(A, pc), pc, reduce_pair(acc_a, acc_b), pos, best); \
-                acc_a = acc_b = 0.f;                                                   \
-                jc = 0;                                                                \
-                pc += G;                                                               \
-            } else {                                                                   \
-                ++jc;                                                                  \
-            }                                                                          \
-        }                                                                              \
-        MV_LOAD(X);                                                                    \
-    }
-    PairRaw<T> bA, bB, bC;
-    MV_LOAD(bA);  // the first three items in flight during the prologue
-    MV_LOAD(bB);
-    MV_LOAD(bC);
-    mv_prologue_finish<ACT, NORM, NP>(A, L, R);
-    __syncthreads();
-    while (pc < pstop) {
-        MV_STEP(bA);
-        MV_STEP(bB);
-        MV_STEP(bC);
-    }
-#undef MV_STEP
-#undef MV_LOAD
-    // pairs of other types (mixed-type segments): one at a time
-    for (int p = pc; p < pend; p += G) {
-        const PairRef r = pair_ref<EPI>(A, p);
-        const float a = generic_row_any<ACT>(r.sa.type, r.sa, r.ra, A.cols, L);
-        const float b = r.vb ? generic_row_any<ACT>(r.sb.type, r.sb, r.rb, A.cols, L) : 0.f;
-        epilogue<EPI>(A, r, p, reduce_pair(a, b), pos, best);
-    }
-    return best;
-}
-
 // A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
 // split by workgroup: workgroups [0, split_wgs) run the pairs of type T, the rest the
 // pairs of type T2, each group pipelined in its own type (no divergence in a workgroup).
@@ -287,23 +195,18 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     const Lds L = carve(smem, ACT, A.cols);
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
+    float* F = (float*)(smem + fold_off(ACT, A.cols, kMVWaves)) + wave * kFoldFloats;
     unsigned long long best;
-#if LLMI_MV_RING && !defined(LLMI_EXP_TRACE)
-#define MV_BODY mv_body3
-#else
-#define MV_BODY mv_body
-#endif
     if constexpr (T2 == T) {
-        best = MV_BODY<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.npairs);
+        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.npairs);
     } else {
         if ((int)blockIdx.x < A.split_wgs)
-            best = MV_BODY<ACT, NORM, EPI, T, NP>(A, L, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
+            best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
                                                   A.split_pairs);
         else
-            best = MV_BODY<ACT, NORM, EPI, T2, NP>(A, L, A.split_pairs + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
+            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, F, A.split_pairs + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
                                                    (gridDim.x - A.split_wgs) * kMVWaves, A.split_pairs, A.npairs);
     }
-#undef MV_BODY
     if constexpr (EPI == EPI_LOGITS) {
         // workgroup max of the waves' keys, then one atomic into this workgroup's slot
         const int cur_pos = A.st->pos;
@@ -325,29 +228,32 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
 // ffn_down, 70B-wide inputs).  A workgroup's 16 waves form 16/KS pair slots of KS waves;
 // the waves of a slot split the pair's items (wave sub takes items sub, sub+KS, ...),
 // so every item of the first pair is in flight during the prologue, instead of one
-// item per wave with the rest fetched serially after it.  Per-lane item values go to
-// LDS; the slot's wave 0 adds them in item order starting from 0.f — exactly the
-// single-wave loop's `acc += item value` sequence, so the fp32 association (the
-// oracle's device order) is unchanged — then runs the butterfly and the epilogue.
-// LDS part buffer double-buffered by round: one barrier per round.
+// item per wave with the rest fetched serially after it.  KS >= 2: each wave writes its
+// items' block terms to the slot's part buffer P[slot][item]; after the round's barrier
+// the slot's wave 0 folds the items in order (the generic order runs over the row's
+// blocks in sequence) and runs the epilogue.  KS = 1: one wave per pair folds each item
+// as it goes, as k_matvec does (no part buffer, no barrier).
 constexpr int kKSThreads = 1024, kKSWaves = kKSThreads / 64;  // one workgroup per CU
+__host__ __device__ inline size_t ks_part_off(int act, int cols) {
+    return fold_off(act, cols, kKSWaves) + (size_t)kKSWaves * kFoldFloats * 4;
+}
 template <int KS>
 __host__ __device__ inline size_t ks_part_bytes(int cols) {
     const int nj = ((cols >> 6) + 63) >> 6;
-    return (size_t)2 * (kKSWaves / KS) * nj * 128 * sizeof(float);
+    return KS == 1 ? 0 : (size_t)(kKSWaves / KS) * nj * 2 * kFoldRow * sizeof(float);
 }
-__host__ __device__ inline size_t ks_part_off(int act, int cols) { return a16(lds_red_off(act, cols) + kKSWaves * sizeof(double)); }
 
 template <int ACT, bool NORM, int EPI, int T, int NP, int KS>
 __global__ __launch_bounds__(kKSThreads) void k_matvec_ks(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Lds L = carve(smem, ACT, A.cols);
-    float* part = (float*)(smem + ks_part_off(ACT, A.cols));  // [2][PPW][NJ][2][64]
     constexpr int PPW = kKSWaves / KS;
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int slot = wave / KS, sub = wave % KS;
     const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+    float* F = (float*)(smem + fold_off(ACT, A.cols, kKSWaves)) + wave * kFoldFloats;
+    float* part = (float*)(smem + ks_part_off(ACT, A.cols)) + (size_t)slot * NJ * 2 * kFoldRow;  // [NJ][2][kFoldRow]
     const int stride = gridDim.x * PPW;
     const int rounds = (A.npairs + stride - 1) / stride;
     int pos = 0;
@@ -366,10 +272,9 @@ __global__ __launch_bounds__(kKSThreads) void k_matvec_ks(MVArgs A) {
     mv_prologue_finish<ACT, NORM, NP, kKSThreads>(A, L, R);
     __syncthreads();
 
-    int buf = 0;
     for (int rd = 0; rd < rounds; ++rd, pr += stride) {
         const bool have = pr < A.npairs;
-        float* pb = part + (size_t)(buf * PPW + slot) * NJ * 128;
+        float acc = 0.f;
         for (int j = sub; j < NJ; j += KS) {
             // the wave's next item: (pr, j+KS) or (pr+stride, sub); loads always issued
             int jn = j + KS, prn = pr;
@@ -385,23 +290,28 @@ __global__ __launch_bounds__(kKSThreads) void k_matvec_ks(MVArgs A) {
                 const int ch = lane + 64 * j;
                 const int chc = ch < nch ? ch : nch - 1;
                 const Act act = load_act<ACT>(L, chc, nch);
-                const float va = dot_chunk<T>(cur.a, act, chc), vb = dot_chunk<T>(cur.b, act, chc);
-                pb[j * 128 + lane] = ch < nch ? va : 0.f;
-                pb[j * 128 + 64 + lane] = ch < nch ? vb : 0.f;
+                float* P = KS == 1 ? F : part + (size_t)j * 2 * kFoldRow;
+                item_terms<T>(cur.a, act, chc, ch < nch, P);
+                item_terms<T>(cur.b, act, chc, ch < nch, P + kFoldRow);
+                if constexpr (KS == 1) {
+                    wave_lds_sync();
+                    fold_item<ACT>(F, item_blocks<ACT>(A.cols, j), acc);
+                    wave_lds_sync();
+                }
             }
             cur = nxt;
             rows = rowsn;
         }
-        __syncthreads();
-        if (sub == 0 && have) {
-            float acc_a = 0.f, acc_b = 0.f;
-            for (int j = 0; j < NJ; ++j) {
-                acc_a += pb[j * 128 + lane];
-                acc_b += pb[j * 128 + 64 + lane];
+        if constexpr (KS == 1) {
+            if (have) epilogue<EPI>(A, pair_ref<EPI>(A, pr), pr, fold_final<ACT>(F, acc), pos, best);
+        } else {
+            __syncthreads();
+            if (sub == 0 && have) {
+                for (int j = 0; j < NJ; ++j) fold_item<ACT>(part + (size_t)j * 2 * kFoldRow, item_blocks<ACT>(A.cols, j), acc);
+                epilogue<EPI>(A, pair_ref<EPI>(A, pr), pr, fold_final<ACT>(F, acc), pos, best);
             }
-            epilogue<EPI>(A, pair_ref<EPI>(A, pr), pr, reduce_pair(acc_a, acc_b), pos, best);
+            __syncthreads();
         }
-        buf ^= 1;
     }
     if constexpr (EPI == EPI_LOGITS) {
         const int cur_pos = A.st->pos;
@@ -431,9 +341,9 @@ __global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* ou
     const int nch = cols >> 6;
     for (int e = threadIdx.x; e < cols; e += blockDim.x) {
         const int ch = e >> 6, t = e & 63;
-        if (ACT == 0) {
-            const int k = (t & 31) >> 4;
-            const int8_t qv = (int8_t)((t < 32 ? L.lo : L.hi)[16 * (k * nch + ch) + (t & 15)]);
+        if (ACT == 0) {  // residue order: element t = 32 h + l + 8 i at part l / 4, byte 4 (l % 4) + i
+            const int l = t & 7, i = (t & 31) >> 3;
+            const int8_t qv = (int8_t)((t < 32 ? L.lo : L.hi)[16 * ((l >> 2) * nch + ch) + 4 * (l & 3) + i]);
             out[(size_t)(e >> 8) * 292 + 4 + (e & 255)] = (uint8_t)qv;
         } else {
             out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = L.lo[16 * ((t >> 4) * nch + ch) + (t & 15)];
@@ -1210,21 +1120,25 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
     if (b >= nblk) return;
     const int64_t row = b / nbr, bi = b % nbr, nch = (int64_t)nbr * 4, ch = bi * 4 + c;
     uint8_t* arow = A + row * nch * 32;
+    // residue order: byte 4m + i of part k holds chunk elements t = l + 8i (low nibble)
+    // and 32 + t (high nibble), l = 4k + m
     if (type == T_Q4_K || type == T_Q5_K) {
         const int bb = type == T_Q4_K ? 144 : 176;
         const uint8_t* x = raw + b * bb;
         const uint8_t* qs = x + (type == T_Q4_K ? 16 : 48);
         for (int k = 0; k < 2; ++k)
-            for (int i = 0; i < 16; ++i) arow[(k * nch + ch) * 16 + i] = qs[32 * c + 16 * k + i];
+            for (int m = 0; m < 4; ++m)
+                for (int i = 0; i < 4; ++i) arow[(k * nch + ch) * 16 + 4 * m + i] = qs[32 * c + 4 * k + m + 8 * i];
         if (c == 0)
             for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[i];
-        if (type == T_Q5_K) {  // bit l of the lo word: qh[l] bit 2c; hi word: bit 2c+1
+        if (type == T_Q5_K) {  // bit 4l + i of the lo word: qh[l + 8i] bit 2c; hi word: bit 2c+1
             const uint8_t* qh = x + 16;
             uint32_t lo = 0, hi = 0;
-            for (int l = 0; l < 32; ++l) {
-                lo |= (uint32_t)((qh[l] >> (2 * c)) & 1) << l;
-                hi |= (uint32_t)((qh[l] >> (2 * c + 1)) & 1) << l;
-            }
+            for (int l = 0; l < 8; ++l)
+                for (int i = 0; i < 4; ++i) {
+                    lo |= (uint32_t)((qh[l + 8 * i] >> (2 * c)) & 1) << (4 * l + i);
+                    hi |= (uint32_t)((qh[l + 8 * i] >> (2 * c + 1)) & 1) << (4 * l + i);
+                }
             uint8_t* h = H + (row * nch + ch) * 8;
             for (int k = 0; k < 4; ++k) { h[k] = (uint8_t)(lo >> (8 * k)); h[4 + k] = (uint8_t)(hi >> (8 * k)); }
         }
@@ -1240,17 +1154,20 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
             return lo | (hi << 4);
         };
         for (int k = 0; k < 2; ++k)
-            for (int i = 0; i < 16; ++i) {
-                const int t = 16 * k + i;
-                arow[(k * nch + ch) * 16 + i] = (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
-            }
-        // H dword g = 2*hi + k: byte j bits [2m, 2m+1] = high2 of chunk weight 32*hi + 16k + 4m + j
+            for (int m = 0; m < 4; ++m)
+                for (int i = 0; i < 4; ++i) {
+                    const int t = 4 * k + m + 8 * i;
+                    arow[(k * nch + ch) * 16 + 4 * m + i] = (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
+                }
+        // H dword g = 2*hi + k: byte i bits [2m, 2m+1] = (high 2 bits of chunk element
+        // 32*hi + 4k + m + 8i) XOR 2, which v_perm turns into the high part of q - 32
         uint8_t* h = H + (row * nch + ch) * 16;
         for (int g = 0; g < 4; ++g)
-            for (int j = 0; j < 4; ++j) {
+            for (int i = 0; i < 4; ++i) {
                 uint8_t v = 0;
-                for (int m = 0; m < 4; ++m) v |= (uint8_t)((u6(64 * c + 32 * (g >> 1) + 16 * (g & 1) + 4 * m + j) >> 4) << (2 * m));
-                h[4 * g + j] = v;
+                for (int m = 0; m < 4; ++m)
+                    v |= (uint8_t)(((u6(64 * c + 32 * (g >> 1) + 4 * (g & 1) + m + 8 * i) >> 4) ^ 2) << (2 * m));
+                h[4 * g + i] = v;
             }
         for (int i = 0; i < 4; ++i) S[b * 16 + 4 * c + i] = x[192 + 4 * c + i];
         if (c == 0) { Dp[b * 2] = x[208]; Dp[b * 2 + 1] = x[209]; }

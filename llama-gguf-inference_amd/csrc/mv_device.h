@@ -1,8 +1,9 @@
-// mv_device.h — device helpers of the quantized matvec shared by the per-op kernels
-// (kernels.hip) and the persistent decode step (step.hip): cross-lane exchange, the
+// mv_device.h — device helpers of the quantized matvec shared by the single-token
+// (kernels.hip), batched (batch.hip) and prefill kernels: cross-lane exchange, the
 // activation prologue (RMSNorm + q8_K / q8_0 quantization, bit-exact with ggml), the
-// chunk-planar weight loads, the per-chunk integer dot products with ggml's fp32 combine,
-// row-pair bookkeeping and the epilogues.  Everything here is __device__ inline.
+// chunk-planar weight loads, the per-chunk integer sums and ggml's generic fp32 order
+// (the fold), row-pair bookkeeping, the epilogues and the attention bodies.  Everything
+// here is __device__ inline.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -122,9 +123,9 @@ __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirs
 // ----------------------------------------------------------------------------------
 // LDS image of the quantized activation, in the weights' chunk-part order (common.h):
 //   K-quants (block_q8_K): LO[k][ch], HI[k][ch]: 16 int8 each = activation of the
-//     weights in the low / high nibbles of quant part k of chunk ch (chunk weights
-//     16k..16k+15 and 32+16k..32+16k+15); BS[4ch+i] = bsums in natural order;
-//     D[b] per 256-block.
+//     weights in the low / high nibbles of quant part k of chunk ch, in residue order:
+//     byte 4m + i of part k = chunk element l + 8i (LO) / 32 + l + 8i (HI), l = 4k + m;
+//     BS[4ch+i] = bsums in natural order; D[b] per 256-block.
 //   Q8_0 (block_q8_0): LO[k][ch] (k < 4) = elements 64ch+16k..+15; D[b] per 32-block
 //     (f16-rounded, as stored by quantize_row_q8_0).
 // Lane L reads LO[k][L + 64j]: 16 consecutive 16-B slots per ds_read_b128 lane group,
@@ -190,7 +191,6 @@ template <int ACT>
 __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const float (&v)[16]) {
     const int tid = threadIdx.x;
     int q[16];
-    uint8_t* dst;
     if constexpr (ACT == 0) {
         // max |y| of the Q8_K block (order-free), then the SIGNED value ggml keeps: the
         // first element (lowest index) whose |y| equals it ('if (ax > amax)' scan).  Key =
@@ -226,10 +226,17 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
             }
             dval = 1.0f / iscale;
         }
-        // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: lo part k=qq (qq<2), hi part k=qq-2
+        // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: half h = qq/2 (LO / HI image),
+        // elements tt = 16*(qq%2) + j of the half.  Residue order (common.h): element tt of
+        // a half sits at part k = l/4, byte 4*(l%4) + i with l = tt%8, i = tt/8, so q[j]
+        // and q[j+8] (same l, i = 2*(qq%2) + 0/1) are one 16-bit store.
         const int nch = cols >> 6, ch = sb >> 2, qq = sb & 3;
         const int hoff = qq < 2 ? 0 : (int)(L.hi - L.lo);  // (no pointer select: it spills to scratch)
-        dst = L.lo + hoff + 16 * ((qq & 1) * nch + ch);
+        uint8_t* base = L.lo + hoff + 16 * ch + 2 * (qq & 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            *(uint16_t*)(base + 16 * nch * (j >> 2) + 4 * (j & 3)) =
+                (uint16_t)((q[j] & 0xff) | ((q[j + 8] & 0xff) << 8));
         L.bs[sb] = (int16_t)bsum;
         if ((tid & 15) == 0) L.d[sb >> 4] = dval;
     } else {
@@ -243,14 +250,13 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
         for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
         if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
         const int nch = cols >> 6;
-        dst = L.lo + 16 * ((sb & 3) * nch + (sb >> 2));
-    }
-    u32x4 pk;
+        u32x4 pk;
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
-        pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
-                ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
-    *(u32x4*)dst = pk;
+        for (int w = 0; w < 4; ++w)
+            pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
+                    ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
+        *(u32x4*)(L.lo + 16 * ((sb & 3) * nch + (sb >> 2))) = pk;
+    }
 }
 
 // Prologue in two halves so a caller can put the weight prefetch between them:
@@ -459,16 +465,56 @@ __device__ __forceinline__ Act load_act(const Lds& L, int ch, int nch) {
     return a;
 }
 
-// ggml_vec_dot_<T>_q8_K restricted to one 64-weight chunk; exact int32 sums, fp32
-// combine exactly as ggml's per-block formula (d_w*d_a*isum - dmin_w*d_a*imin).
+// ----------------------------------------------------------------------------------
+// ggml's generic fp32 order (oracle/ggml_oracle.c vd_q4_K/vd_q5_K/vd_q6_K,
+// vd_q8_0, restating upstream ggml_vec_dot_*_generic).  Per row:
+//   K-quants: for each 256-block b in order
+//       aux32[l] = sum over the block's elements e with e % 8 == l of scale(e)*q(e)*a(e)
+//       sums[l] += (d_w(b) * d_a(b)) * (float)aux32[l]       (8 fp32 chains, l = 0..7)
+//       sumf    -= (dmin_w(b) * d_a(b)) * (float)sumi(b)     (Q4_K/Q5_K; sumi = min terms)
+//     then sumf += sums[0]; ... sumf += sums[7]
+//   Q8_0:     sumf += (float)sumi(b) * (d_w(b) * d_a(b)) per 32-block b in order
+// Integer sums are exact in any grouping; the fp32 operations run exactly in this order.
+//
+// Device mapping.  Lane L of a wave holds chunk L (+64 j) of the wave's two rows.
+//   chunk_isum  the chunk's integer sums by residue l (the residue-order layout makes
+//               every sdot4 a same-residue dot: t[l] = sc0*dot(lo) + sc1*dot(hi))
+//   quad        the 4 chunks of block b are lanes 4b..4b+3; a reduce-scatter over the
+//               quad leaves residues 2c, 2c+1 of the block's aux32 in lane c
+//   item_terms  the block's fp32 terms d*(float)aux32[l] and -(dmin*(float)sumi) go to
+//               the wave's LDS fold buffer F[row][chain][block]
+//   fold_item   18 fold lanes (2 rows x 9 chains; Q8_0: 2 lanes, one chain) add the
+//               item's terms block after block onto their running chain
+//   fold_final  sumf chain + sums[0..7] in order, both rows, every lane
+// ----------------------------------------------------------------------------------
+struct PairSum {
+    float a, b;
+};
+constexpr int kFoldRow = 144;                     // floats per row: 9 chains x 16 blocks (Q8_0: 128 blocks)
+constexpr int kFoldFloats = 2 * kFoldRow + 32;   // + the chain results G[18] (padded)
+
+// LDS accesses of one wave handed between its own lanes: LDS executes a wave's
+// instructions in order, so only the compiler must not move accesses across this point
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+struct ISum {
+    int t[8];   // K-quants: per-residue sums of the chunk; Q8_0: t[0], t[1] = its two 32-block sums
+    int imin;   // Q4_K/Q5_K: min term of the chunk (m0*(bs0+bs1) + m1*(bs2+bs3)); else 0
+};
+
+// Q6_K high bits are stored XOR 2 (common.h): v_perm maps them straight to the signed
+// high part of q - 32 ({0x00, 0x10, 0xE0, 0xF0} for stored 0..3)
+__device__ __forceinline__ uint32_t q6_hi_bytes(uint32_t sel) { return __builtin_amdgcn_perm(0xF0E01000u, 0xF0E01000u, sel); }
+
 template <int T>
-__device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, int ch) {
+__device__ __forceinline__ ISum chunk_isum(const Raw& r, const Act& a, int ch) {
+    ISum s;
+    s.imin = 0;
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
         const int c = ch & 3;
         int sc0, m0, sc1, m1;
         scale_min(2 * c, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
         scale_min(2 * c + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
-        int lo = 0, hi = 0;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const u32x4 q = k ? r.q1 : r.q0;
@@ -480,16 +526,16 @@ __device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, int ch) {
                     l4 |= spread4((r.qh.x >> (16 * k + 4 * m)) & 0xFu) << 4;
                     h4 |= spread4((r.qh.y >> (16 * k + 4 * m)) & 0xFu) << 4;
                 }
-                lo = dot4(l4, al[m], lo);
-                hi = dot4(h4, ah[m], hi);
+                // |dot| <= 4*31*127: 24-bit multiplies are exact
+                s.t[4 * k + m] = __mul24(sc0, dot4(l4, al[m], 0)) + __mul24(sc1, dot4(h4, ah[m], 0));
             }
         }
-        const int isum = sc0 * lo + sc1 * hi;
-        const int imin = m0 * (a.bs[0] + a.bs[1]) + m1 * (a.bs[2] + a.bs[3]);
-        const float d = h2f(r.hdr.x), dmin = h2f(r.hdr.x >> 16);
-        return (d * a.d0) * (float)isum - (dmin * a.d0) * (float)imin;
+        s.imin = m0 * (a.bs[0] + a.bs[1]) + m1 * (a.bs[2] + a.bs[3]);
     } else if constexpr (T == T_Q6_K) {
-        int dm[4] = {0, 0, 0, 0};
+        // bytes 0,1 of a dword are elements l, l+8 (sub-block 4c + 2h), bytes 2,3 are
+        // l+16, l+24 (sub-block 4c + 2h + 1): one masked sdot4 per sub-block
+        const int c0 = (int)(int8_t)(r.e0 & 0xff), c1 = (int)(int8_t)((r.e0 >> 8) & 0xff),
+                  c2 = (int)(int8_t)((r.e0 >> 16) & 0xff), c3 = (int)(int8_t)(r.e0 >> 24);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const u32x4 q = k ? r.q1 : r.q0;
@@ -497,16 +543,14 @@ __device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, int ch) {
             const uint32_t hl = r.hdr[k], hh = r.hdr[2 + k];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const uint32_t ulo = (q[m] & M4) | (((hl >> (2 * m)) & M2) << 4);
-                const uint32_t uhi = ((q[m] >> 4) & M4) | (((hh >> (2 * m)) & M2) << 4);
-                dm[k] = dot4(ulo, al[m], dm[k]);
-                dm[2 + k] = dot4(uhi, ah[m], dm[2 + k]);
+                const uint32_t wl = (q[m] & M4) | q6_hi_bytes((hl >> (2 * m)) & M2);
+                const uint32_t wh = ((q[m] >> 4) & M4) | q6_hi_bytes((hh >> (2 * m)) & M2);
+                const int s0 = dot4(wl, al[m] & 0xffff, 0), s1 = dot4(wl, al[m] & (int)0xffff0000u, 0);
+                const int s2 = dot4(wh, ah[m] & 0xffff, 0), s3 = dot4(wh, ah[m] & (int)0xffff0000u, 0);
+                // |s| <= 2*32*127, |c| <= 128: exact in 24-bit multiplies
+                s.t[4 * k + m] = __mul24(c0, s0) + __mul24(c1, s1) + __mul24(c2, s2) + __mul24(c3, s3);
             }
         }
-        int isum = 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) isum += (int)(int8_t)(r.e0 >> (8 * m)) * (dm[m] - 32 * a.bs[m]);
-        return (h2f(r.e1) * a.d0) * (float)isum;
     } else {
         int s0 = 0, s1 = 0;
 #pragma unroll
@@ -516,8 +560,112 @@ __device__ __forceinline__ float dot_chunk(const Raw& r, const Act& a, int ch) {
             s1 = dot4(r.q2[m], a.a2[m], s1);
             s1 = dot4(r.q3[m], a.a3[m], s1);
         }
-        return (float)s0 * (h2f(r.e0) * a.d0) + (float)s1 * (h2f(r.e0 >> 16) * a.d1);
+        s.t[0] = s0;
+        s.t[1] = s1;
     }
+    return s;
+}
+
+// Quad reduce-scatter of the block's per-residue sums (lanes 4b..4b+3): lane c keeps
+// residues 2c, 2c+1 (a0, a1); the min term is summed into every lane of the quad.
+__device__ __forceinline__ void quad_scatter(ISum& s, int& a0, int& a1) {
+    const bool b0 = (threadIdx.x & 1) != 0, b1 = (threadIdx.x & 2) != 0;
+    // level 1 (lane ^ 1): keep residue pairs b0 and b0 + 2
+    int k[4];
+    {
+        const int s0 = b0 ? s.t[0] : s.t[2], s1 = b0 ? s.t[1] : s.t[3];
+        const int s2 = b0 ? s.t[4] : s.t[6], s3 = b0 ? s.t[5] : s.t[7];
+        k[0] = (b0 ? s.t[2] : s.t[0]) + xor_partner_i<1>(s0);
+        k[1] = (b0 ? s.t[3] : s.t[1]) + xor_partner_i<1>(s1);
+        k[2] = (b0 ? s.t[6] : s.t[4]) + xor_partner_i<1>(s2);
+        k[3] = (b0 ? s.t[7] : s.t[5]) + xor_partner_i<1>(s3);
+    }
+    // level 2 (lane ^ 2): keep pair b0 + 2*b1 = c
+    const int r0 = b1 ? k[0] : k[2], r1 = b1 ? k[1] : k[3];
+    a0 = (b1 ? k[2] : k[0]) + xor_partner_i<2>(r0);
+    a1 = (b1 ? k[3] : k[1]) + xor_partner_i<2>(r1);
+    s.imin += xor_partner_i<1>(s.imin);
+    s.imin += xor_partner_i<2>(s.imin);
+}
+
+// The item's fp32 terms of one row into its fold buffer Fr (chain ch, block bi at
+// Fr[ch * 16 + bi]; Q8_0: Fr[bi], 128 blocks).  Every lane calls it (cross-lane ops);
+// `valid` (the chunk exists) guards only the stores — chunks past the row come in whole
+// blocks (cols % 256 == 0).
+template <int T>
+__device__ __forceinline__ void item_terms(const Raw& r, const Act& a, int ch, bool valid, float* Fr) {
+    ISum s = chunk_isum<T>(r, a, ch);
+    const int lane = threadIdx.x & 63;
+    if constexpr (T == T_Q8_0) {
+        const float t0 = (float)s.t[0] * (h2f(r.e0) * a.d0), t1 = (float)s.t[1] * (h2f(r.e0 >> 16) * a.d1);
+        if (valid) *(float2*)(Fr + 2 * lane) = make_float2(t0, t1);
+    } else {
+        int a0, a1;
+        quad_scatter(s, a0, a1);
+        const int c = lane & 3, bi = lane >> 2;
+        const float d = (T == T_Q6_K ? h2f(r.e1) : h2f(r.hdr.x)) * a.d0;
+        const float p0 = d * (float)a0, p1 = d * (float)a1;
+        float nq = 0.f;
+        if constexpr (T != T_Q6_K) nq = -((h2f(r.hdr.x >> 16) * a.d0) * (float)s.imin);
+        if (valid) {
+            Fr[(2 * c) * 16 + bi] = p0;
+            Fr[(2 * c + 1) * 16 + bi] = p1;
+            if (c == 0) Fr[8 * 16 + bi] = nq;  // Q6_K: no min chain (+0 terms, as sumf = 0)
+        }
+    }
+}
+
+// blocks of item j of a row of `cols` weights (K-quants: 16 per item, Q8_0: 128)
+template <int ACT>
+__device__ __forceinline__ int item_blocks(int cols, int j) {
+    const int nb = ACT ? (cols >> 5) - 128 * j : (cols >> 8) - 16 * j;
+    const int per = ACT ? 128 : 16;
+    return nb < per ? nb : per;
+}
+
+// Fold lane f (< 18, Q8_0 < 2) adds chain f's terms of nb blocks in block order.
+template <int ACT>
+__device__ __forceinline__ void fold_item(const float* F, int nb, float& acc) {
+    constexpr int NC = ACT ? 1 : 9, CS = ACT ? 128 : 16;
+    const int lane = threadIdx.x & 63;
+    if (lane < 2 * NC) {
+        const int r = lane >= NC ? 1 : 0;
+        const float* p = F + r * kFoldRow + (lane - r * NC) * CS;
+        for (int b = 0; b < nb; b += 4) {
+            const float4 v = *(const float4*)(p + b);
+            acc += v.x;
+            if (b + 1 < nb) acc += v.y;
+            if (b + 2 < nb) acc += v.z;
+            if (b + 3 < nb) acc += v.w;
+        }
+    }
+}
+
+// Both rows' final sums in every lane: sumf chain, then += sums[0..7] (K-quants).
+template <int ACT>
+__device__ __forceinline__ PairSum fold_final(float* F, float acc) {
+    constexpr int NC = ACT ? 1 : 9;
+    float* G = F + 2 * kFoldRow;
+    const int lane = threadIdx.x & 63;
+    wave_lds_sync();
+    if (lane < 2 * NC) G[lane] = acc;
+    wave_lds_sync();
+    PairSum v;
+    if constexpr (ACT) {
+        v.a = G[0];
+        v.b = G[1];
+    } else {
+        float sa = G[8], sb = G[17];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            sa += G[l];
+            sb += G[9 + l];
+        }
+        v.a = sa;
+        v.b = sb;
+    }
+    wave_lds_sync();
+    return v;
 }
 
 // (the descriptor type is a template parameter: the persistent step reads its phase
@@ -598,14 +746,6 @@ __device__ __forceinline__ PairRaw<T> load_item(const PairRows<T>& pr, int ch, i
     return w;
 }
 
-// Row sums of a pair: one 64-lane butterfly per row (steps 1,2,4,8,16,32; DPP and
-// permlane swaps, no LDS), the oracle's device order models this tree exactly.
-struct PairSum {
-    float a, b;
-};
-__device__ __forceinline__ PairSum reduce_pair(float acc_a, float acc_b) {
-    return {wave_sum(acc_a), wave_sum(acc_b)};
-}
 
 // ordered key of (logit, row): larger logit wins, ties -> smaller row (first max wins,
 // as upstream llama_sampler_greedy's strict '>' scan)
@@ -699,30 +839,44 @@ __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, P
 }
 
 // Non-pipelined fallback for pairs whose type is not the kernel's primary type (the
-// Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs).
+// Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs): the same
+// terms and fold, one item at a time, each row in its own type.
 template <int ACT, int T>
-__device__ __forceinline__ float generic_row(const Seg& s, int row, int cols, const Lds& L) {
+__device__ __forceinline__ void row_terms(const Seg& s, int row, int cols, int ch, const Act& act, float* Fr) {
     const int nch = cols >> 6;
     const RowPtr rp = row_ptr<T>(s, row, cols);
-    float acc = 0.f;
-    for (int ch = threadIdx.x & 63; ch < nch; ch += 64) {
-        const Raw w = load_chunk<T>(rp, ch, nch);
-        acc += dot_chunk<T>(w, load_act<ACT>(L, ch, nch), ch);
-    }
-    return acc;
+    const int chc = ch < nch ? ch : nch - 1;
+    item_terms<T>(load_chunk<T>(rp, chc, nch), act, chc, ch < nch, Fr);
 }
 template <int ACT>
-__device__ __forceinline__ float generic_row_any(int type, const Seg& s, int row, int cols, const Lds& L) {
+__device__ __forceinline__ void row_terms_any(int type, const Seg& s, int row, int cols, int ch, const Act& act,
+                                              float* Fr) {
     if constexpr (ACT == 1) {
-        return generic_row<1, T_Q8_0>(s, row, cols, L);
+        row_terms<1, T_Q8_0>(s, row, cols, ch, act, Fr);
     } else {
         switch (type) {
-            case T_Q4_K: return generic_row<0, T_Q4_K>(s, row, cols, L);
-            case T_Q5_K: return generic_row<0, T_Q5_K>(s, row, cols, L);
-            case T_Q6_K: return generic_row<0, T_Q6_K>(s, row, cols, L);
-            default: return 0.f;
+            case T_Q4_K: row_terms<0, T_Q4_K>(s, row, cols, ch, act, Fr); break;
+            case T_Q5_K: row_terms<0, T_Q5_K>(s, row, cols, ch, act, Fr); break;
+            case T_Q6_K: row_terms<0, T_Q6_K>(s, row, cols, ch, act, Fr); break;
+            default: break;
         }
     }
+}
+template <int ACT>
+__device__ __forceinline__ PairSum pair_any(const PairRef& r, int cols, const Lds& L, float* F) {
+    const int nch = cols >> 6, NJ = (nch + 63) >> 6;
+    const int lane = threadIdx.x & 63;
+    float acc = 0.f;
+    for (int j = 0; j < NJ; ++j) {
+        const int ch = lane + 64 * j, chc = ch < nch ? ch : nch - 1;
+        const Act act = load_act<ACT>(L, chc, nch);
+        row_terms_any<ACT>(r.sa.type, r.sa, r.ra, cols, ch, act, F);
+        row_terms_any<ACT>(r.sb.type, r.sb, r.vb ? r.rb : r.ra, cols, ch, act, F + kFoldRow);
+        wave_lds_sync();
+        fold_item<ACT>(F, item_blocks<ACT>(cols, j), acc);
+        wave_lds_sync();
+    }
+    return fold_final<ACT>(F, acc);
 }
 
 // get_rows: element e of row `row` dequantized from the device layout (bit-exact with
@@ -734,24 +888,26 @@ __device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int 
         case T_Q4_K:
         case T_Q5_K:
         case T_Q6_K: {
+            // residue order (common.h): chunk element t = 32 hi + l + 8 i sits in part
+            // k = l / 4, byte 4 (l % 4) + i (low nibble: hi = 0, high nibble: hi = 1)
             const int nch = cols >> 6, nbr = cols >> 8;
-            const int ch = e >> 6, t = e & 63, hi = t >= 32, l = t & 31, k = l >> 4, i = l & 15;
+            const int ch = e >> 6, t = e & 63, hi = t >= 32, l = t & 7, i = (t & 31) >> 3, k = l >> 2, m = l & 3;
             const size_t gb = (size_t)row * nbr + (e >> 8);
-            const uint8_t qb = w.a[(size_t)row * nch * 32 + (size_t)(k * nch + ch) * 16 + i];
+            const uint8_t qb = w.a[(size_t)row * nch * 32 + (size_t)(k * nch + ch) * 16 + 4 * m + i];
             int q = hi ? (qb >> 4) : (qb & 0xF);
-            if (w.type == T_Q6_K) {  // H dword (2*hi + k), byte i&3, bits 2*(i>>2)
-                const uint8_t hb = w.h[((size_t)row * nch + ch) * 16 + (2 * hi + k) * 4 + (i & 3)];
-                q |= ((hb >> (2 * (i >> 2))) & 3) << 4;
+            if (w.type == T_Q6_K) {  // H dword (2*hi + k), byte i, bits 2m: the 2 high bits XOR 2
+                const uint8_t hb = w.h[((size_t)row * nch + ch) * 16 + (2 * hi + k) * 4 + i];
+                q |= (((hb >> (2 * m)) & 3) ^ 2) << 4;
                 const float d = h2f(*(const uint16_t*)(w.d + gb * 2));
                 const int sc = (int8_t)w.s[gb * 16 + ((e & 255) >> 4)];
                 return d * (float)sc * (float)(q - 32);
             }
             const uint32_t* s32 = (const uint32_t*)(w.s + gb * 16);
-            int sc, m;
-            scale_min(2 * (ch & 3) + hi, s32[1], s32[2], s32[3], sc, m);
-            if (w.type == T_Q5_K) q += ((ldw4(w.h + ((size_t)row * nch + ch) * 8 + 4 * hi) >> l) & 1) << 4;
+            int sc, mn;
+            scale_min(2 * (ch & 3) + hi, s32[1], s32[2], s32[3], sc, mn);
+            if (w.type == T_Q5_K) q += ((ldw4(w.h + ((size_t)row * nch + ch) * 8 + 4 * hi) >> (4 * l + i)) & 1) << 4;
             const float d = h2f(s32[0]), dmin = h2f(s32[0] >> 16);
-            const float d1 = d * (float)sc, m1 = dmin * (float)m;
+            const float d1 = d * (float)sc, m1 = dmin * (float)mn;
             return d1 * (float)q - m1;
         }
         case T_Q8_0: {

@@ -255,10 +255,6 @@ class Context:
                     "GBps": (by[i] / (us[i] * 1e-6) / 1e9) if us[i] > 0 else 0.0}
                 for i, k in enumerate(self.KERNEL_CLASSES)}
 
-    def step_path(self, pos: int) -> int:
-        """1: the step at pos runs as the persistent one-launch step; 0: per-op launches."""
-        return int(lib().llmi_step_path(self._h, int(pos)))
-
     def kv_clear(self) -> None:
         lib().llama_kv_self_clear(self._h)
 

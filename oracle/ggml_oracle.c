@@ -346,62 +346,6 @@ static float vd_f32(int n, const float* x, const float* y) {
     return (float)sumf;
 }
 
-/* ---------------------------------------------------------------------------
- * Device-order dot (or_set_dot_order(1)): the SAME exact integer block math as the
- * generic functions above, split into 64-weight CHUNKS (the HIP kernel's unit: quarter
- * c of a K-quant block, or two Q8_0 blocks), with the fp32 association the kernel uses
- * (DESIGN.md §Numerics): chunk ci contributes
- *   K-quants: (d*dA)*(float)isum - (dmin*dA)*(float)imin      (Q6_K: no min term)
- *   Q8_0    : (float)s0*(d0*dA0) + (float)s1*(d1*dA1)
- * lane L = ci % 64 accumulates its chunks in order, then a 64-lane xor butterfly
- * (steps 1,2,4,8,16,32 as in kernels.hip wave_sum).
- * Integer sums are ggml's exactly; only fp32 rounding order differs from the
- * generic loop (whose own order differs again from every SIMD variant upstream).
- * --------------------------------------------------------------------------- */
-static int g_dot_order = 0;
-void or_set_dot_order(int mode) { g_dot_order = mode; }
-int or_get_dot_order(void) { return g_dot_order; }
-
-static int q6_u6(const block_q6_K* x, int w) {
-    const int n = w >> 7, r = w & 127, quad = r >> 5, l = r & 31;
-    const uint8_t qlb = x->ql[64 * n + l + 32 * (quad & 1)];
-    const int lo = (quad >> 1) ? (qlb >> 4) : (qlb & 0xF);
-    const int hi = (x->qh[32 * n + l] >> (2 * quad)) & 3;
-    return lo | (hi << 4);
-}
-
-static float chunk_kq(int wtype, const uint8_t* blk, const block_q8_K* y, int c) {
-    const int8_t* a = y->qs + 64 * c;
-    const int16_t* bs = y->bsums + 4 * c;
-    if (wtype == OR_Q6_K) {
-        const block_q6_K* x = (const block_q6_K*)blk;
-        int isum = 0;
-        for (int m = 0; m < 4; ++m) {
-            int dot = 0;
-            for (int t = 0; t < 16; ++t) dot += q6_u6(x, 64 * c + 16 * m + t) * a[16 * m + t];
-            isum += x->scales[4 * c + m] * (dot - 32 * bs[m]);
-        }
-        return (llmi_h2f(x->d) * y->d) * (float)isum;
-    }
-    const uint8_t* scales; const uint8_t* qs; const uint8_t* qh = NULL; uint16_t d16, m16;
-    if (wtype == OR_Q4_K) { const block_q4_K* x = (const block_q4_K*)blk; scales = x->scales; qs = x->qs; d16 = x->d; m16 = x->dmin; }
-    else { const block_q5_K* x = (const block_q5_K*)blk; scales = x->scales; qs = x->qs; qh = x->qh; d16 = x->d; m16 = x->dmin; }
-    uint8_t sc0, m0, sc1, m1;
-    get_scale_min_k4(2 * c, scales, &sc0, &m0);
-    get_scale_min_k4(2 * c + 1, scales, &sc1, &m1);
-    int lo = 0, hi = 0;
-    for (int t = 0; t < 32; ++t) {
-        int ql = qs[32 * c + t] & 0xF, qq = qs[32 * c + t] >> 4;
-        if (qh) { ql += ((qh[t] >> (2 * c)) & 1) << 4; qq += ((qh[t] >> (2 * c + 1)) & 1) << 4; }
-        lo += ql * a[t];
-        hi += qq * a[32 + t];
-    }
-    const int isum = sc0 * lo + sc1 * hi;
-    const int imin = m0 * (bs[0] + bs[1]) + m1 * (bs[2] + bs[3]);
-    const float dA = y->d;
-    return (llmi_h2f(d16) * dA) * (float)isum - (llmi_h2f(m16) * dA) * (float)imin;
-}
-
 /* Unpack one K-quant block into its 256 unsigned quant values in natural element order
  * (Q4_K 0..15, Q5_K 0..31, Q6_K 0..63; the generic functions' unpack loops, without
  * Q6_K's -32), then the 16-element integer dots against the q8_K block: every chunk's
@@ -434,92 +378,11 @@ static void block_unpack_kq(int wtype, const uint8_t* blk, uint8_t* u) {
         }
     }
 }
-static void block_dots16(const uint8_t* u, const block_q8_K* y, int dots[16]) {
-#if defined(__AVX2__)
-    /* the same exact integer sums (u <= 63, |a| <= 128: no int16 saturation in maddubs) */
-    const __m256i ones = _mm256_set1_epi16(1);
-    for (int j = 0; j < 16; j += 2) {
-        const __m256i uv = _mm256_loadu_si256((const __m256i*)(u + 16 * j));
-        const __m256i av = _mm256_loadu_si256((const __m256i*)(y->qs + 16 * j));
-        const __m256i p4 = _mm256_madd_epi16(_mm256_maddubs_epi16(uv, av), ones); /* 8 x sum of 4 */
-        const __m256i h = _mm256_hadd_epi32(p4, p4);  /* per 128-bit half: [s01, s23, s01, s23] */
-        const __m256i h2 = _mm256_hadd_epi32(h, h);
-        dots[j] = _mm256_extract_epi32(h2, 0);
-        dots[j + 1] = _mm256_extract_epi32(h2, 4);
-    }
-#else
-    for (int j = 0; j < 16; ++j) {
-        int d = 0;
-        for (int t = 0; t < 16; ++t) d += (int)u[16 * j + t] * (int)y->qs[16 * j + t];
-        dots[j] = d;
-    }
-#endif
-}
-
-/* chunk c (64 weights) of a K-quant block from its 16-element dots: the kernel's
- * dot_chunk (kernels.hip) formula, fp32 exactly as written there */
-static float chunk_from_dots(int wtype, const uint8_t* blk, const block_q8_K* y, const int dots[16], int c) {
-    const int16_t* bs = y->bsums + 4 * c;
-    if (wtype == OR_Q6_K) {
-        const block_q6_K* x = (const block_q6_K*)blk;
-        int isum = 0;
-        for (int m = 0; m < 4; ++m) isum += x->scales[4 * c + m] * (dots[4 * c + m] - 32 * bs[m]);
-        return (llmi_h2f(x->d) * y->d) * (float)isum;
-    }
-    const uint8_t* scales; uint16_t d16, m16;
-    if (wtype == OR_Q4_K) { const block_q4_K* x = (const block_q4_K*)blk; scales = x->scales; d16 = x->d; m16 = x->dmin; }
-    else { const block_q5_K* x = (const block_q5_K*)blk; scales = x->scales; d16 = x->d; m16 = x->dmin; }
-    uint8_t sc0, m0, sc1, m1;
-    get_scale_min_k4(2 * c, scales, &sc0, &m0);
-    get_scale_min_k4(2 * c + 1, scales, &sc1, &m1);
-    const int lo = dots[4 * c] + dots[4 * c + 1], hi = dots[4 * c + 2] + dots[4 * c + 3];
-    const int isum = sc0 * lo + sc1 * hi;
-    const int imin = m0 * (bs[0] + bs[1]) + m1 * (bs[2] + bs[3]);
-    const float dA = y->d;
-    return (llmi_h2f(d16) * dA) * (float)isum - (llmi_h2f(m16) * dA) * (float)imin;
-}
-
-static float vd_device_order(int wtype, int n, const void* w, const void* act) {
-    float acc[64];
-    for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
-    const int nch = n / 64;
-    if (wtype == OR_Q8_0) {
-        for (int ci = 0; ci < nch; ++ci) {
-            const block_q8_0* x = (const block_q8_0*)w + 2 * ci;
-            const block_q8_0* y = (const block_q8_0*)act + 2 * ci;
-            int s0 = 0, s1 = 0;
-            for (int j = 0; j < 32; ++j) { s0 += x[0].qs[j] * y[0].qs[j]; s1 += x[1].qs[j] * y[1].qs[j]; }
-            const float v = (float)s0 * (llmi_h2f(x[0].d) * llmi_h2f(y[0].d)) + (float)s1 * (llmi_h2f(x[1].d) * llmi_h2f(y[1].d));
-            acc[ci % 64] = acc[ci % 64] + v;
-        }
-    } else {
-        const size_t bb = or_type_size(wtype);
-        for (int ib = 0; ib < nch / 4; ++ib) {
-            const uint8_t* blk = (const uint8_t*)w + (size_t)ib * bb;
-            const block_q8_K* y = (const block_q8_K*)act + ib;
-            int dots[16];
-            uint8_t u[QK_K];
-            block_unpack_kq(wtype, blk, u);
-            block_dots16(u, y, dots);
-            for (int c = 0; c < 4; ++c) {
-                const int ci = 4 * ib + c;
-                acc[ci % 64] = acc[ci % 64] + chunk_from_dots(wtype, blk, y, dots, c);
-            }
-        }
-    }
-    /* xor butterfly, steps 1,2,4,8,16,32 (kernels.hip wave_sum: DPP + permlane swaps) */
-    for (int o = 1; o < 64; o <<= 1) {
-        float nxt[64];
-        for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
-        for (int l = 0; l < 64; ++l) acc[l] = nxt[l];
-    }
-    return acc[0];
-}
-
-/* vd_device_order for a K-quant row whose quant values are already unpacked (u: the
- * row's block_unpack_kq output) and whose per-block constants are decoded once
- * (RowConst: h2f(d), h2f(dmin), the 6-bit scales/mins or Q6_K's int8 scales): identical
- * operations, hoisted out of the token loop of or_prefill. */
+/* The generic functions above for a K-quant row whose quant values are already
+ * unpacked (u: the row's block_unpack_kq output) and whose per-block constants are
+ * decoded once (RowConst: h2f(d), h2f(dmin), the 6-bit scales/mins or Q6_K's int8
+ * scales): the same integer sums (exact in any grouping) and the same fp32 operations
+ * in the same order, hoisted out of the token loop of or_prefill. */
 typedef struct { float d, dmin; int sc[16], mn[8]; } RowConst;
 
 static void row_consts(int wtype, const uint8_t* blk, RowConst* rc) {
@@ -536,62 +399,36 @@ static void row_consts(int wtype, const uint8_t* blk, RowConst* rc) {
     for (int j = 0; j < 8; ++j) { uint8_t a, b; get_scale_min_k4(j, scales, &a, &b); rc->sc[j] = a; rc->mn[j] = b; }
 }
 
-static float vd_device_order_unpacked(int wtype, int n, const RowConst* rcs, const uint8_t* u, const void* act) {
-    float acc[64];
-    for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
+static float vd_generic_unpacked(int wtype, int n, const RowConst* rcs, const uint8_t* u, const void* act) {
+    float sums[8]; float sumf = 0;
+    for (int l = 0; l < 8; ++l) sums[l] = 0;
     for (int ib = 0; ib < n / QK_K; ++ib) {
         const block_q8_K* y = (const block_q8_K*)act + ib;
         const RowConst* rc = rcs + ib;
-        int dots[16];
-        block_dots16(u + (size_t)ib * QK_K, y, dots);
-        const float dA = y->d;
-        for (int c = 0; c < 4; ++c) {
-            const int16_t* bs = y->bsums + 4 * c;
-            float v;
-            if (wtype == OR_Q6_K) {
-                int isum = 0;
-                for (int m = 0; m < 4; ++m) isum += rc->sc[4 * c + m] * (dots[4 * c + m] - 32 * bs[m]);
-                v = (rc->d * dA) * (float)isum;
-            } else {
-                const int lo = dots[4 * c] + dots[4 * c + 1], hi = dots[4 * c + 2] + dots[4 * c + 3];
-                const int isum = rc->sc[2 * c] * lo + rc->sc[2 * c + 1] * hi;
-                const int imin = rc->mn[2 * c] * (bs[0] + bs[1]) + rc->mn[2 * c + 1] * (bs[2] + bs[3]);
-                v = (rc->d * dA) * (float)isum - (rc->dmin * dA) * (float)imin;
-            }
-            const int ci = 4 * ib + c;
-            acc[ci % 64] = acc[ci % 64] + v;
+        const uint8_t* ub = u + (size_t)ib * QK_K;
+        int32_t aux32[8];
+        for (int l = 0; l < 8; ++l) aux32[l] = 0;
+        if (wtype == OR_Q6_K) {
+            for (int j = 0; j < 16; ++j)
+                for (int e = 0; e < 16; ++e) aux32[e & 7] += rc->sc[j] * (((int)ub[16 * j + e] - 32) * y->qs[16 * j + e]);
+        } else {
+            for (int j = 0; j < 8; ++j)
+                for (int e = 0; e < 32; ++e) aux32[e & 7] += rc->sc[j] * ((int)ub[32 * j + e] * y->qs[32 * j + e]);
+        }
+        const float d = rc->d * y->d;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+        if (wtype != OR_Q6_K) {
+            int sumi = 0;
+            for (int j = 0; j < QK_K / 16; ++j) sumi += y->bsums[j] * rc->mn[j / 2];
+            const float dmin = rc->dmin * y->d;
+            sumf -= dmin * sumi;
         }
     }
-    for (int o = 1; o < 64; o <<= 1) {
-        float nxt[64];
-        for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
-        for (int l = 0; l < 64; ++l) acc[l] = nxt[l];
-    }
-    return acc[0];
-}
-
-/* The device order once more, chunk by chunk with per-element unpacking (chunk_kq):
- * an independent restatement tests pin vd_device_order's vectorised block dots against
- * (tests/test_oracle_simd.py). */
-float or_vec_dot_device_ref(int wtype, int n, const void* w, const void* act) {
-    float acc[64];
-    for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
-    const int nch = n / 64;
-    if (wtype == OR_Q8_0) return vd_device_order(wtype, n, w, act);
-    const size_t bb = or_type_size(wtype);
-    for (int ci = 0; ci < nch; ++ci)
-        acc[ci % 64] = acc[ci % 64] + chunk_kq(wtype, (const uint8_t*)w + (size_t)(ci / 4) * bb, (const block_q8_K*)act + ci / 4, ci % 4);
-    for (int o = 1; o < 64; o <<= 1) {
-        float nxt[64];
-        for (int l = 0; l < 64; ++l) nxt[l] = acc[l] + acc[l ^ o];
-        for (int l = 0; l < 64; ++l) acc[l] = nxt[l];
-    }
-    return acc[0];
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
+    return sumf;
 }
 
 float or_vec_dot(int wtype, int n, const void* w, const void* a) {
-    if (g_dot_order == 1 && (wtype == OR_Q4_K || wtype == OR_Q5_K || wtype == OR_Q6_K || wtype == OR_Q8_0) && n % 256 == 0)
-        return vd_device_order(wtype, n, w, a);
     switch (wtype) {
         case OR_Q4_K: return vd_q4_K(n, w, a);
         case OR_Q5_K: return vd_q5_K(n, w, a);
@@ -967,8 +804,8 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
 
 /* T consecutive or_decode steps at positions pos0.. with no logits (a prompt), the
  * loops reordered for speed: per layer each weight row is unpacked once and dotted with
- * the T activations (device order: vd_device_order_unpacked; generic order: or_vec_dot
- * per token), then attention per (token, head).  Every token's operations are exactly
+ * the T activations (vd_generic_unpacked: or_vec_dot's operations with the row's
+ * unpacking and constants hoisted), then attention per (token, head).  Every token's operations are exactly
  * or_decode's (the KV rows a token attends to are written by the same layer before).
  * Leaves the last token's state (x, taps) as or_decode would.  Test infrastructure for
  * the long parity tests (2048-token prompts at 7B widths). */
@@ -988,12 +825,12 @@ static void matmul_t(const or_tensor* W, const float* X, int T, float* Y, int nt
 #pragma omp for schedule(dynamic, 8)
         for (int64_t r = 0; r < rows; ++r) {
             const uint8_t* w = (const uint8_t*)W->data + (size_t)r * row_bytes;
-            if (g_dot_order == 1 && kq) {
+            if (kq) {
                 for (int64_t ib = 0; ib < cols / QK_K; ++ib) {
                     block_unpack_kq(wtype, w + (size_t)ib * bb, u + ib * QK_K);
                     row_consts(wtype, w + (size_t)ib * bb, rcs + ib);
                 }
-                for (int t = 0; t < T; ++t) Y[(size_t)t * rows + r] = vd_device_order_unpacked(wtype, (int)cols, rcs, u, acts + ab * t);
+                for (int t = 0; t < T; ++t) Y[(size_t)t * rows + r] = vd_generic_unpacked(wtype, (int)cols, rcs, u, acts + ab * t);
             } else {
                 for (int t = 0; t < T; ++t) Y[(size_t)t * rows + r] = or_vec_dot(wtype, (int)cols, w, acts + ab * t);
             }

@@ -43,11 +43,6 @@ void or_quantize_row_q8_K(const float* x, void* y, int64_t n);
 void or_quantize_row_q8_0(const float* x, void* y, int64_t n);
 /* ggml_vec_dot_<wtype>_<vec_dot_type>_generic: one weight row against one quantized activation */
 float or_vec_dot(int wtype, int n, const void* wrow, const void* act);
-/* fp32 association of or_vec_dot for quantized types: 0 = ggml generic loop (default,
- * the restatement), 1 = the HIP kernel's chunk/butterfly order (same integer math).
- * Process-global; tests set it explicitly. */
-void or_set_dot_order(int mode);
-int or_get_dot_order(void);
 /* y[r] = vec_dot(W[r], quantize(x)) for r < rows (x is f32[cols]); OpenMP over rows */
 int or_matvec(int wtype, const void* W, int64_t rows, int64_t cols, const float* x, float* y, int nthreads);
 

@@ -57,11 +57,8 @@ def lib() -> C.CDLL:
         "or_quantize_row_q8_K": (None, [P, P, C.c_int64]),
         "or_quantize_row_q8_0": (None, [P, P, C.c_int64]),
         "or_vec_dot": (C.c_float, [C.c_int, C.c_int, P, P]),
-        "or_vec_dot_device_ref": (C.c_float, [C.c_int, C.c_int, P, P]),
         "or_matvec": (C.c_int, [C.c_int, P, C.c_int64, C.c_int64, P, P, C.c_int]),
         "or_rms_norm_mul": (None, [P, P, P, C.c_int, C.c_float]),
-        "or_set_dot_order": (None, [C.c_int]),
-        "or_get_dot_order": (C.c_int, []),
         "or_model_load": (P, [C.c_char_p, C.c_int]),
         "or_model_free": (None, [P]),
         "or_last_error": (C.c_char_p, []),
@@ -151,18 +148,6 @@ def matvec(type_: int, W: np.ndarray, rows: int, cols: int, x: np.ndarray, threa
     y = np.empty(rows, dtype=np.float32)
     assert lib().or_matvec(type_, _p(W), rows, cols, _p(x), _p(y), threads or nthreads()) == 0
     return y
-
-
-GENERIC, DEVICE_ORDER = 0, 1
-
-
-def set_dot_order(mode: int) -> None:
-    """0: ggml generic fp32 association (the restatement); 1: the HIP kernel's order."""
-    lib().or_set_dot_order(int(mode))
-
-
-def get_dot_order() -> int:
-    return int(lib().or_get_dot_order())
 
 
 def expf(x: float) -> float:

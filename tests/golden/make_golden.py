@@ -9,7 +9,7 @@ llama.cpp itself stays unpinned.
   tiny-mixed.gguf        the synthetic tiny-mixed preset (seed 1): E=256, 2 layers,
                          every quant type (Q4_K/Q5_K/Q6_K/Q8_0), 1.45 MB
   greedy16.npz           prompt, 16 greedy steps: per-step logits (f32, full vocab)
-                         and ids, in the generic and the device dot order
+                         and ids
   blocks.npz             hand-built single blocks with closed-form dequant values
 """
 import os
@@ -29,25 +29,21 @@ PROMPT = [1, 17, 300, 42, 999 % 1000, 5, 6, 123]
 N_GEN = 16
 
 
-def greedy(path, order):
-    po.set_dot_order(order)
-    try:
-        om = po.OracleModel(path, n_ctx=64, threads=1)
-        logits, ids = [], []
-        cur, pos = PROMPT[0], 0
-        for step in range(len(PROMPT) + N_GEN - 1):
-            lg = om.decode(cur, pos)
-            logits.append(lg.copy())
-            pos += 1
-            if pos < len(PROMPT):
-                cur = PROMPT[pos]
-            else:
-                cur = int(np.argmax(lg))
-                ids.append(cur)
-        om.close()
-        return np.stack(logits).astype(np.float32), np.array(ids, dtype=np.int32)
-    finally:
-        po.set_dot_order(po.GENERIC)
+def greedy(path):
+    om = po.OracleModel(path, n_ctx=64, threads=1)
+    logits, ids = [], []
+    cur, pos = PROMPT[0], 0
+    for step in range(len(PROMPT) + N_GEN - 1):
+        lg = om.decode(cur, pos)
+        logits.append(lg.copy())
+        pos += 1
+        if pos < len(PROMPT):
+            cur = PROMPT[pos]
+        else:
+            cur = int(np.argmax(lg))
+            ids.append(cur)
+    om.close()
+    return np.stack(logits).astype(np.float32), np.array(ids, dtype=np.int32)
 
 
 def blocks():
@@ -111,14 +107,10 @@ def main():
 
     path = os.path.join(HERE, "tiny-mixed.gguf")
     llmi.write_synthetic_gguf(path, "tiny-mixed", seed=1)
-    lg_g, ids_g = greedy(path, po.GENERIC)
-    lg_d, ids_d = greedy(path, po.DEVICE_ORDER)
-    np.savez_compressed(os.path.join(HERE, "greedy16.npz"), prompt=np.array(PROMPT, np.int32),
-                        logits_generic=lg_g, ids_generic=ids_g, logits_device=lg_d, ids_device=ids_d)
+    lg, ids = greedy(path)
+    np.savez_compressed(os.path.join(HERE, "greedy16.npz"), prompt=np.array(PROMPT, np.int32), logits=lg, ids=ids)
     np.savez_compressed(os.path.join(HERE, "blocks.npz"), **blocks())
-    print("generic ids", ids_g.tolist())
-    print("device  ids", ids_d.tolist())
-    print("max |generic - device|", float(np.abs(lg_g - lg_d).max()))
+    print("ids", ids.tolist())
 
 
 if __name__ == "__main__":

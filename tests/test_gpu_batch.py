@@ -212,7 +212,7 @@ def test_batched_attention_paths(gpu, tiny_models, monkeypatch, mode):
 
 @pytest.mark.parametrize("preset", ["tiny-mixed-d128", "tiny-mixed"])
 def test_batched_steps_vs_oracle(gpu, tiny_models, preset):
-    """The batched step against the oracle directly (device fp32 order): 4 sequences at
+    """The batched step against the oracle directly (ggml's generic fp32 order): 4 sequences at
     different positions advance one token per llama_decode call (one batched step; for
     tiny-mixed, whose layer 0 mixes gate/up types, the per-sequence fallback), and every
     sequence's logits equal the oracle's decode of that sequence, bit for bit."""
@@ -221,27 +221,24 @@ def test_batched_steps_vs_oracle(gpu, tiny_models, preset):
     path = tiny_models[preset]
     rng = np.random.default_rng(31)
     prompts = _prompts(rng, 4, min_len=3, max_len=30)
-    po.set_dot_order(po.DEVICE_ORDER)
-    try:
-        oms = [po.OracleModel(path, n_ctx=256) for _ in prompts]
-        m = llmi.Model(path)
-        c = llmi.Context(m, n_ctx=256, n_seq=4)
-        cur, pos = [], []
-        for s, p in enumerate(prompts):
-            for k, t in enumerate(p[:-1]):
-                oms[s].decode(t, k, logits=False)
-            assert c.decode(p[:-1], seq=[s] * (len(p) - 1)) == 0
-            cur.append(p[-1])
-            pos.append(len(p) - 1)
-        for step in range(6):
-            assert c.decode(cur, pos=pos, seq=[0, 1, 2, 3], logits_all=True) == 0
-            for s in range(4):
-                want = oms[s].decode(cur[s], pos[s])
-                got = c.logits(s)
-                assert np.array_equal(got, want), f"step {step} seq {s}: max |d| {np.abs(got - want).max():.3g}"
-                cur[s] = int(np.argmax(want))
-                pos[s] += 1
-        for om in oms:
-            om.close()
-    finally:
-        po.set_dot_order(po.GENERIC)
+    oms = [po.OracleModel(path, n_ctx=256) for _ in prompts]
+    m = llmi.Model(path)
+    c = llmi.Context(m, n_ctx=256, n_seq=4)
+    cur, pos = [], []
+    for s, p in enumerate(prompts):
+        for k, t in enumerate(p[:-1]):
+            oms[s].decode(t, k, logits=False)
+        assert c.decode(p[:-1], seq=[s] * (len(p) - 1)) == 0
+        cur.append(p[-1])
+        pos.append(len(p) - 1)
+    for step in range(6):
+        assert c.decode(cur, pos=pos, seq=[0, 1, 2, 3], logits_all=True) == 0
+        for s in range(4):
+            want = oms[s].decode(cur[s], pos[s])
+            got = c.logits(s)
+            assert np.array_equal(got, want), f"step {step} seq {s}: max |d| {np.abs(got - want).max():.3g}"
+            cur[s] = int(np.argmax(want))
+            pos[s] += 1
+    for om in oms:
+        om.close()
+

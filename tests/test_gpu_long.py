@@ -33,25 +33,21 @@ import pyoracle as po
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_run(path, prompt, n_ctx, n_gen, order=po.DEVICE_ORDER):
+def _oracle_run(path, prompt, n_ctx, n_gen):
     """Oracle logits after the prompt (batched or_prefill for all but the last token)
     and for n_gen greedy steps after it."""
-    po.set_dot_order(order)
-    try:
-        om = po.OracleModel(path, n_ctx=n_ctx)
-        if len(prompt) > 1:
-            om.prefill(prompt[:-1])
-        lo = om.decode(prompt[-1], len(prompt) - 1)
-        out = [lo]
-        pos = len(prompt)
-        for _ in range(n_gen):
-            lo = om.decode(int(np.argmax(lo)), pos)
-            out.append(lo)
-            pos += 1
-        om.close()
-        return out
-    finally:
-        po.set_dot_order(po.GENERIC)
+    om = po.OracleModel(path, n_ctx=n_ctx)
+    if len(prompt) > 1:
+        om.prefill(prompt[:-1])
+    lo = om.decode(prompt[-1], len(prompt) - 1)
+    out = [lo]
+    pos = len(prompt)
+    for _ in range(n_gen):
+        lo = om.decode(int(np.argmax(lo)), pos)
+        out.append(lo)
+        pos += 1
+    om.close()
+    return out
 
 
 def _gpu_run(path, prompt, n_ctx, n_gen):
@@ -268,7 +264,6 @@ def test_generic_order_tolerance_report(gpu, synth_dir, preset, n_vocab):
     rng = np.random.default_rng(21)
     prompt = [1] + [int(t) for t in rng.integers(3, 30000, 7)]
     n_gen = 12
-    po.set_dot_order(po.GENERIC)
     om = po.OracleModel(path, n_ctx=64)
     m = llmi.Model(path)
     c = llmi.Context(m, n_ctx=64)

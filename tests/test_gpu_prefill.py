@@ -23,24 +23,20 @@ pytestmark = pytest.mark.gpu
 
 
 def _oracle_prompt_logits(path, prompt, n_ctx, n_gen):
-    """Oracle (device order): logits after the prompt and greedy continuation logits."""
-    po.set_dot_order(po.DEVICE_ORDER)
-    try:
-        om = po.OracleModel(path, n_ctx=n_ctx)
-        out = []
-        lo = None
-        for pos, t in enumerate(prompt):
-            lo = om.decode(t, pos)
+    """Oracle (ggml's generic order): logits after the prompt and greedy continuation logits."""
+    om = po.OracleModel(path, n_ctx=n_ctx)
+    out = []
+    lo = None
+    for pos, t in enumerate(prompt):
+        lo = om.decode(t, pos)
+    out.append(lo)
+    pos = len(prompt)
+    for _ in range(n_gen):
+        t = int(np.argmax(lo))
+        lo = om.decode(t, pos)
         out.append(lo)
-        pos = len(prompt)
-        for _ in range(n_gen):
-            t = int(np.argmax(lo))
-            lo = om.decode(t, pos)
-            out.append(lo)
-            pos += 1
-        return out
-    finally:
-        po.set_dot_order(po.GENERIC)
+        pos += 1
+    return out
 
 
 def _gpu_prompt_logits(path, prompt, n_ctx, n_gen, monkeypatch=None, no_prefill=False):
