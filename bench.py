@@ -2,10 +2,15 @@
 """bench.py — decode tokens/sec + achieved HBM GB/s, Llama-3-8B Q4_K_M, 1->8 MI355X.
 
 BASELINE.json `metric` on `configs[1]`: Llama-3-8B-Instruct Q4_K_M, 128-token prompt ->
-greedy decode, one model replica per GPU.  A STEP is one decoded token (one pass of the
-hot path: 194 kernel launches replayed from a HIP graph; the next token is fed back on
-the device).  Workload per rank: prefill the 128-token prompt (untimed), W warmup
-tokens, then K timed tokens (defaults W=32, K=480: 512 generated tokens, 128->640 ctx).
+512-token greedy decode (context 128 -> 640), one model replica per GPU.  A STEP is one
+decoded token (one pass of the hot path: 162 kernel launches replayed from a HIP graph;
+the next token is fed back on the device).  Workload per rank: prefill the 128-token
+prompt (untimed), then untimed decode steps up to the timed window, W warmup tokens
+among them, then K timed tokens.  The window is placed on the C2 trajectory so that its
+mean context is the trajectory's (383.5): the defaults (W=32, K=480) time positions
+160..639; a short window (e.g. the driver's K=20) is centred at position 374..393.
+Beside `value`, `c2_full` times the whole trajectory: all 512 decode tokens after a
+fresh 128-token prompt.
 
 Multi-GPU (`torch.distributed.run --nproc-per-node N`): replicas only — each rank
 decodes its own stream (prompt seed 4+rank) with no data-path collective; rank 0's
@@ -29,7 +34,10 @@ sys.path.insert(0, os.path.join(ROOT, "llama-gguf-inference_amd"))
 import torch  # noqa: E402  (before libllmi: one HIP runtime per process, see llmi/_lib.py)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak per GPU (MI355X_MICROARCH.md)
-DOMINANT = "ffn_gate_up"  # k_matvec<0,true,3>: fused ffn_gate+ffn_up Q4_K matvec + SwiGLU
+DOMINANT = "ffn_gate_up"  # k_matvec<..., EPI_SWIGLU>: fused ffn_gate+ffn_up matvec + SwiGLU
+# ffn_gate / ffn_up weight type of each synthetic preset (llmi_synth.h type tables)
+GATE_TYPE = {"llama3-8b-q4km": "Q4_K", "llama3-70b-q4km": "Q4_K", "mistral7b-q6k": "Q6_K",
+             "mistral7b-q5km": "Q5_K", "tinyllama-q8_0": "Q8_0"}
 
 
 def parse(argv=None):
@@ -49,7 +57,8 @@ def parse(argv=None):
     ap.add_argument("--batch-steps", type=int, default=64)
     ap.add_argument("--eager", action="store_true",
                     help="launch the step kernels one by one instead of replaying HIP graphs (PMC passes)")
-    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r02"),
+    ap.add_argument("--no-c2-full", action="store_true", help="skip the full-trajectory (128 -> 640) timing")
+    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r03"),
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
     return ap.parse_args(argv)
 
@@ -105,10 +114,22 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+C2_PROMPT, C2_DECODE = 128, 512  # BASELINE.json configs[1]: 128-token prompt -> 512-token decode
+
+
+def window_start(prompt: int, steps: int, warmup: int) -> int:
+    """First position of the timed window: its mean context is the C2 trajectory's
+    (positions prompt .. prompt+511), and at least W warmup steps precede it."""
+    mid = prompt + (C2_DECODE - 1) / 2.0
+    return max(prompt + warmup, int(round(mid - (steps - 1) / 2.0)))
+
+
 def timed_decode(engine, dist: Dist, steps: int, warmup: int) -> tuple[float, float]:
-    """The contract's timed region: W untimed warmup steps, then exactly K steps bracketed
-    by barrier + device sync on both sides; returns (this rank's seconds, max over ranks)."""
-    engine.warmup(warmup)
+    """The contract's timed region: untimed steps up to the window (the last W of them the
+    warmup), then exactly K steps bracketed by barrier + device sync on both sides;
+    returns (this rank's seconds, max over ranks)."""
+    pre = window_start(engine.pos, steps, warmup) - engine.pos
+    engine.warmup(pre)
     dist.barrier()
     engine.sync()
     t0 = time.perf_counter()
@@ -152,11 +173,13 @@ class LlmiEngine:
             log(f"wrote {path} in {time.perf_counter() - t:.1f}s")
         dist.barrier()
         self.path = path
+        self.gate_type = GATE_TYPE.get(args.preset, "?")
         t = time.perf_counter()
         self.model = llmi.Model(path, main_gpu=dist.local_rank, no_upload=dist.rank != 0)
         self.load_s = time.perf_counter() - t
         self.fanout_s = replica_fanout(self.model, dist, llmi.rccl_unique_id)
-        n_ctx = ((args.prompt + args.warmup + args.steps + args.profile_steps + 2 + 255) // 256) * 256
+        last = window_start(args.prompt, args.steps, args.warmup) + args.steps
+        n_ctx = ((max(last, args.prompt + C2_DECODE) + args.profile_steps + 2 + 255) // 256) * 256
         self.ctx = llmi.Context(self.model, n_ctx=n_ctx, use_graphs=not args.eager)
         rng = np.random.default_rng(4 + dist.rank)
         bos = self.model.bos if self.model.bos >= 0 else 1
@@ -188,6 +211,20 @@ class LlmiEngine:
         import torch
 
         torch.cuda.synchronize()
+
+    def c2_full(self) -> dict:
+        """The whole C2 trajectory: the 128-token prompt again (KV cache rebuilt), then all
+        512 greedy decode tokens timed (context 128 -> 640), device-resident feedback."""
+        self.ctx.kv_clear()
+        assert self.ctx.decode(self.prompt) == 0
+        first = self.ctx.greedy(-1)
+        self.sync()
+        t0 = time.perf_counter()
+        self.ctx.generate_greedy(first, len(self.prompt), C2_DECODE)
+        self.sync()
+        dt = time.perf_counter() - t0
+        return {"tokens": C2_DECODE, "ctx": f"{len(self.prompt)}->{len(self.prompt) + C2_DECODE}",
+                "tok_s": round(C2_DECODE / dt, 2), "ms_per_token": round(dt / C2_DECODE * 1e3, 4)}
 
     def profile(self, n):
         """Per-class kernel time at the current position (consumes no tokens)."""
@@ -315,7 +352,9 @@ def main(argv=None):
     tok_s = n * args.steps / dt_max
     # end-to-end roofline: algorithmic bytes of the timed tokens / time (this rank)
     e2e_gbps = eng.bytes / (eng.us * 1e-6) / 1e9 if eng.us > 0 else 0.0
+    window = (eng.pos - args.steps, eng.pos)
     prof = eng.profile(args.profile_steps) if args.profile_steps > 0 else {}
+    c2 = eng.c2_full() if not args.no_c2_full and args.prompt == C2_PROMPT else None
     counts = [int(x) for x in args.batch_seqs.split(",") if x.strip()]
     batched = None
     if counts:
@@ -349,17 +388,21 @@ def main(argv=None):
             "dtype": "int8",
             "data": f"synthetic: random-init GGUF blocks with the exact {args.preset} shapes/type table "
                     f"(llmi_synth.h); random {args.prompt}-token prompts",
-            "config": {"workload": f"{args.preset}: {args.prompt}-token prompt -> greedy decode "
-                                   f"{args.warmup}+{args.steps} tokens, 1 replica per GPU",
-                       "model": args.preset, "prompt_tokens": args.prompt, "ctx_end": eng.pos,
+            "config": {"workload": f"{args.preset}: {args.prompt}-token prompt -> greedy decode on the "
+                                   f"{args.prompt}->{args.prompt + C2_DECODE} trajectory, {args.steps} timed tokens at "
+                                   f"positions {window[0]}..{window[1] - 1} (mean context of the trajectory), "
+                                   "1 replica per GPU",
+                       "model": args.preset, "prompt_tokens": args.prompt, "timed_window": list(window),
                        "parallelism": f"replicas x{n} (RCCL weight fan-out)", "global_batch": n},
-            "roofline": {"bound": "hbm", "kernel": "k_matvec<0,true,3> (ffn_gate+ffn_up Q4_K + SwiGLU)",
+            "c2_full": c2,
+            "roofline": {"bound": "hbm", "kernel": f"k_matvec (ffn_gate+ffn_up {eng.gate_type} + SwiGLU)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "traffic_source": (prof_c.get("source") if traffic else
                                             f"null: no FETCH_SIZE pass committed for preset {args.preset}"),
                          "bytes_per_launch": k["bytes"], "us_per_launch": round(k["us"], 3),
-                         "us_source": "start/stop events on each launch in this run (llmi_profile_kernels)",
+                         "us_source": "kernel start/stop events on every launch of 20 whole decode steps "
+                                      "in this run, each kernel in its place in the step (llmi_profile_kernels)",
                          "rocprof_us_per_launch": prof_c.get("rocprof_us"),
                          "rocprof_frac": (round(k["bytes"] / (prof_c["rocprof_us"] * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
                                           if prof_c.get("rocprof_us") else None)},

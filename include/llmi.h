@@ -155,16 +155,16 @@ double llmi_model_upload_s(const struct llama_model* model);
 /* Roofline accounting of the last llama_decode / llmi_generate_greedy call:
  * algorithmic HBM bytes it streamed and its device time in microseconds. */
 void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec);
-/* Per-kernel-class device timing (roofline evidence).  For each class k in [0,7) the
- * class's launches of n_steps decode steps at position pos0 (token `first`; every
- * layer, the decode graph's exact grids and arguments) run back to back, each timed by
- * an event pair recorded at kernel start and end (hipExtLaunchKernelGGL):
- * us[k] = mean device microseconds per launch (execution only, no launch gaps),
- * bytes[k] = mean algorithmic HBM bytes per launch, launches[k] = launches per step.
- * Consumes no tokens: the context is left ready to decode `first` at pos0.
- * Classes: 0 embed, 1 qkv(+RoPE, KV write), 2 attention (1 or 2 kernels), 3
- * attn_output(+residual), 4 ffn_gate_up(+SwiGLU), 5 ffn_down(+residual), 6
- * output(+argmax).  0 on success. */
+/* Per-kernel-class device timing (roofline evidence), in situ: n_steps whole decode
+ * steps at position pos0 (token `first`; the decode graph's exact kernels, grids and
+ * arguments in their order) are launched one by one, every kernel armed with an event
+ * pair recorded at kernel start and end (hipExtLaunchKernelGGL), so each kernel runs
+ * after its real predecessor: us[k] = mean device microseconds per launch of class k
+ * (execution only, no launch gaps), bytes[k] = mean algorithmic HBM bytes per launch,
+ * launches[k] = launches per step.  Consumes no tokens: the context is left ready to
+ * decode `first` at pos0.  Classes: 0 embed, 1 qkv(+RoPE, KV write), 2 attention (1-4
+ * kernels, timed as one), 3 attn_output(+residual), 4 ffn_gate_up(+SwiGLU), 5
+ * ffn_down(+residual), 6 output(+argmax).  0 on success. */
 int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps,
                              double* us, double* bytes, int32_t* launches);
 /* Test options (tests only; no environment variable reaches these): sets `name` to

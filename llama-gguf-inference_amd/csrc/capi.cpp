@@ -542,37 +542,40 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
         return -1;
     }
     (void)hipSetDevice(c.m->device);
-    // Per kernel class: the class's launches of n_steps steps at position pos0 (every
-    // layer, the decode graph's exact grids and arguments) are launched back to back,
-    // each armed with an event pair that the runtime records when the kernel starts
-    // and ends (hipExtLaunchKernelGGL): kernel execution time without launch gaps.
-    // The per-layer classes rotate through every layer's weights, so each launch
-    // streams its matrix from HBM as in decode.  No tokens are consumed: the state is
-    // reset to (first, pos0) afterwards.
+    // In situ: n_steps whole decode steps at position pos0 (the decode graph's exact
+    // kernels, grids and arguments, in their order), launched one by one with EVERY
+    // kernel armed with an event pair that the runtime records when it starts and ends
+    // (hipExtLaunchKernelGGL): each kernel's execution time in its real place in the
+    // step (caches as its predecessor leaves them), without launch gaps.  One warm step
+    // first.  No tokens are consumed: the state is reset to (first, pos0) afterwards.
     const int kv_bound = std::min(c.n_ctx, (pos0 / 256 + 1) * 256);
     std::string err;
     int rc = 0;
-    for (int k = 0; k < K_NCLASS && rc == 0; ++k) {
-        Prof pe;
-        pe.only = K_EMBED;
-        Prof pk;
-        pk.only = k;
-        pk.timed = true;
-        if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); rc = -3; break; }
-        c.prof = &pe;  // sets pos/token of the step
+    {
+        Prof warm;
+        if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { set_err("state set failed"); return -3; }
+        c.prof = &warm;
         bool ok = step_enqueue(c, kv_bound, err);
-        c.prof = &pk;
-        for (int r = 0; ok && r < n_steps; ++r) ok = step_enqueue(c, kv_bound, err);
+        Prof pk;
+        pk.timed = true;
+        for (int r = 0; ok && r < n_steps; ++r) {
+            if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess) { ok = false; break; }
+            c.prof = &pk;
+            ok = step_enqueue(c, kv_bound, err);
+        }
         c.prof = nullptr;
         if (!ok || hipStreamSynchronize(c.stream) != hipSuccess) {
             set_err("llmi_profile_kernels: " + (err.empty() ? std::string("launch failed") : err));
             rc = -4;
-            break;
         }
-        const int n = std::max(1, pk.launches);
-        us[k] = pk.used ? pk.elapsed_us() / (double)pk.used : 0.0;
-        bytes[k] = (pk.bytes + pk.per_kv * (double)(pos0 + 1)) / n;
-        launches[k] = pk.launches / n_steps;
+        for (int k = 0; rc == 0 && k < K_NCLASS; ++k) {
+            int used = 0;
+            const double t = pk.elapsed_us(k, &used);
+            const int n = std::max(1, pk.launches[k]);
+            us[k] = used ? t / (double)used : 0.0;
+            bytes[k] = (pk.bytes[k] + pk.per_kv[k] * (double)(pos0 + 1)) / n;
+            launches[k] = pk.launches[k] / n_steps;
+        }
     }
     if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess) {
         if (rc == 0) { set_err("llmi_profile_kernels: state reset failed"); rc = -4; }
@@ -833,13 +836,13 @@ int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, co
                      int32_t n_tok, float* y, double* usec) {
     if (!pf_gemm_ok(type, (int)rows, (int)cols) || n_tok <= 0) { set_err("llmi_pf_gemm: unsupported type/shape"); return -1; }
     const int tpad = (n_tok + 31) / 32 * 32;
-    int8_t* aq = nullptr;
+    void* aq = nullptr;
     int16_t* abs = nullptr;
     float* ad = nullptr;
-    hipError_t e = hipMalloc(&aq, (size_t)tpad * cols);
+    hipError_t e = hipMalloc(&aq, (size_t)tpad * cols * 2);
     if (e == hipSuccess) e = hipMalloc(&abs, (size_t)tpad * (cols / 16) * 2);
     if (e == hipSuccess) e = hipMalloc(&ad, (size_t)tpad * (cols / 32) * 4);
-    if (e == hipSuccess) e = hipMemset(aq, 0, (size_t)tpad * cols);
+    if (e == hipSuccess) e = hipMemset(aq, 0, (size_t)tpad * cols * 2);
     if (e == hipSuccess) e = hipMemset(abs, 0, (size_t)tpad * (cols / 16) * 2);
     if (e == hipSuccess) e = hipMemset(ad, 0, (size_t)tpad * (cols / 32) * 4);
     if (e == hipSuccess) e = launch_pf_quant(x, (int)cols, nw, eps, (int)cols, act_kind(type), n_tok, aq, abs, ad, nullptr);

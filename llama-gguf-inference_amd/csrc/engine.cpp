@@ -459,24 +459,29 @@ bool context_fault_ok(Context& c, std::string& err) {
     return false;
 }
 
-bool Prof::arm() {
+bool Prof::arm(int k) {
     if (!timed) return true;
     while (ev.size() < 2 * (used + 1)) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return false;
         ev.push_back(e);
     }
+    if (ev_cls.size() < used + 1) ev_cls.resize(used + 1);
+    ev_cls[used] = k;
     set_launch_events(ev[2 * used], ev[2 * used + 1]);
     ++used;
     return true;
 }
 void Prof::disarm() { set_launch_events(nullptr, nullptr); }
-double Prof::elapsed_us() const {
+double Prof::elapsed_us(int k, int* n) const {
     double t = 0;
+    int cnt = 0;
     for (size_t i = 0; i < used; ++i) {
+        if (ev_cls[i] != k) continue;
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) == hipSuccess) t += ms * 1e3;
+        if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) == hipSuccess) { t += ms * 1e3; ++cnt; }
     }
+    if (n) *n = cnt;
     return t;
 }
 Prof::~Prof() {
@@ -530,7 +535,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
 #define LLMI_RUN(K, EXPR)                                  \
     do {                                                   \
         if (want(K)) {                                     \
-            if (P && !P->arm()) {                          \
+            if (P && !P->arm(K)) {                         \
                 err = "hipEventCreate failed";             \
                 return false;                              \
             }                                              \
@@ -777,7 +782,7 @@ bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& er
 // one launch per op over all of them (prefill.hip.inc): embed -> per layer [norm+quant,
 // q/k/v GEMMs (RoPE, KV write), causal attention, quant, attn_output GEMM (+residual),
 // norm+quant, gate/up GEMM (SwiGLU), quant, down GEMM (+residual)].  Results equal T
-// decode steps bit for bit (the GEMM keeps the matvec's device order); the caller runs
+// decode steps bit for bit (both follow ggml's generic order); the caller runs
 // the prompt's last token as an ordinary decode step for its logits.
 // ---------------------------------------------------------------------------------
 bool prefill_supported(const Model& m) {
@@ -804,11 +809,11 @@ static bool prefill_alloc(Context& c, std::string& err) {
     HIPC(hipMalloc(&c.pf_q, cap * QD * 4));
     HIPC(hipMalloc(&c.pf_att, cap * QD * 4));
     HIPC(hipMalloc(&c.pf_h, cap * F * 4));
-    HIPC(hipMalloc(&c.pf_aq, cap * maxc));
+    HIPC(hipMalloc(&c.pf_aq, cap * maxc * 2));
     HIPC(hipMalloc(&c.pf_abs, cap * (maxc / 16) * 2));
     HIPC(hipMalloc(&c.pf_ad, cap * (maxc / 32) * 4));
     // padded token rows of the activation buffers are read (never stored): keep them finite
-    HIPC(hipMemsetAsync(c.pf_aq, 0, cap * maxc, c.stream));
+    HIPC(hipMemsetAsync(c.pf_aq, 0, cap * maxc * 2, c.stream));
     HIPC(hipMemsetAsync(c.pf_abs, 0, cap * (maxc / 16) * 2, c.stream));
     HIPC(hipMemsetAsync(c.pf_ad, 0, cap * (maxc / 32) * 4, c.stream));
     c.pf_cap = cap;

@@ -43,26 +43,26 @@ struct Model {
 };
 
 // Kernel-class timing (llmi_profile_kernels): step_enqueue with a Prof attached only
-// enqueues the launches of class `only` (all classes if -1) and records their
-// algorithmic bytes; the caller captures that subset into a graph and times replays
-// of it between two events on the context stream.
+// enqueues the launches of class `only` (all classes if -1), records their algorithmic
+// bytes per class and, when `timed`, arms an event pair (kernel start / end) on each.
 enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_NCLASS };
 struct Prof {
-    int only = -1;               // class filter
+    int only = -1;               // class filter (-1: every class)
     bool timed = false;          // arm an event pair around every filtered launch
-    int launches = 0;            // launches of the filtered class enqueued
-    double bytes = 0;            // their fixed algorithmic bytes ...
-    double per_kv = 0;           // ... + per_kv * n_kv (attention: K and V rows read)
+    int launches[K_NCLASS] = {};    // launches enqueued per class
+    double bytes[K_NCLASS] = {};    // their fixed algorithmic bytes ...
+    double per_kv[K_NCLASS] = {};   // ... + per_kv * n_kv (attention: K and V rows read)
     std::vector<hipEvent_t> ev;  // 2 per timed launch
+    std::vector<int> ev_cls;     // class of each timed launch
     size_t used = 0;
     bool want(int k) const { return only < 0 || only == k; }
     void add(int k, double b, double b_per_kv = 0.0) {
         if (!want(k)) return;
-        ++launches; bytes += b; per_kv += b_per_kv;
+        ++launches[k]; bytes[k] += b; per_kv[k] += b_per_kv;
     }
-    bool arm();                  // next event pair -> set_launch_events
+    bool arm(int k);             // next event pair -> set_launch_events
     static void disarm();
-    double elapsed_us() const;   // sum over the recorded pairs (after a sync)
+    double elapsed_us(int k, int* n) const;  // sum over class k's recorded pairs (after a sync)
     ~Prof();
 };
 
@@ -110,7 +110,7 @@ struct Context {
     int pf_cap = 0;
     int32_t* pf_tok = nullptr;
     float *pf_x = nullptr, *pf_q = nullptr, *pf_att = nullptr, *pf_h = nullptr;
-    int8_t* pf_aq = nullptr;
+    void* pf_aq = nullptr;         // f16 MFMA fragments of the ubatch's activations
     int16_t* pf_abs = nullptr;
     float* pf_ad = nullptr;
     ~Context();

@@ -134,8 +134,8 @@ struct PfGemm {
     Seg w, w2;                 // weights (SWIGLU: w = gate, w2 = up)
     int rows = 0, cols = 0;
     int T = 0;                 // tokens (activation rows are padded to a multiple of 32)
-    const int8_t* aq = nullptr;   // [Tpad][cols] q8 activations, natural order
-    const int16_t* abs = nullptr; // [Tpad][cols/16] bsums (q8_K)
+    const void* aq = nullptr;     // f16 MFMA fragments of the q8 activations (prefill.hip.inc pf_aq_off), Tpad x cols x 2 B
+    const int16_t* abs = nullptr; // [Tpad][cols/32] bsum pairs (q8_K)
     const float* ad = nullptr;    // [Tpad][cols/256] (q8_K) or [Tpad][cols/32] (q8_0) d
     float* y = nullptr;        // STORE / ADD / SWIGLU / QKV q: [T][ldy]
     int ldy = 0;
@@ -156,7 +156,7 @@ struct PfAttn {
 bool pf_gemm_ok(int type, int rows, int cols);
 hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* toks, float* X, int T, int32_t* hist,
                            int pos0, int n_ctx, hipStream_t s);
-hipError_t launch_pf_quant(const float* x, int ldx, const float* nw, float eps, int cols, int act, int T, int8_t* aq,
+hipError_t launch_pf_quant(const float* x, int ldx, const float* nw, float eps, int cols, int act, int T, void* aq,
                            int16_t* abs, float* ad, hipStream_t s);
 hipError_t launch_pf_gemm(const PfGemm& g, int epi, hipStream_t s);
 hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipStream_t s);

@@ -18,11 +18,17 @@ module answers that contract:
   tokens, tok/s over decode time, HBM GB/s of the last decode call (the gateway passes
   the body through, scripts/gateway.py:360-363)
 
-Decoding is greedy (temperature is accepted and ignored: the north star's workload is
-greedy); `ignore_eos` and `n_predict` follow llama-server.  Every GPU replica is one
-llmi Context with `--parallel` sequences (llama-server's slots) driven by one scheduler
-thread: requests go to the least-loaded replica and are decoded there together, one
-batched step per token for up to 8 sequences (continuous batching).
+Sampling follows llama-server (llmi/sampling.py): temperature / top_k / top_p / min_p /
+repeat, presence and frequency penalties / seed per request, llama-server's defaults
+(temperature 0.8, top_k 40, top_p 0.95, min_p 0.05) or the --temp / --top-k / ... flags;
+`stop` strings end the generation (the text stops before them); `ignore_eos` and
+`n_predict` follow llama-server; `n` > 1 and `logprobs` are rejected with a 400.
+Greedy requests (temperature 0 or top_k 1, no penalties) decode on the device with
+on-device argmax feedback; sampled ones copy each step's logits to the host.  Every GPU
+replica is one llmi Context with `--parallel` sequences (llama-server's slots) driven by
+one scheduler thread: requests go to the least-loaded replica and are decoded there
+together, one batched step per token for up to 8 sequences (continuous batching,
+SURVEY.md §8f row 3).
 
 Text: the GGUF's own tokenizer (SPM or byte-level BPE from tokenizer.ggml.*) and chat
 template (tokenizer.chat_template, sandboxed Jinja2), llmi/tokenizer.py; streamed text
@@ -40,6 +46,8 @@ import time
 import uuid
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Callable, Iterable, Optional
+
+from .sampling import Sampler, SamplingParams, StopFilter, find_stop, parse_stop
 
 VERSION = "llmi-server 0.1 (libllmi, gfx950)"
 
@@ -171,10 +179,15 @@ class TextCodec:
 # driven by one scheduler thread (continuous batching)
 # --------------------------------------------------------------------------------------
 class Request:
-    """One generation: prompt ids in, token lists out through `q` (None terminates)."""
+    """One generation: prompt ids in, token lists out through `q` (None terminates).
+    `sampling` None or greedy: device argmax; else a host Sampler over each step's logits.
+    `stop`: strings that end the generation (checked on the detokenized output)."""
 
-    def __init__(self, prompt: list[int], max_tokens: int, ignore_eos: bool):
+    def __init__(self, prompt: list[int], max_tokens: int, ignore_eos: bool,
+                 sampling: Optional[SamplingParams] = None, stop: Optional[list[str]] = None):
         self.prompt, self.max_tokens, self.ignore_eos = list(prompt), max_tokens, ignore_eos
+        self.sampler = Sampler(sampling) if sampling is not None and not sampling.greedy else None
+        self.stop = list(stop or [])
         self.out: list[int] = []
         self.q: "queue.Queue" = queue.Queue()
         self.finish: Optional[str] = None
@@ -209,9 +222,11 @@ class Replica:
     and advances all active ones together with llmi_generate_greedy_batch (one weight
     stream per step for up to 8 sequences), `chunk` tokens per call."""
 
-    def __init__(self, idx: int, ctx, slots: int, eog: set, chunk: int, n_ctx: int, device: int = 0):
+    def __init__(self, idx: int, ctx, slots: int, eog: set, chunk: int, n_ctx: int, device: int = 0,
+                 detok: Optional[Callable[[list[int]], str]] = None):
         self.idx, self.ctx, self.slots, self.eog, self.chunk, self.n_ctx = idx, ctx, slots, eog, chunk, n_ctx
         self.device = device
+        self.detok = detok
         self.pending: "queue.Queue[Request]" = queue.Queue()
         self.active: list[Request] = []
         self.free = list(range(slots))
@@ -265,7 +280,7 @@ class Replica:
             self.busy_s += time.perf_counter() - t0
             if rc != 0:
                 raise RuntimeError(f"llama_decode returned {rc}")
-            first = c.greedy(-1)
+            first = c.greedy(-1) if r.sampler is None else r.sampler.sample(c.logits(-1), r.prompt)
             r.seq, r.pos = seq, len(r.prompt)
             if self._take(r, [first]):
                 self.free.append(seq)
@@ -290,6 +305,9 @@ class Replica:
                 break
         r.emit(emit)
         self.tokens += len(emit)
+        if r.stop and self.detok is not None and find_stop(self.detok(r.out), r.stop) is not None:
+            r.done("stop")
+            return True
         if len(r.out) >= r.max_tokens:
             r.done("length")
             return True
@@ -298,14 +316,27 @@ class Replica:
     def _step(self) -> None:
         batch = self.active[:8]
         k = max(1, min(self.chunk, min(r.max_tokens - len(r.out) for r in batch)))
+        if any(r.stop for r in batch):
+            k = min(k, 4)  # stop strings are checked between decode calls
         c = self.ctx
         t0 = time.perf_counter()
-        try:
-            outs = c.generate_greedy_batch([r.seq for r in batch], [r.last for r in batch], [r.pos for r in batch], k)
-        except Exception:
-            # not batchable here (e.g. a context past the batched attention's bound):
-            # one sequence at a time, same results
-            outs = [c.generate_greedy_batch([r.seq], [r.last], [r.pos], k)[0] for r in batch]
+        if any(r.sampler is not None for r in batch):
+            # one token per call: every slot's logits (llama_decode with one token per
+            # sequence = one batched step), sampled on the host or argmax on the device
+            k = 1
+            rc = c.decode([r.last for r in batch], pos=[r.pos for r in batch], seq=[r.seq for r in batch],
+                          logits_all=True)
+            if rc != 0:
+                raise RuntimeError(f"llama_decode returned {rc}")
+            outs = [[c.greedy(i) if r.sampler is None else r.sampler.sample(c.logits(i), r.prompt + r.out)]
+                    for i, r in enumerate(batch)]
+        else:
+            try:
+                outs = c.generate_greedy_batch([r.seq for r in batch], [r.last for r in batch], [r.pos for r in batch], k)
+            except Exception:
+                # not batchable here (e.g. a context past the batched attention's bound):
+                # one sequence at a time, same results
+                outs = [c.generate_greedy_batch([r.seq], [r.last], [r.pos], k)[0] for r in batch]
         self.busy_s += time.perf_counter() - t0
         self._stats()
         done = []
@@ -346,8 +377,9 @@ class Engine:
     ties to the lowest index) and are served there with continuous batching."""
 
     def __init__(self, path: str, n_ctx: int, n_gpu_layers: int, devices: list[int], slots: int = 4,
-                 chunk: int = 8, contexts=None):
+                 chunk: int = 8, contexts=None, sampling: Optional[SamplingParams] = None):
         self.path, self.n_ctx, self.ngl, self.devices = path, n_ctx, n_gpu_layers, devices
+        self.sampling = sampling or SamplingParams()  # server defaults (llama-server's)
         self.slots, self.chunk = max(1, slots), max(1, chunk)
         self.ready = False
         self.error: Optional[str] = None
@@ -379,23 +411,27 @@ class Engine:
                     else T.make_tokenizer(meta)
                 self.vocab = TextCodec(tok, meta.get("tokenizer.chat_template"))
             eog = getattr(self.vocab, "eog", {self.vocab.eos})
+            detok = getattr(self.vocab, "detokenize", None)
             self.replicas = [Replica(i, c, self.slots, eog, self.chunk, self.n_ctx,
-                                     self.devices[i] if i < len(self.devices) else i) for i, c in enumerate(ctxs)]
+                                     self.devices[i] if i < len(self.devices) else i, detok)
+                             for i, c in enumerate(ctxs)]
             self.load_s = time.perf_counter() - t0
             self.t_ready = time.perf_counter()
             self.ready = True
         except Exception as e:  # reported by /health
             self.error = str(e)
 
-    def submit(self, prompt: list[int], max_tokens: int, ignore_eos: bool) -> Request:
-        r = Request(prompt, max_tokens, ignore_eos)
+    def submit(self, prompt: list[int], max_tokens: int, ignore_eos: bool,
+               sampling: Optional[SamplingParams] = None, stop: Optional[list[str]] = None) -> Request:
+        r = Request(prompt, max_tokens, ignore_eos, sampling, stop)
         rep = min(self.replicas, key=lambda x: (x.load(), x.idx))
         rep.submit(r)
         return r
 
     def generate(self, prompt: list[int], max_tokens: int, ignore_eos: bool, on_tokens: Callable[[list[int]], None],
-                 chunk: int = 8) -> tuple[list[int], str]:
-        r = self.submit(prompt, max_tokens, ignore_eos)
+                 chunk: int = 8, sampling: Optional[SamplingParams] = None,
+                 stop: Optional[list[str]] = None) -> tuple[list[int], str]:
+        r = self.submit(prompt, max_tokens, ignore_eos, sampling, stop)
         while True:
             toks = r.q.get()
             if toks is None:
@@ -515,6 +551,12 @@ class Handler(BaseHTTPRequestHandler):
             max_tokens = int(req.get("max_tokens", req.get("n_predict", 16 if not chat else 256)))
             if max_tokens < 0:
                 max_tokens = eng.n_ctx
+            if int(req.get("n", 1)) != 1:
+                raise ValueError("only n = 1 is supported")
+            if req.get("logprobs") not in (None, False, 0) or req.get("top_logprobs") not in (None, 0):
+                raise ValueError("logprobs are not supported")
+            sampling = getattr(eng, "sampling", SamplingParams()).with_request(req)
+            stop = parse_stop(req.get("stop"))
         except (ValueError, TypeError) as e:
             return self._send_json(400, _error(400, str(e), "invalid_request_error"))
         ignore_eos = bool(req.get("ignore_eos", False))
@@ -524,10 +566,14 @@ class Handler(BaseHTTPRequestHandler):
         obj = "chat.completion" if chat else "text_completion"
         if not stream:
             try:
-                ids, finish = eng.generate(prompt, max_tokens, ignore_eos, lambda _t: None, chunk=32)
+                ids, finish = eng.generate(prompt, max_tokens, ignore_eos, lambda _t: None, chunk=32,
+                                           sampling=sampling, stop=stop)
             except Exception as e:  # a failed llama_decode: OpenAI-shaped 500, not a dropped socket
                 return self._send_json(500, _error(500, str(e), "server_error"))
             text = v.detokenize(ids)
+            cut = find_stop(text, stop)
+            if cut is not None:
+                text, finish = text[:cut], "stop"
             choice = ({"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": finish}
                       if chat else {"index": 0, "text": text, "logprobs": None, "finish_reason": finish})
             return self._send_json(200, {
@@ -553,19 +599,22 @@ class Handler(BaseHTTPRequestHandler):
                    "choices": [{"index": 0, "delta": {"role": "assistant"}, "finish_reason": None}]})
 
         sd = v.stream()
+        sf = StopFilter(stop)
 
         def on_tokens(ts: list[int]) -> None:
             for t in ts:
-                piece = sd.push(t)
+                piece = sf.push(sd.push(t))
                 if not piece:
-                    continue  # an incomplete UTF-8 sequence: held until its last byte
+                    continue  # an incomplete UTF-8 sequence, or a possible stop-string prefix: held back
                 ch = ({"index": 0, "delta": {"content": piece}, "finish_reason": None} if chat
                       else {"index": 0, "text": piece, "logprobs": None, "finish_reason": None})
                 event({"id": rid, "object": cobj, "created": created, "model": eng.model_id, "choices": [ch]})
 
         try:
-            ids, finish = eng.generate(prompt, max_tokens, ignore_eos, on_tokens, chunk=4)
-            tail = sd.flush()
+            ids, finish = eng.generate(prompt, max_tokens, ignore_eos, on_tokens, chunk=4, sampling=sampling, stop=stop)
+            tail = sf.push(sd.flush()) + sf.flush()
+            if sf.stopped:
+                finish = "stop"
             if tail:
                 ch = ({"index": 0, "delta": {"content": tail}, "finish_reason": None} if chat
                       else {"index": 0, "text": tail, "logprobs": None, "finish_reason": None})
@@ -609,6 +658,17 @@ def parse_args(argv=None):
     ap.add_argument("-np", "--parallel", type=int, default=int(os.environ.get("LLMI_SLOTS", "4")),
                     help="sequences (slots) per replica decoded together (continuous batching)")
     ap.add_argument("--decode-chunk", type=int, default=8, help="tokens per batched decode call")
+    # llama-server's sampling flags and defaults (per-request fields override them)
+    d = SamplingParams()
+    ap.add_argument("--temp", type=float, default=d.temperature)
+    ap.add_argument("--top-k", type=int, default=d.top_k)
+    ap.add_argument("--top-p", type=float, default=d.top_p)
+    ap.add_argument("--min-p", type=float, default=d.min_p)
+    ap.add_argument("--repeat-penalty", type=float, default=d.repeat_penalty)
+    ap.add_argument("--repeat-last-n", type=int, default=d.repeat_last_n)
+    ap.add_argument("--presence-penalty", type=float, default=d.presence_penalty)
+    ap.add_argument("--frequency-penalty", type=float, default=d.frequency_penalty)
+    ap.add_argument("-s", "--seed", type=int, default=d.seed)
     args, extra = ap.parse_known_args(argv)
     return args, extra
 
@@ -626,8 +686,11 @@ def main(argv=None) -> int:
     key = args.api_key
     if args.api_key_file:
         key = open(args.api_key_file).read().strip()
+    sp = SamplingParams(temperature=args.temp, top_k=args.top_k, top_p=args.top_p, min_p=args.min_p,
+                        repeat_penalty=args.repeat_penalty, repeat_last_n=args.repeat_last_n,
+                        presence_penalty=args.presence_penalty, frequency_penalty=args.frequency_penalty, seed=args.seed)
     eng = Engine(args.model, args.ctx_size, args.ngl, list(range(max(1, args.replicas))), slots=args.parallel,
-                 chunk=args.decode_chunk)
+                 chunk=args.decode_chunk, sampling=sp)
     srv = make_server(eng, args.host, args.port, key)
     threading.Thread(target=eng.load, daemon=True).start()
     print(f"[llmi-server] listening on {args.host}:{args.port}", file=sys.stderr, flush=True)

@@ -34,7 +34,7 @@ def test_server_matches_direct_decode(gpu, tiny_models):
         for stream in (False, True):
             conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
             conn.request("POST", "/v1/completions", body=json.dumps(
-                {"prompt": prompt, "max_tokens": n, "ignore_eos": True, "stream": stream}),
+                {"prompt": prompt, "max_tokens": n, "ignore_eos": True, "stream": stream, "temperature": 0}),
                 headers={"content-type": "application/json", "Connection": "close"})
             r = conn.getresponse()
             raw = r.read().decode()
@@ -47,6 +47,21 @@ def test_server_matches_direct_decode(gpu, tiny_models):
                 events = [e for e in raw.split("\n\n") if e]
                 text = "".join(json.loads(e[6:])["choices"][0]["text"] for e in events[:-1])
                 assert text == "".join(m.token_text(t) for t in want)
+        # sampled (llama-server's chain on the host logits): a fixed seed reproduces, and
+        # top_p -> 0 (only the most likely token kept) equals greedy through the sampled
+        # path's per-token batched steps
+        outs = []
+        for body in ({"temperature": 1.0, "seed": 11}, {"temperature": 1.0, "seed": 11},
+                     {"temperature": 1.0, "top_k": 0, "top_p": 1e-6, "min_p": 0.0}):
+            conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+            conn.request("POST", "/v1/completions", body=json.dumps(
+                {"prompt": prompt, "max_tokens": n, "ignore_eos": True, **body}),
+                headers={"content-type": "application/json", "Connection": "close"})
+            r = conn.getresponse()
+            outs.append(json.loads(r.read())["llmi"]["tokens"])
+            conn.close()
+        assert outs[0] == outs[1] and len(outs[0]) == n
+        assert outs[2] == want
     finally:
         srv.shutdown()
         srv.server_close()

@@ -30,8 +30,9 @@ class FakeEngine:
         self.n_ctx = 256
         self.calls = []
 
-    def generate(self, prompt, max_tokens, ignore_eos, on_tokens, chunk=8):
+    def generate(self, prompt, max_tokens, ignore_eos, on_tokens, chunk=8, sampling=None, stop=None):
         self.calls.append((list(prompt), max_tokens, ignore_eos))
+        self.last_sampling, self.last_stop = sampling, stop
         out = []
         t = prompt[-1]
         while len(out) < max_tokens:

@@ -15,6 +15,7 @@ import time
 
 import pytest
 
+from llmi.sampling import SamplingParams
 from llmi.server import Engine, Vocab, make_server
 
 V = 100
@@ -78,7 +79,9 @@ class FakeCtx:
 def _engine(n_rep, slots, delay=0.002):
     vocab = Vocab(["<unk>", "<s>", "</s>"] + [f" w{i}" for i in range(3, V)], 1, 2)
     ctxs = [FakeCtx(delay=delay) for _ in range(n_rep)]
-    eng = Engine("fake.gguf", 512, 99, list(range(n_rep)), slots=slots, chunk=4, contexts=(ctxs, vocab))
+    # the server started with --temp 0 (greedy by default; per-request fields still override)
+    eng = Engine("fake.gguf", 512, 99, list(range(n_rep)), slots=slots, chunk=4, contexts=(ctxs, vocab),
+                 sampling=SamplingParams(temperature=0.0))
     eng.load()
     assert eng.ready, eng.error
     return eng, ctxs
