@@ -4,10 +4,10 @@
 //
 // k_mvn is the matvec (kernels.hip k_matvec) with NT activation vectors: the prologue
 // quantizes the NT inputs into NT LDS images exactly as the single-token prologue does
-// (per-16 sub-block q8_K / q8_0, RMSNorm with a double sum); the main loop loads a row
-// pair's chunk once and forms NT sets of block terms against it, each folded onto its
-// token's chains in ggml's generic order (mv_device.h) — so every sequence's results are
-// bit-identical to its own single-token decode.
+// (per-16 sub-block q8_K / q8_0, RMSNorm with a double sum); the main loop loads each
+// lane's weight unit once and forms NT sets of block terms against it, each folded onto
+// its token's chains in ggml's generic order (mv_device.h) — so every sequence's results
+// are bit-identical to its own single-token decode.
 //
 // Attention runs the split kernels' bodies (mv_device.h) with a third grid dimension
 // over the batch slots, each slot reading its own sequence's KV cache.
@@ -121,125 +121,75 @@ __device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t) {
 
 }  // namespace
 
-// fold buffer floats per wave for NT tokens: [NT][2 rows][kFoldRow] + the chain results [NT][18]
-template <int NT>
-__host__ __device__ constexpr int mvn_fold_floats() { return NT * 2 * kFoldRow + ((NT * 18 + 3) & ~3); }
-
 template <int ACT, bool NORM, int EPI, int T, int NT>
 __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const size_t img = img_bytes(ACT, A.cols);
     double* red = (double*)(smem + NT * img);
-    constexpr int NC = ACT ? 1 : 9;   // chains per row
-    constexpr int NF = 2 * NC * NT;   // fold chains of the wave
-    constexpr int NU = (NF + 63) / 64;
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
-    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * mvn_fold_floats<NT>();
-    float* Gr = F + NT * 2 * kFoldRow;  // [NT][2 * NC] chain results
-    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * kFoldFloats;
+    const TaskGeo g = task_geo(A);
+    const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
+    const int r = lane / g.lr, ul = lane - r * g.lr;
     const int G = gridDim.x * kBW;
-    const int my_pos = A.tpos ? A.tpos[lane < NT ? lane : 0] : 0;
-    unsigned long long best = 0;  // lane t < NT: token t's LOGITS key
+    unsigned long long best[NT];  // per token: the lane's LOGITS key
+#pragma unroll
+    for (int t = 0; t < NT; ++t) best[t] = 0;
     bprologue<ACT, NORM, NT>(A, smem, img, red);
 
-    int p = blockIdx.x * kBW + wave;
-    if (p < A.npairs) {
-        PairRef r = pair_ref<EPI>(A, p);
-        PairRows<T> rows = pair_rows<T>(r, A.cols);
-        PairRaw<T> cur = load_item<T>(rows, lane, nch);
-        int j = 0;
-        float acc[NU];
+    int task = blockIdx.x * kBW + wave;
+    if (task < A.ntasks) {
+        int s = 0;
+        Sub b = sub_of<EPI>(A, g, task, 0);
+        Seg sg = pick(A, b.si);
+        LaneUnit lu = lane_unit(g, b, sg, r, ul);
+        UnitW<T> cur = load_unit<T>(sg, lu.row, lu.u, g.U);
+        float acc[NT], vg[NT];
 #pragma unroll
-        for (int u = 0; u < NU; ++u) acc[u] = 0.f;
+        for (int t = 0; t < NT; ++t) acc[t] = vg[t] = 0.f;
         for (;;) {
-            int pn = p, jn = j + 1;
-            PairRef rn = r;
-            PairRows<T> rowsn = rows;
-            if (jn == NJ) {
-                jn = 0;
-                pn = p + G;
-                if (pn < A.npairs) {
-                    rn = pair_ref<EPI>(A, pn);
-                    rowsn = pair_rows<T>(rn, A.cols);
-                }
+            int tn = task, sn = s + 1;
+            if (sn == S) {
+                sn = 0;
+                tn = task + G;
             }
-            const bool has_next = pn < A.npairs;
-            PairRaw<T> nxt{};
-            if (has_next) nxt = load_item<T>(rowsn, lane + 64 * jn, nch);
-            const int ch = lane + 64 * j;
-            const int chc = ch < nch ? ch : nch - 1;
+            const bool has_next = tn < A.ntasks;
+            Sub bn = b;
+            Seg sgn = sg;
+            if (has_next) {
+                bn = sub_of<EPI>(A, g, tn, sn);
+                sgn = pick(A, bn.si);
+            }
+            const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
+            const UnitW<T> nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const Act act = load_act<ACT>(carve_t(smem, ACT, A.cols, t, img), chc, nch);
-                item_terms<T>(cur.a, act, chc, ch < nch, F + t * 2 * kFoldRow);
-                item_terms<T>(cur.b, act, chc, ch < nch, F + t * 2 * kFoldRow + kFoldRow);
+                float tm[9];
+                unit_terms<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, tm);
+                const MVArgs B = token_view(A, t);
+                const int pos = A.tpos ? A.tpos[t] : 0;
+                sub_finish<ACT, EPI>(B, F, g, s, b, sg, tm, lu, r, ul, acc[t], vg[t], pos, best[t]);
             }
-            wave_lds_sync();
-            {   // fold chain f = (token, row, chain) onto acc[u] of lane f - 64 u
-                const int nb = item_blocks<ACT>(A.cols, j);
-                constexpr int CS = ACT ? 128 : 16;
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int f = lane + 64 * u;
-                    if (f < NF) {
-                        const int t = f / (2 * NC), rr = f % (2 * NC), row = rr / NC, c = rr % NC;
-                        const float* q = F + t * 2 * kFoldRow + row * kFoldRow + c * CS;
-                        for (int b = 0; b < nb; b += 4) {
-                            const float4 v = *(const float4*)(q + b);
-                            acc[u] += v.x;
-                            if (b + 1 < nb) acc[u] += v.y;
-                            if (b + 2 < nb) acc[u] += v.z;
-                            if (b + 3 < nb) acc[u] += v.w;
-                        }
-                    }
-                }
-            }
-            if (j == NJ - 1) {
-                wave_lds_sync();
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int f = lane + 64 * u;
-                    if (f < NF) Gr[f] = acc[u];
-                    acc[u] = 0.f;
-                }
-                wave_lds_sync();
-                if (lane < NT) {  // token `lane`: sumf chain + sums[0..7] of both rows, its epilogue
-                    const float* g = Gr + lane * 2 * NC;
-                    PairSum v;
-                    if constexpr (ACT) {
-                        v.a = g[0];
-                        v.b = g[1];
-                    } else {
-                        float sa = g[8], sb = g[17];
-#pragma unroll
-                        for (int l = 0; l < 8; ++l) {
-                            sa += g[l];
-                            sb += g[9 + l];
-                        }
-                        v.a = sa;
-                        v.b = sb;
-                    }
-                    const MVArgs B = token_view(A, lane);
-                    epilogue<EPI, false, MVArgs, true>(B, r, p, v, my_pos, best);
-                }
-            }
-            wave_lds_sync();
             if (!has_next) break;
             cur = nxt;
-            p = pn;
-            j = jn;
-            r = rn;
-            rows = rowsn;
+            task = tn;
+            s = sn;
+            b = bn;
+            sg = sgn;
+            lu = lun;
         }
     }
     if constexpr (EPI == EPI_LOGITS) {
-        // per token: workgroup max of the waves' keys (lane t holds token t's), one atomic
-        // into the slot of its sequence's StepState; workgroup 0 advances the sequence's
-        // next position
+        // per token: workgroup max of the lanes' keys, one atomic into the slot of its
+        // sequence's StepState; workgroup 0 advances the sequence's next position
         unsigned long long* wred = (unsigned long long*)red;  // [kBW][NT]
         __syncthreads();
-        if (lane < NT) wred[wave * NT + lane] = best;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const unsigned long long k = wave_max_u64(best[t]);
+            if (lane == 0) wred[wave * NT + t] = k;
+        }
         __syncthreads();
         if ((int)threadIdx.x < NT) {
             const int t = threadIdx.x;
@@ -298,12 +248,11 @@ __global__ __launch_bounds__(512) void k_battn_pv16(BAttnArgs b, int kvb) {
 
 // ---- launchers -----------------------------------------------------------------------------
 size_t mvn_lds_bytes(int act, int cols, int nt) {
-    const size_t fold = (size_t)nt * 2 * kFoldRow + (size_t)((nt * 18 + 3) & ~3);
-    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * fold * 4;
+    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * kFoldFloats * 4;
 }
 
 template <typename K>
-static int mvn_grid(K kernel, int npairs, size_t lds, int max_blocks) {
+static int mvn_grid(K kernel, int ntasks, size_t lds, int max_blocks) {
     static std::mutex mu;
     static std::map<std::tuple<const void*, size_t, int>, int> cache;
     int dev = 0;
@@ -324,7 +273,7 @@ static int mvn_grid(K kernel, int npairs, size_t lds, int max_blocks) {
             cache.emplace(key, cap);
         }
     }
-    int blocks = (npairs + kBW - 1) / kBW;
+    int blocks = (ntasks + kBW - 1) / kBW;
     blocks = std::min(blocks, std::min(cap, max_blocks));
     return std::max(blocks, 1);
 }
@@ -334,7 +283,7 @@ static hipError_t mvn_launch(const MVArgs& a, int max_blocks, hipStream_t s) {
     auto k = k_mvn<ACT, NORM, EPI, T, NT>;
     const size_t lds = mvn_lds_bytes(ACT, a.cols, NT);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const int blocks = mvn_grid(k, a.npairs, lds, max_blocks);
+    const int blocks = mvn_grid(k, a.ntasks, lds, max_blocks);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(kBT), lds, s, a);
     return hipGetLastError();
 }
@@ -374,8 +323,10 @@ static hipError_t mvn_type(const MVArgs& a, int epi, int nt, int max_blocks, hip
 
 static int mvn_pad(int nt) { return nt <= 1 ? 1 : nt == 2 ? 2 : nt <= 4 ? 4 : 8; }
 
-hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
-    if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0 || nt < 1 || nt > kMaxBatch) return hipErrorInvalidValue;
+hipError_t launch_mvn(const MVArgs& a0, int epi, int nt, int max_blocks, hipStream_t s) {
+    if (a0.nseg < 1 || a0.cols <= 0 || a0.cols % 256 || nt < 1 || nt > kMaxBatch) return hipErrorInvalidValue;
+    MVArgs a = a0;
+    if (!mv_geometry(a, epi)) return hipErrorInvalidValue;
     const int t = a.seg[0].type;
     for (int i = 1; i < a.nseg; ++i)
         if (a.seg[i].type != t) return hipErrorInvalidValue;  // callers group segments by type

@@ -1,20 +1,29 @@
 // common.h — shared host/device definitions of the llmi decode path.
 //
 // Device weight layouts (DESIGN.md §Data layout in HBM).  Every quantized matrix is
-// repacked once at load into "chunk-planar" form.  A CHUNK is 64 consecutive weights of
-// a row (K-quants: quarter c of a 256-block, whose low nibbles are weights 64c+0..31 and
-// high nibbles 64c+32..63 of native qs[32c..32c+31]; Q8_0: two 32-blocks).  The quant
-// bytes of each chunk are split into 16-B parts k and stored part-major per row:
-//     A[row][k][chunk][16 B]      (k < 2 for K-quants, k < 4 for Q8_0)
-// so lane L reading part k of chunk L touches 1 KiB of consecutive bytes per wave
-// instruction.  Per-block headers / per-chunk high bits live in their own planes.
-// Byte counts equal GGUF exactly (the repack moves bytes, it never widens them):
-//   Q4_K  A: qs 128 B/block   S: header {d, dmin, scales[12]} 16 B/block
-//   Q5_K  A: qs 128 B/block   H: 8 B/chunk (fifth bits: lo 32 then hi 32)   S: header 16 B/block
-//   Q6_K  A: ql 128 B/block   H: 16 B/chunk (2-bit highs, shift-decodable)
-//         S: scales 16 B/block (= 4 B/chunk, native order)   D: fp16 d 2 B/block
-//   Q8_0  A: qs 32 B/block    D: fp16 d 2 B/block (= 4 B/chunk)
+// repacked once at load into a UNIT-MAJOR planar form.  A UNIT is 256 consecutive
+// weights of a row (a K-quant block, or eight Q8_0 blocks); a row of `cols` weights has
+// U = cols / 256 units.  Each unit's quant bytes are split into 16-B PARTS p, stored
+// part-major per row:
+//     A[row][p][unit][16 B]   (8 parts for K-quants, 16 for Q8_0)
+// so lanes that hold consecutive units of a row read consecutive 16-B pieces (the
+// matvec gives lane L unit L of its row, kernels.hip).  Per-unit headers / high bits
+// live in their own planes, unit-major as well.  Byte counts equal GGUF exactly (the
+// repack moves bytes, it never widens them):
+//   Q4_K  A: qs 128 B/unit   S: header {d, dmin, scales[12]} 16 B/unit
+//   Q5_K  A: qs 128 B/unit   H: [row][2][unit][16 B] fifth bits   S: header 16 B/unit
+//   Q6_K  A: ql 128 B/unit   H: [row][4][unit][16 B] 2-bit highs (XOR 2)
+//         S: scales 16 B/unit (native order)   D: fp16 d 2 B/unit
+//   Q8_0  A: qs 256 B/unit (part p = 32-block p/2, half p%2)   D: 8 fp16 d = 16 B/unit
 //   F32/F16 plain (A).
+// K-quant parts are in RESIDUE ORDER: part p = 2c + k of chunk c (64 weights: low
+// nibbles = weights 64c + t, high nibbles = 64c + 32 + t of native qs[32c + t]), byte
+// 4m + i = native byte t = l + 8i with l = 4k + m: one dword holds the 8 weights of
+// residue class l (element index mod 8) of the chunk — the grouping ggml's generic dot
+// sums by (aux32[l], mv_device.h).  Q5_K fifth bits: 8 B per chunk (lo word: low-nibble
+// weights, hi word: high-nibble weights; bit 4l + i as above), chunks 2h, 2h+1 in H
+// part h.  Q6_K high bits: 16 B per chunk in H part c: dword 2*hi + k, byte i, bits 2m
+// (XOR 2, so v_perm maps them to the signed high part of q - 32).
 #pragma once
 
 #include <cstddef>

@@ -13,7 +13,7 @@ namespace llmi {
 #ifndef LLMI_MV_THREADS
 #define LLMI_MV_THREADS 256
 #endif
-constexpr int kMVThreads = LLMI_MV_THREADS;  // matvec workgroup; each wave owns one row pair at a time
+constexpr int kMVThreads = LLMI_MV_THREADS;  // matvec workgroup; each wave owns one row task at a time
 constexpr int kMVWaves = kMVThreads / 64;
 constexpr int kFusedAttnMaxKV = 8192;  // fused one-launch attention up to this KV bound (LDS scores)
 constexpr size_t kSplitAttnMaxLds = 128 * 1024;  // split attention: G * kv_bound f32 probabilities in LDS
@@ -55,7 +55,7 @@ struct MVArgs {
     Seg seg[3];
     int nseg = 0;
     int cols = 0;
-    int npairs = 0;              // row pairs (SWIGLU: gate/up pairs)
+    int npairs = 0;              // row pairs (SWIGLU: gate/up pairs) — sizes the launch
     const float* x = nullptr;    // f32[cols] input
     const float* nw = nullptr;   // RMSNorm weight (nullptr: quantize x as is)
     float eps = 0.f;
@@ -68,8 +68,12 @@ struct MVArgs {
     int head_dim = 0, n_rot = 0, n_ctx = 0, nq = 0, nk = 0;
     unsigned long long* argmax = nullptr;  // LOGITS
     unsigned long long* trace = nullptr;   // LLMI_EXP_TRACE builds: per-wave s_memrealtime stamps
-    int split_pairs = 0;                   // two-type launches: pairs of the first type group ...
-    int split_wgs = 0;                     // ... and the workgroups that run them (set by launch_matvec)
+    // row tasks (mv_device.h; set by launch_matvec / launch_mvn from the segments)
+    int lr = 0;                            // lanes per row (a multiple of 4)
+    int rpt = 0;                           // rows per task R (SwiGLU: gate/up pairs)
+    int ntasks = 0;
+    int split_tasks = 0;                   // two-type launches: tasks of the first type group ...
+    int split_wgs = 0;                     // ... and the workgroups that run them
     int xfirst = 0;                        // experiment: multi-round launches also wait for x before weights
     // batched decode (batch.hip, k_mvn): token t of the batch is one decode step of
     // sequence tseq[t] at position tpos[t]; x / y rows are x_stride / y_stride floats
@@ -163,6 +167,9 @@ hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipS
 
 // activation kind of a weight type: 0 = block_q8_K (K-quants), 1 = block_q8_0
 __host__ __device__ inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
+// row-task geometry of a matvec launch (lr, rpt, ntasks); false if the segments cannot
+// be cut into tasks (a QKV segment boundary that is not on an even row)
+bool mv_geometry(MVArgs& a, int epi);
 size_t mv_lds_bytes(int act, int cols);
 
 // All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).

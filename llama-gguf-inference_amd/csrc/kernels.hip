@@ -63,132 +63,84 @@ __host__ __device__ inline size_t fold_off(int act, int cols, int waves) {
 }
 size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + (size_t)kMVWaves * kFoldFloats * 4; }
 
-// The matvec of the pair range [pbeg, pend) by waves starting at pair p0 with stride G
-// (one type group of a launch); returns the wave's LOGITS argmax key.  Per item (pair
-// p, chunks lane + 64 j): the two rows' block terms into the wave's fold buffer F, the
-// 18 fold lanes add them onto their chains; after the pair's last item both row sums
-// (ggml's generic order, mv_device.h) go to the epilogue.
+// The matvec of the task range [tbeg, tend) by waves starting at task t0 with stride G
+// (one type group of a launch); returns the wave's LOGITS argmax key.  Per sub-item:
+// every lane's unit terms into the wave's fold buffer F, the fold lanes add them onto
+// their chains; after a row set's last sub-item the row sums (ggml's generic order,
+// mv_device.h) go to the epilogue.  The next sub-item's units are in flight meanwhile.
 template <int ACT, bool NORM, int EPI, int T, int NP>
-__device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int p0, int G, int pbeg,
-                                                      int pend) {
+__device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
+                                                      int tend) {
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = A.st->pos;
     unsigned long long best = 0;
     const int lane = threadIdx.x & 63;
-    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
+    const TaskGeo g = task_geo(A);
+    const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
+    const int r = lane / g.lr, ul = lane - r * g.lr;
 
-#if defined(LLMI_EXP_TRACE)
-    const int wave = threadIdx.x >> 6;
-    const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long tr1 = 0, tr2 = 0, tr_x = 0, tr_q = 0;
-    int tr_items = 0;
-#endif
-    int p = p0;
-    PairRef r;
-    PairRows<T> rows;
-    bool pipe = false;
+    int task = t0;
     ProRegs<NORM, NP> R;
     mv_prologue_issue<NORM, NP>(A, R);  // activation loads first ...
-    // Single-round launches (every wave owns at most one pair: QKV, attn_output) issue
+    // Single-round launches (every wave owns at most one task: QKV, attn_output) issue
     // their weights only once the activation has arrived: the activation loads then do
     // not queue behind the chip-wide weight burst, and the weight latency overlaps the
-    // quantization instead (4096x4096: 5.2 -> 4.7 us).  Multi-round launches keep the
-    // weights in flight from the start.
-    if (pend - pbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    r = pair_ref<EPI>(A, p < pend ? p : pend - 1);
-    pipe = p < pend && r.type == T;
-    rows = pair_rows<T>(r, A.cols);
-    // ... then the first weights, in flight during the prologue.  Issued on every path
-    // (a wave without a pipelined pair reads a dummy chunk inside x: every plane offset
-    // of one chunk stays below cols*4 bytes) so the prologue's first wait counts only
-    // the activation loads.
-    {
-        const uint8_t* xb = (const uint8_t*)A.x;
-        const RowPtr dummy{xb, xb, xb, xb};
-        if (!pipe) rows.a = rows.b = dummy;
-    }
-    PairRaw<T> cur = load_item<T>(rows, lane, nch);
-#if defined(LLMI_EXP_TRACE)
-    asm volatile("" ::"v"(R.x[0][0]), "v"(R.x[0][15]));
-    tr_x = __builtin_amdgcn_s_memrealtime();
-#endif
+    // quantization instead.  Multi-round launches keep the weights in flight from the start.
+    if (tend - tbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool pipe = task < tend && task_is<EPI, T>(A, g, task);
+    Sub b = sub_of<EPI>(A, g, task < tend ? task : tend - 1, 0);
+    Seg sg = pick(A, b.si);
+    LaneUnit lu = lane_unit(g, b, sg, r, ul);
+    // ... then the first units, in flight during the prologue (issued on every path: an
+    // idle wave re-reads row 0, so the prologue's first wait counts only the activation)
+    UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
     mv_prologue_finish<ACT, NORM, NP>(A, L, R);
-#if defined(LLMI_EXP_TRACE)
-    tr_q = __builtin_amdgcn_s_memrealtime();
-#endif
     __syncthreads();
-#if defined(LLMI_EXP_TRACE)
-    tr1 = __builtin_amdgcn_s_memrealtime();
-#endif
 
     if (pipe) {
-        int j = 0;
-        float acc = 0.f;  // fold lane: its chain of the current pair
+        int s = 0;
+        float acc = 0.f, vg = 0.f;
         for (;;) {
-            // next work item: (p, j+1) or (p+G, 0); uniform control flow
-            int pn = p, jn = j + 1;
-            PairRef rn = r;
-            PairRows<T> rowsn = rows;
-            if (jn == NJ) {
-                jn = 0;
-                pn = p + G;
-                if (pn < pend) {
-                    rn = pair_ref<EPI>(A, pn);
-                    rowsn = pair_rows<T>(rn, A.cols);
-                }
+            // next sub-item: (task, s+1) or (task+G, 0); uniform control flow
+            int tn = task, sn = s + 1;
+            Sub bn = b;
+            Seg sgn = sg;
+            bool has_next = true;
+            if (sn == S) {
+                sn = 0;
+                tn = task + G;
+                has_next = tn < tend && task_is<EPI, T>(A, g, tn);
             }
-            const bool has_next = pn < pend && rn.type == T;
-            // always issue the prefetch (a valid re-load of the current item if none)
-            const PairRaw<T> nxt = load_item<T>(has_next ? rowsn : rows, lane + 64 * (has_next ? jn : j), nch);
-            const int ch = lane + 64 * j;
-            const int chc = ch < nch ? ch : nch - 1;
-            const Act act = load_act<ACT>(L, chc, nch);
-            item_terms<T>(cur.a, act, chc, ch < nch, F);
-            item_terms<T>(cur.b, act, chc, ch < nch, F + kFoldRow);
-            wave_lds_sync();
-            fold_item<ACT>(F, item_blocks<ACT>(A.cols, j), acc);
-            if (j == NJ - 1) {
-                epilogue<EPI>(A, r, p, fold_final<ACT>(F, acc), pos, best);
-                acc = 0.f;
-#if defined(LLMI_EXP_TRACE)
-                if (tr_items++ == 0) tr2 = __builtin_amdgcn_s_memrealtime();
-#endif
+            if (has_next) {
+                bn = sub_of<EPI>(A, g, tn, sn);
+                sgn = pick(A, bn.si);
             }
-            wave_lds_sync();  // the fold lanes' reads before the next item's stores
+            const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
+            // always issue the prefetch (a valid re-load of the current unit if none)
+            const UnitW<T> nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
+            float tm[9];
+            unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
+            sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
             if (!has_next) {
-                p = pn;
+                task = tn;
                 break;
             }
             cur = nxt;
-            p = pn;
-            j = jn;
-            r = rn;
-            rows = rowsn;
+            task = tn;
+            s = sn;
+            b = bn;
+            sg = sgn;
+            lu = lun;
         }
     }
-    // remaining pairs of other types (or all pairs if the first was not of type T)
-    for (; p < pend; p += G) {
-        r = pair_ref<EPI>(A, p);
-        epilogue<EPI>(A, r, p, pair_any<ACT>(r, A.cols, L, F), pos, best);
-    }
-#if defined(LLMI_EXP_TRACE)
-    if (A.trace && lane == 0) {
-        unsigned hw = 0;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        unsigned xcc = 0;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        unsigned long long* t = A.trace + ((size_t)blockIdx.x * kMVWaves + wave) * 8;
-        t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = __builtin_amdgcn_s_memrealtime();
-        t[4] = hw; t[5] = ((unsigned long long)xcc << 32) | (unsigned)tr_items;
-        t[6] = tr_x; t[7] = tr_q;
-    }
-#endif
+    // remaining tasks of other types (or all tasks if the first was not of type T)
+    for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
     return best;
 }
 
 // A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
-// split by workgroup: workgroups [0, split_wgs) run the pairs of type T, the rest the
-// pairs of type T2, each group pipelined in its own type (no divergence in a workgroup).
+// split by workgroup: workgroups [0, split_wgs) run the tasks of type T, the rest the
+// tasks of type T2, each group pipelined in its own type (no divergence in a workgroup).
 template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T>
 __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -198,19 +150,20 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     float* F = (float*)(smem + fold_off(ACT, A.cols, kMVWaves)) + wave * kFoldFloats;
     unsigned long long best;
     if constexpr (T2 == T) {
-        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.npairs);
+        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.ntasks);
     } else {
         if ((int)blockIdx.x < A.split_wgs)
             best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
-                                                  A.split_pairs);
+                                                  A.split_tasks);
         else
-            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, F, A.split_pairs + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
-                                                   (gridDim.x - A.split_wgs) * kMVWaves, A.split_pairs, A.npairs);
+            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, F, A.split_tasks + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
+                                                   (gridDim.x - A.split_wgs) * kMVWaves, A.split_tasks, A.ntasks);
     }
     if constexpr (EPI == EPI_LOGITS) {
-        // workgroup max of the waves' keys, then one atomic into this workgroup's slot
+        // workgroup max of the lanes' keys, then one atomic into this workgroup's slot
         const int cur_pos = A.st->pos;
         unsigned long long* red = (unsigned long long*)L.red;
+        best = wave_max_u64(best);
         __syncthreads();
         if (lane == 0) red[wave] = best;
         __syncthreads();
@@ -218,111 +171,6 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
             unsigned long long b = red[0];
 #pragma unroll
             for (int w = 1; w < kMVWaves; ++w) b = red[w] > b ? red[w] : b;
-            if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
-            if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
-        }
-    }
-}
-
-// K-split matvec for rows longer than one 64-chunk item (NJ = ceil(cols/4096) >= 2:
-// ffn_down, 70B-wide inputs).  A workgroup's 16 waves form 16/KS pair slots of KS waves;
-// the waves of a slot split the pair's items (wave sub takes items sub, sub+KS, ...),
-// so every item of the first pair is in flight during the prologue, instead of one
-// item per wave with the rest fetched serially after it.  KS >= 2: each wave writes its
-// items' block terms to the slot's part buffer P[slot][item]; after the round's barrier
-// the slot's wave 0 folds the items in order (the generic order runs over the row's
-// blocks in sequence) and runs the epilogue.  KS = 1: one wave per pair folds each item
-// as it goes, as k_matvec does (no part buffer, no barrier).
-constexpr int kKSThreads = 1024, kKSWaves = kKSThreads / 64;  // one workgroup per CU
-__host__ __device__ inline size_t ks_part_off(int act, int cols) {
-    return fold_off(act, cols, kKSWaves) + (size_t)kKSWaves * kFoldFloats * 4;
-}
-template <int KS>
-__host__ __device__ inline size_t ks_part_bytes(int cols) {
-    const int nj = ((cols >> 6) + 63) >> 6;
-    return KS == 1 ? 0 : (size_t)(kKSWaves / KS) * nj * 2 * kFoldRow * sizeof(float);
-}
-
-template <int ACT, bool NORM, int EPI, int T, int NP, int KS>
-__global__ __launch_bounds__(kKSThreads) void k_matvec_ks(MVArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Lds L = carve(smem, ACT, A.cols);
-    constexpr int PPW = kKSWaves / KS;
-    const int wave = uniform((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    const int slot = wave / KS, sub = wave % KS;
-    const int nch = A.cols >> 6, NJ = (nch + 63) >> 6;
-    float* F = (float*)(smem + fold_off(ACT, A.cols, kKSWaves)) + wave * kFoldFloats;
-    float* part = (float*)(smem + ks_part_off(ACT, A.cols)) + (size_t)slot * NJ * 2 * kFoldRow;  // [NJ][2][kFoldRow]
-    const int stride = gridDim.x * PPW;
-    const int rounds = (A.npairs + stride - 1) / stride;
-    int pos = 0;
-    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
-    unsigned long long best = 0;
-    const uint8_t* xb = (const uint8_t*)A.x;
-    const RowPtr dummy{xb, xb, xb, xb};
-
-    ProRegs<NORM, NP> R;
-    mv_prologue_issue<NORM, NP, kKSThreads>(A, R);  // activation loads first, then this wave's first item
-    if (A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int pr = blockIdx.x * PPW + slot;   // this slot's pair in the current round
-    PairRows<T> rows = pair_rows<T>(pair_ref<EPI>(A, pr < A.npairs ? pr : A.npairs - 1), A.cols);
-    if (!(pr < A.npairs && sub < NJ)) rows.a = rows.b = dummy;
-    PairRaw<T> cur = load_item<T>(rows, lane + 64 * (sub < NJ ? sub : 0), nch);
-    mv_prologue_finish<ACT, NORM, NP, kKSThreads>(A, L, R);
-    __syncthreads();
-
-    for (int rd = 0; rd < rounds; ++rd, pr += stride) {
-        const bool have = pr < A.npairs;
-        float acc = 0.f;
-        for (int j = sub; j < NJ; j += KS) {
-            // the wave's next item: (pr, j+KS) or (pr+stride, sub); loads always issued
-            int jn = j + KS, prn = pr;
-            PairRows<T> rowsn = rows;
-            if (jn >= NJ) {
-                jn = sub;
-                prn = pr + stride;
-                rowsn = pair_rows<T>(pair_ref<EPI>(A, prn < A.npairs ? prn : A.npairs - 1), A.cols);
-                if (prn >= A.npairs) rowsn.a = rowsn.b = dummy;
-            }
-            const PairRaw<T> nxt = load_item<T>(rowsn, lane + 64 * jn, nch);
-            if (have) {
-                const int ch = lane + 64 * j;
-                const int chc = ch < nch ? ch : nch - 1;
-                const Act act = load_act<ACT>(L, chc, nch);
-                float* P = KS == 1 ? F : part + (size_t)j * 2 * kFoldRow;
-                item_terms<T>(cur.a, act, chc, ch < nch, P);
-                item_terms<T>(cur.b, act, chc, ch < nch, P + kFoldRow);
-                if constexpr (KS == 1) {
-                    wave_lds_sync();
-                    fold_item<ACT>(F, item_blocks<ACT>(A.cols, j), acc);
-                    wave_lds_sync();
-                }
-            }
-            cur = nxt;
-            rows = rowsn;
-        }
-        if constexpr (KS == 1) {
-            if (have) epilogue<EPI>(A, pair_ref<EPI>(A, pr), pr, fold_final<ACT>(F, acc), pos, best);
-        } else {
-            __syncthreads();
-            if (sub == 0 && have) {
-                for (int j = 0; j < NJ; ++j) fold_item<ACT>(part + (size_t)j * 2 * kFoldRow, item_blocks<ACT>(A.cols, j), acc);
-                epilogue<EPI>(A, pair_ref<EPI>(A, pr), pr, fold_final<ACT>(F, acc), pos, best);
-            }
-            __syncthreads();
-        }
-    }
-    if constexpr (EPI == EPI_LOGITS) {
-        const int cur_pos = A.st->pos;
-        unsigned long long* red = (unsigned long long*)L.red;
-        __syncthreads();
-        if (lane == 0) red[wave] = best;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long b = red[0];
-#pragma unroll
-            for (int w = 1; w < kKSWaves; ++w) b = red[w] > b ? red[w] : b;
             if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
             if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
         }
@@ -338,23 +186,25 @@ __global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* ou
     else mv_prologue<ACT, false>(A, L);
     __syncthreads();
     const int cols = A.cols;
-    const int nch = cols >> 6;
     for (int e = threadIdx.x; e < cols; e += blockDim.x) {
-        const int ch = e >> 6, t = e & 63;
-        if (ACT == 0) {  // residue order: element t = 32 h + l + 8 i at part l / 4, byte 4 (l % 4) + i
-            const int l = t & 7, i = (t & 31) >> 3;
-            const int8_t qv = (int8_t)((t < 32 ? L.lo : L.hi)[16 * ((l >> 2) * nch + ch) + 4 * (l & 3) + i]);
-            out[(size_t)(e >> 8) * 292 + 4 + (e & 255)] = (uint8_t)qv;
+        const uint8_t* rec = L.act + (size_t)(e >> 8) * kRec;
+        const int t = e & 255;
+        if (ACT == 0) {  // residue order: element 64c + 32h + l + 8i at part 2c + l/4, half h, byte 4 (l % 4) + i
+            const int c = t >> 6, h = (t >> 5) & 1, l = t & 7, i = (t & 31) >> 3;
+            out[(size_t)(e >> 8) * 292 + 4 + t] = rec[32 * (2 * c + (l >> 2)) + 16 * h + 4 * (l & 3) + i];
         } else {
-            out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = L.lo[16 * ((t >> 4) * nch + ch) + (t & 15)];
+            out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = rec[t];
         }
     }
     if (ACT == 0) {
-        for (int b = threadIdx.x; b < cols / 256; b += blockDim.x) *(float*)(out + (size_t)b * 292) = L.d[b];
+        for (int b = threadIdx.x; b < cols / 256; b += blockDim.x)
+            *(float*)(out + (size_t)b * 292) = *(const float*)(L.act + (size_t)b * kRec + kRecD);
         for (int sb = threadIdx.x; sb < cols / 16; sb += blockDim.x)
-            *(int16_t*)(out + (size_t)(sb >> 4) * 292 + 260 + 2 * (sb & 15)) = L.bs[sb];
+            *(int16_t*)(out + (size_t)(sb >> 4) * 292 + 260 + 2 * (sb & 15)) =
+                *(const int16_t*)(L.act + (size_t)(sb >> 4) * kRec + kRecBs + 2 * (sb & 15));
     } else {
-        for (int b = threadIdx.x; b < cols / 32; b += blockDim.x) *(uint16_t*)(out + (size_t)b * 34) = f2h(L.d[b]);
+        for (int b = threadIdx.x; b < cols / 32; b += blockDim.x)
+            *(uint16_t*)(out + (size_t)b * 34) = f2h(*(const float*)(L.act + (size_t)(b >> 3) * kRec + kRecBs + 4 * (b & 7)));
     }
 }
 
@@ -1109,8 +959,8 @@ __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
 }
 
 // ----------------------------------------------------------------------------------
-// Load-time repack of GGUF blocks into the chunk-planar layout (common.h).
-// One thread per (block, chunk c in 0..3); nbr = blocks per row.
+// Load-time repack of GGUF blocks into the unit-major layout (common.h).
+// One thread per (block, chunk c in 0..3); nbr = blocks (units) per row.
 // ----------------------------------------------------------------------------------
 __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H, uint8_t* S, uint8_t* Dp, int64_t nblk,
                             int nbr) {
@@ -1118,29 +968,31 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
     const int64_t b = gid >> 2;
     const int c = (int)(gid & 3);
     if (b >= nblk) return;
-    const int64_t row = b / nbr, bi = b % nbr, nch = (int64_t)nbr * 4, ch = bi * 4 + c;
-    uint8_t* arow = A + row * nch * 32;
-    // residue order: byte 4m + i of part k holds chunk elements t = l + 8i (low nibble)
-    // and 32 + t (high nibble), l = 4k + m
+    const int64_t row = b / nbr, u = b % nbr, U = nbr;
+    uint8_t* arow = A + row * U * 128;
+    // residue order: byte 4m + i of part 2c + k holds chunk elements t = l + 8i (low
+    // nibble) and 32 + t (high nibble), l = 4k + m
     if (type == T_Q4_K || type == T_Q5_K) {
         const int bb = type == T_Q4_K ? 144 : 176;
         const uint8_t* x = raw + b * bb;
         const uint8_t* qs = x + (type == T_Q4_K ? 16 : 48);
         for (int k = 0; k < 2; ++k)
             for (int m = 0; m < 4; ++m)
-                for (int i = 0; i < 4; ++i) arow[(k * nch + ch) * 16 + 4 * m + i] = qs[32 * c + 4 * k + m + 8 * i];
+                for (int i = 0; i < 4; ++i) arow[((2 * c + k) * U + u) * 16 + 4 * m + i] = qs[32 * c + 4 * k + m + 8 * i];
         if (c == 0)
             for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[i];
-        if (type == T_Q5_K) {  // bit 4l + i of the lo word: qh[l + 8i] bit 2c; hi word: bit 2c+1
+        if (type == T_Q5_K) {  // byte i, bit l of the lo word: qh[l + 8i] bit 2c; hi word: bit 2c+1
             const uint8_t* qh = x + 16;
-            uint32_t lo = 0, hi = 0;
-            for (int l = 0; l < 8; ++l)
-                for (int i = 0; i < 4; ++i) {
-                    lo |= (uint32_t)((qh[l + 8 * i] >> (2 * c)) & 1) << (4 * l + i);
-                    hi |= (uint32_t)((qh[l + 8 * i] >> (2 * c + 1)) & 1) << (4 * l + i);
+            uint8_t* h = H + row * U * 32 + ((c >> 1) * U + u) * 16 + 8 * (c & 1);
+            for (int i = 0; i < 4; ++i) {
+                uint8_t lo = 0, hi = 0;
+                for (int l = 0; l < 8; ++l) {
+                    lo |= (uint8_t)(((qh[l + 8 * i] >> (2 * c)) & 1) << l);
+                    hi |= (uint8_t)(((qh[l + 8 * i] >> (2 * c + 1)) & 1) << l);
                 }
-            uint8_t* h = H + (row * nch + ch) * 8;
-            for (int k = 0; k < 4; ++k) { h[k] = (uint8_t)(lo >> (8 * k)); h[4 + k] = (uint8_t)(hi >> (8 * k)); }
+                h[i] = lo;
+                h[4 + i] = hi;
+            }
         }
     } else {  // Q6_K
         const uint8_t* x = raw + b * 210;
@@ -1157,11 +1009,12 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
             for (int m = 0; m < 4; ++m)
                 for (int i = 0; i < 4; ++i) {
                     const int t = 4 * k + m + 8 * i;
-                    arow[(k * nch + ch) * 16 + 4 * m + i] = (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
+                    arow[((2 * c + k) * U + u) * 16 + 4 * m + i] =
+                        (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
                 }
-        // H dword g = 2*hi + k: byte i bits [2m, 2m+1] = (high 2 bits of chunk element
-        // 32*hi + 4k + m + 8i) XOR 2, which v_perm turns into the high part of q - 32
-        uint8_t* h = H + (row * nch + ch) * 16;
+        // H part c, dword g = 2*hi + k: byte i bits [2m, 2m+1] = (high 2 bits of chunk
+        // element 32*hi + 4k + m + 8i) XOR 2, which v_perm turns into the high part of q - 32
+        uint8_t* h = H + row * U * 64 + (c * U + u) * 16;
         for (int g = 0; g < 4; ++g)
             for (int i = 0; i < 4; ++i) {
                 uint8_t v = 0;
@@ -1174,19 +1027,17 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
     }
 }
 
-// Q8_0: one thread per 64-weight chunk (two blocks)
-__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nchunk, int nch_row) {
+// Q8_0: one thread per 32-block; unit u = 8 blocks, block b of the unit in parts 2b, 2b+1
+__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nblk, int nb_row) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= nchunk) return;
-    const int64_t row = g / nch_row, ch = g % nch_row;
-    uint8_t* arow = A + row * nch_row * 64;
-    for (int half = 0; half < 2; ++half) {
-        const uint8_t* x = raw + (g * 2 + half) * 34;
-        for (int k = 0; k < 2; ++k)
-            for (int i = 0; i < 16; ++i) arow[((2 * half + k) * nch_row + ch) * 16 + i] = x[2 + 16 * k + i];
-        Dp[(g * 2 + half) * 2] = x[0];
-        Dp[(g * 2 + half) * 2 + 1] = x[1];
-    }
+    if (g >= nblk) return;
+    const int64_t row = g / nb_row, bi = g % nb_row, U = nb_row / 8, u = bi >> 3, b = bi & 7;
+    const uint8_t* x = raw + g * 34;
+    uint8_t* arow = A + row * U * 256;
+    for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < 16; ++i) arow[((2 * b + h) * U + u) * 16 + i] = x[2 + 16 * h + i];
+    Dp[(row * U + u) * 16 + 2 * b] = x[0];
+    Dp[(row * U + u) * 16 + 2 * b + 1] = x[1];
 }
 
 // Streaming-read reference (achievable HBM rate for a perfectly coalesced 16-B/lane
@@ -1244,11 +1095,10 @@ static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t 
     return hipGetLastError();
 }
 
-// Two type groups (pairs [0, split) of type T, [split, npairs) of type T2): the
-// resident grid is dealt to the groups so that the largest per-wave byte count (pairs per
-// wave rounded up x bytes per pair) is smallest, >= 1 workgroup each.  (Dealing by pair
-// count left the Q6_K attn_v group of an 8B QKV at 2 pairs = 13.4 KB per wave while the
-// Q4_K waves had 9.2 KB.)  Which wave reduces a pair never changes a result.
+// Two type groups (tasks [0, split) of type T, [split, ntasks) of type T2): the
+// resident grid is dealt to the groups so that the largest per-wave byte count (tasks per
+// wave rounded up x bytes per task) is smallest, >= 1 workgroup each.  Which wave reduces
+// a task never changes a result.
 static int split_groups(int wgs, int p1, int p2, double b1, double b2) {
     int best = 1;
     double best_cost = 1e300;
@@ -1260,18 +1110,18 @@ static int split_groups(int wgs, int p1, int p2, double b1, double b2) {
     return best;
 }
 template <int ACT, bool NORM, int T, int T2, int EPI, int NP>
-static hipError_t mv_launch2(const MVArgs& a0, int split_pairs, dim3 grid, size_t lds, hipStream_t s) {
+static hipError_t mv_launch2(const MVArgs& a0, int split_tasks, dim3 grid, size_t lds, hipStream_t s) {
     auto k = k_matvec<ACT, NORM, EPI, T, NP, T2>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
-    a.split_pairs = split_pairs;
+    a.split_tasks = split_tasks;
     int w1;
-    if (g_split_by_pairs) {  // A/B: the round-1 deal by pair count
-        w1 = (int)(((long long)g.x * split_pairs + a.npairs / 2) / a.npairs);
+    if (g_split_by_pairs) {  // A/B: deal by task count
+        w1 = (int)(((long long)g.x * split_tasks + a.ntasks / 2) / a.ntasks);
         w1 = w1 < 1 ? 1 : w1 > (int)g.x - 1 ? (int)g.x - 1 : w1;
     } else {
-        w1 = split_groups((int)g.x, split_pairs, a.npairs - split_pairs, (double)tensor_bytes(T, 2, a.cols),
-                          (double)tensor_bytes(T2, 2, a.cols));
+        w1 = split_groups((int)g.x, split_tasks, a.ntasks - split_tasks, (double)tensor_bytes(T, a.rpt, a.cols),
+                          (double)tensor_bytes(T2, a.rpt, a.cols));
     }
     a.split_wgs = w1;
     launch_k(k, g, dim3(kMVThreads), lds, s, true, true, a);
@@ -1284,51 +1134,8 @@ static int prologue_np(int cols) {
     return per <= 1 ? 1 : per <= 2 ? 2 : 4;
 }
 
-template <int ACT, bool NORM, int T, int EPI, int NP, int KS>
-static hipError_t mv_launch_ks(const MVArgs& a, int max_blocks, hipStream_t s) {
-    auto k = k_matvec_ks<ACT, NORM, EPI, T, NP, KS>;
-    const size_t lds = ks_part_off(ACT, a.cols) + ks_part_bytes<KS>(a.cols);
-    constexpr int PPW = kKSWaves / KS;
-    int blocks = (a.npairs + PPW - 1) / PPW;
-    if (blocks > max_blocks) blocks = max_blocks;
-    launch_k(k, resident_grid(k, dim3(blocks), lds, kKSThreads), dim3(kKSThreads), lds, s, true, true, a);
-    return hipGetLastError();
-}
-
-static thread_local int g_mv_max_blocks = 1024;  // set by launch_matvec
-
-// K-split is taken for rows of >= 2 items when every segment has the pipelined type
-static bool use_ks(const MVArgs& a, int T) {
-    if (((a.cols >> 6) + 63) >> 6 < 2) return false;
-    for (int i = 0; i < a.nseg; ++i)
-        if (a.seg[i].type != T) return false;
-    return true;
-}
-
 template <int ACT, bool NORM, int T, int EPI>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if (use_ks(a, T)) {  // one 1024-thread workgroup per CU: NP from 1024 threads
-        const int nj = ((a.cols >> 6) + 63) >> 6;
-        const int per = (a.cols / 16 + kKSThreads - 1) / kKSThreads;
-        const int mb = g_mv_max_blocks;
-        // K-split width (waves per pair slot), measured (profiles/r01/ks_sweep.md):
-        //   rows of >= 6 items (70B ffn_down, 28672 columns): KS = 1 when its part buffer
-        //     fits LDS — one pair per wave, no per-round barrier wait (30.7 -> 29.0 us);
-        //   otherwise KS = 2 (8B ffn_down Q4_K 10.3 -> 9.8 us against KS = 4).
-        // LLMI_KS = 2 / 4 forces that width (A/B hook; 4 only for rows of >= 4 items).
-        static const int ks_env = [] {
-            const char* e = getenv("LLMI_KS");
-            return e ? atoi(e) : 0;
-        }();
-        if (ks_env == 4 && nj >= 4) {
-            if (per <= 1) return mv_launch_ks<ACT, NORM, T, EPI, 1, 4>(a, mb, s);
-            return mv_launch_ks<ACT, NORM, T, EPI, 2, 4>(a, mb, s);
-        }
-        if (ks_env == 0 && nj >= 6 && per > 1 && ks_part_off(ACT, a.cols) + ks_part_bytes<1>(a.cols) <= 160 * 1024)
-            return mv_launch_ks<ACT, NORM, T, EPI, 2, 1>(a, mb, s);
-        if (per <= 1) return mv_launch_ks<ACT, NORM, T, EPI, 1, 2>(a, mb, s);
-        return mv_launch_ks<ACT, NORM, T, EPI, 2, 2>(a, mb, s);
-    }
     switch (prologue_np(a.cols)) {
         case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
         case 2: return mv_launch<ACT, NORM, T, EPI, 2>(a, grid, lds, s);
@@ -1356,7 +1163,7 @@ static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t ld
     return hipErrorInvalidValue;
 }
 
-// QKV whose segments form two contiguous type groups split at an even row: both groups
+// QKV whose segments form two contiguous type groups split at a task boundary: both groups
 // pipelined (k_matvec's T2 path).  Returns hipErrorNotSupported when not applicable.
 template <bool NORM>
 static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
@@ -1368,8 +1175,8 @@ static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipSt
         t2 = a.seg[i].type;
         split_row = a.seg[i].row0 - a.seg[0].row0;
     }
-    if (t2 < 0 || (split_row & 1) || prologue_np(a.cols) != 1) return hipErrorNotSupported;
-    const int sp = split_row / 2;
+    if (t2 < 0 || split_row % a.rpt || prologue_np(a.cols) != 1) return hipErrorNotSupported;
+    const int sp = split_row / a.rpt;
 #define LLMI_QKV2(A_, B_)                                                                            \
     if (t1 == A_ && t2 == B_) return mv_launch2<0, NORM, A_, B_, EPI_QKV, 1>(a, sp, grid, lds, s);
     if constexpr (NORM) {
@@ -1403,14 +1210,51 @@ static hipError_t mv_dispatch_type(const MVArgs& a, int epi, dim3 grid, size_t l
     }
 }
 
-hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s) {
-    g_mv_max_blocks = max_blocks;
-    if (a.nseg < 1 || a.cols <= 0 || a.cols % 256 || a.npairs <= 0) return hipErrorInvalidValue;
+// Row-task geometry (mv_device.h "Row tasks"): Lr lanes per row = U rounded up to a
+// multiple of 4, at most 64 (QKV: 32, so that a task holds RoPE pairs); R = 64 / Lr
+// rounded down to a power of two, halved until every segment starts on a task boundary.
+bool mv_geometry(MVArgs& a, int epi) {
+    if (a.nseg < 1 || a.cols < 256 || a.cols % 256) return false;
+    const int U = a.cols >> 8, lmax = epi == EPI_QKV ? 32 : 64;
+    static const int lr_cap = [] {  // A/B knob: cap on lanes per row (more rows per task)
+        const char* e = getenv("LLMI_MV_LR");
+        return e ? atoi(e) : 64;
+    }();
+    int lr = (std::min(std::min(U, lmax), lr_cap) + 3) & ~3;
+    lr = std::min(std::max(lr, 4), lmax);
+    int R = 1;
+    while (2 * R * lr <= 64) R *= 2;
+    auto aligned = [&](int r) {
+        for (int i = 1; i < a.nseg; ++i)
+            if ((a.seg[i].row0 - a.seg[0].row0) % r) return false;
+        return true;
+    };
+    if (epi != EPI_SWIGLU)
+        while (R > 1 && !aligned(R)) R >>= 1;
+    if (epi == EPI_QKV && R < 2) return false;
+    int rows;
+    if (epi == EPI_SWIGLU) {
+        if (a.nseg != 2 || a.seg[0].rows != a.seg[1].rows) return false;
+        rows = a.seg[0].rows;
+    } else {
+        rows = a.seg[a.nseg - 1].row0 + a.seg[a.nseg - 1].rows - a.seg[0].row0;
+    }
+    a.lr = lr;
+    a.rpt = R;
+    a.ntasks = (rows + R - 1) / R;
+    return a.ntasks > 0;
+}
+
+hipError_t launch_matvec(const MVArgs& a0, int epi, int max_blocks, hipStream_t s) {
+    if (a0.nseg < 1 || a0.cols <= 0 || a0.cols % 256) return hipErrorInvalidValue;
+    MVArgs a = a0;
+    if (!mv_geometry(a, epi)) return hipErrorInvalidValue;
     const int act = act_kind(a.seg[0].type);
     for (int i = 1; i < a.nseg; ++i)
         if (act_kind(a.seg[i].type) != act) return hipErrorInvalidValue;
     const size_t lds = mv_lds_bytes(act, a.cols);
-    int blocks = (a.npairs + kMVWaves - 1) / kMVWaves;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    int blocks = (a.ntasks + kMVWaves - 1) / kMVWaves;
     if (blocks > max_blocks) blocks = max_blocks;
 #if defined(LLMI_EXPERIMENTS)
     static const int exp_blocks = [] {  // experiment builds: fixed grid for launch sweeps
@@ -1418,12 +1262,6 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
         return e ? atoi(e) : 0;
     }();
     if (exp_blocks > 0 && exp_blocks < blocks) blocks = exp_blocks;
-#endif
-#if defined(LLMI_EXP_BALANCE)
-    {  // experiment: equal pairs per wave (fewer workgroups when that divides better)
-        const int waves = blocks * kMVWaves, per = (a.npairs + waves - 1) / waves;
-        blocks = ((a.npairs + per - 1) / per + kMVWaves - 1) / kMVWaves;
-    }
 #endif
     const dim3 grid(blocks);
     return a.nw ? mv_dispatch_type<true>(a, epi, grid, lds, s) : mv_dispatch_type<false>(a, epi, grid, lds, s);
@@ -1650,9 +1488,8 @@ hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint
         hipLaunchKernelGGL(k_repack_kq, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, type, (const uint8_t*)raw, a,
                            h, sp, d, nblk, (int)(cols / 256));
     } else if (type == T_Q8_0) {
-        const int64_t nchunk = nblk / 2;
-        hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nchunk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d,
-                           nchunk, (int)(cols / 64));
+        hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d,
+                           nblk, (int)(cols / 32));
     } else {
         return hipErrorInvalidValue;
     }

@@ -16,6 +16,7 @@ namespace llmi {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef short short2_t __attribute__((ext_vector_type(2)));
 
 // Weight loads are nontemporal (nt): every weight byte is read once per token by one
 // CU, so keeping it in L2/MALL only evicts the activations and KV.  Measured with the
@@ -121,39 +122,30 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ----------------------------------------------------------------------------------
-// LDS image of the quantized activation, in the weights' chunk-part order (common.h):
-//   K-quants (block_q8_K): LO[k][ch], HI[k][ch]: 16 int8 each = activation of the
-//     weights in the low / high nibbles of quant part k of chunk ch, in residue order:
-//     byte 4m + i of part k = chunk element l + 8i (LO) / 32 + l + 8i (HI), l = 4k + m;
-//     BS[4ch+i] = bsums in natural order; D[b] per 256-block.
-//   Q8_0 (block_q8_0): LO[k][ch] (k < 4) = elements 64ch+16k..+15; D[b] per 32-block
-//     (f16-rounded, as stored by quantize_row_q8_0).
-// Lane L reads LO[k][L + 64j]: 16 consecutive 16-B slots per ds_read_b128 lane group,
-// conflict-free.
+// LDS image of the quantized activation: one kRec-byte RECORD per 256-element unit
+// (the weights' unit, common.h), in the weights' part order:
+//   K-quants (block_q8_K):  [32 p, 32 p + 16)       LO: activation of the low nibbles
+//                           [32 p + 16, 32 p + 32)  HI: ... of the high nibbles of part p
+//                           (residue order: byte 4m + i of LO = chunk element l + 8i,
+//                           of HI = 32 + l + 8i, chunk c = p / 2, l = 4 (p % 2) + m)
+//                           [256, 288) bsums int16[16], [288, 292) d
+//   Q8_0 (block_q8_0):      [16 p, 16 p + 16) elements 16 p .. +15 (natural order),
+//                           [256, 288) d of the eight 32-blocks (f32 of the f16 value)
+// A lane reads the record of its own unit: the stride of 19 x 16 B (odd) puts the 16
+// lanes of a ds_read_b128 bank group on 16 distinct 16-B bank quads (conflict-free).
 // ----------------------------------------------------------------------------------
+constexpr int kRec = 304, kRecBs = 256, kRecD = 288;
 struct Lds {
-    uint8_t* lo;
-    uint8_t* hi;
-    int16_t* bs;
-    float* d;
+    uint8_t* act;
     double* red;
 };
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
-// byte offsets of the regions; act 0 = q8_K (K-quant weights), 1 = q8_0
-__host__ __device__ inline size_t lds_hi_off(int act, int cols) { return act ? (size_t)cols : (size_t)cols / 2; }
-__host__ __device__ inline size_t lds_bs_off(int act, int cols) { return (size_t)cols; }
-__host__ __device__ inline size_t lds_d_off(int act, int cols) { return a16((size_t)cols + (act ? 0 : (size_t)cols / 8)); }
-__host__ __device__ inline size_t lds_red_off(int act, int cols) {
-    return a16(lds_d_off(act, cols) + (size_t)(act ? cols / 32 : cols / 256) * 4);
-}
+__host__ __device__ inline size_t lds_red_off(int act, int cols) { return (size_t)(cols >> 8) * kRec; }
 // (mv_lds_bytes: defined in kernels.hip)
 
 __device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
     Lds l;
-    l.lo = smem;
-    l.hi = smem + lds_hi_off(act, cols);
-    l.bs = (int16_t*)(smem + lds_bs_off(act, cols));
-    l.d = (float*)(smem + lds_d_off(act, cols));
+    l.act = smem;
     l.red = (double*)(smem + lds_red_off(act, cols));
     return l;
 }
@@ -189,7 +181,6 @@ __device__ double block_sum_d(double v, double* red) {
 // Quantize one 16-element sub-block (values already normed) into the LDS image.
 template <int ACT>
 __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const float (&v)[16]) {
-    const int tid = threadIdx.x;
     int q[16];
     if constexpr (ACT == 0) {
         // max |y| of the Q8_K block (order-free), then the SIGNED value ggml keeps: the
@@ -226,19 +217,18 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
             }
             dval = 1.0f / iscale;
         }
-        // sub-block sb = chunk ch = sb/4, quarter qq = sb%4: half h = qq/2 (LO / HI image),
-        // elements tt = 16*(qq%2) + j of the half.  Residue order (common.h): element tt of
-        // a half sits at part k = l/4, byte 4*(l%4) + i with l = tt%8, i = tt/8, so q[j]
-        // and q[j+8] (same l, i = 2*(qq%2) + 0/1) are one 16-bit store.
-        const int nch = cols >> 6, ch = sb >> 2, qq = sb & 3;
-        const int hoff = qq < 2 ? 0 : (int)(L.hi - L.lo);  // (no pointer select: it spills to scratch)
-        uint8_t* base = L.lo + hoff + 16 * ch + 2 * (qq & 1);
+        // sub-block sb = unit u, 16-element piece s = 4c + 2h + half of chunk c, half
+        // h (LO / HI): elements tt = 16 half + j of the half sit at part 2c + l/4, byte
+        // 4 (l%4) + i with l = tt%8 = j%8, i = tt/8 = 2 half + j/8 (residue order), so
+        // q[j] and q[j+8] are one 16-bit store
+        const int s = sb & 15;
+        uint8_t* rec = L.act + (size_t)(sb >> 4) * kRec;
+        uint8_t* base = rec + 64 * (s >> 2) + 16 * ((s >> 1) & 1) + 2 * (s & 1);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-            *(uint16_t*)(base + 16 * nch * (j >> 2) + 4 * (j & 3)) =
-                (uint16_t)((q[j] & 0xff) | ((q[j + 8] & 0xff) << 8));
-        L.bs[sb] = (int16_t)bsum;
-        if ((tid & 15) == 0) L.d[sb >> 4] = dval;
+            *(uint16_t*)(base + 32 * (j >> 2) + 4 * (j & 3)) = (uint16_t)((q[j] & 0xff) | ((q[j + 8] & 0xff) << 8));
+        *(int16_t*)(rec + kRecBs + 2 * s) = (int16_t)bsum;
+        if (s == 0) *(float*)(rec + kRecD) = dval;
     } else {
         float am = 0.f;
 #pragma unroll
@@ -248,14 +238,14 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
         const float id = d != 0.f ? 1.0f / d : 0.0f;
 #pragma unroll
         for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
-        if ((tid & 1) == 0) L.d[sb >> 1] = h2f(f2h(d));
-        const int nch = cols >> 6;
+        uint8_t* rec = L.act + (size_t)(sb >> 4) * kRec;
+        if ((sb & 1) == 0) *(float*)(rec + kRecBs + 2 * (sb & 15)) = h2f(f2h(d));
         u32x4 pk;
 #pragma unroll
         for (int w = 0; w < 4; ++w)
             pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
                     ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
-        *(u32x4*)(L.lo + 16 * ((sb & 3) * nch + (sb >> 2))) = pk;
+        *(u32x4*)(rec + 16 * (sb & 15)) = pk;
     }
 }
 
@@ -367,7 +357,7 @@ __device__ __forceinline__ void mv_prologue(const MVArgs& A, const Lds& L) {
 }
 
 // ----------------------------------------------------------------------------------
-// Per-type 64-weight chunk: load (global) and integer dot against the LDS activation
+// One lane's 256-weight unit of one row: load (global) and ggml's generic block terms
 // ----------------------------------------------------------------------------------
 constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u, M1 = 0x01010101u;
 
@@ -380,89 +370,68 @@ __device__ __forceinline__ void scale_min(int j, uint32_t s0, uint32_t s1, uint3
     sc = (int)(j < 4 ? (b0 & 63u) : sc_hi);
     m = (int)(j < 4 ? (b1 & 63u) : m_hi);
 }
+// the eight 6-bit scales / mins of a K-quant header as bytes: sc_j = byte j%4 of
+// (j < 4 ? sc.x : sc.y), likewise the mins (get_scale_min_k4 for all j at once)
+__device__ __forceinline__ void scales_mins(uint32_t s0, uint32_t s1, uint32_t s2, u32x2& sc, u32x2& mn) {
+    sc.x = s0 & 0x3F3F3F3Fu;
+    mn.x = s1 & 0x3F3F3F3Fu;
+    sc.y = (s2 & M4) | ((s0 >> 2) & 0x30303030u);
+    mn.y = ((s2 >> 4) & M4) | ((s1 >> 2) & 0x30303030u);
+}
 // 4 bits -> the low bit of 4 bytes
 __device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x00204081u) & M1; }
 
-template <int T>
-__host__ __device__ constexpr int kparts() { return T == T_Q8_0 ? 4 : 2; }
-
-// One chunk of one row in registers.
-struct Raw {
-    u32x4 q0, q1, q2, q3;  // quant parts (q2, q3: Q8_0 only)
-    u32x4 hdr;             // Q4_K/Q5_K block header; Q6_K: 2-bit highs (4 dwords)
-    u32x2 qh;              // Q5_K fifth bits (lo 32, hi 32)
-    uint32_t e0;           // Q6_K chunk scales (4 x int8); Q8_0: the two fp16 d
-    uint32_t e1;           // Q6_K fp16 d
+struct PairSum {
+    float a, b;
 };
 
-// Row view: uniform per-row base pointers (SGPRs) so per-lane addressing is a small
-// 32-bit offset: quant part k of chunk ch at qa + (k*nch + ch)*16.
-struct RowPtr {
-    const uint8_t* qa;  // A plane, this row
-    const uint8_t* hb;  // H plane, this row
-    const uint8_t* sb;  // S plane, this row
-    const uint8_t* db;  // D plane, this row
-};
-template <int T>
-__device__ __forceinline__ RowPtr row_ptr(const Seg& s, int row, int cols) {
-    RowPtr r;
-    const size_t nch = (size_t)(cols >> 6), nblk = (T == T_Q8_0) ? (size_t)(cols >> 5) : (size_t)(cols >> 8);
-    r.qa = s.a + (size_t)row * nch * (T == T_Q8_0 ? 64 : 32);
-    r.hb = s.h + (size_t)row * nch * (T == T_Q6_K ? 16 : 8);
-    r.sb = s.s + (size_t)row * nblk * 16;
-    r.db = s.d + (size_t)row * nblk * 2;
-    return r;
-}
+// LDS accesses of one wave handed between its own lanes: LDS executes a wave's
+// instructions in order, so only the compiler must not move accesses across this point
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// Q6_K high bits are stored XOR 2 (common.h): v_perm maps them straight to the signed
+// high part of q - 32 ({0x00, 0x10, 0xE0, 0xF0} for stored 0..3)
+__device__ __forceinline__ uint32_t q6_hi_bytes(uint32_t sel) { return __builtin_amdgcn_perm(0xF0E01000u, 0xF0E01000u, sel); }
 
 template <int T>
-__device__ __forceinline__ Raw load_chunk(const RowPtr& rp, int ch, int nch) {
-    Raw r;
-    const uint32_t o = (uint32_t)ch * 16, step = (uint32_t)nch * 16;
-    r.q0 = ldw(rp.qa + o);
-    r.q1 = ldw(rp.qa + o + step);
-    if constexpr (T == T_Q4_K || T == T_Q5_K) {
-        // the block header is shared by the 4 lanes of a block: default policy (nt loads
-        // of duplicated addresses were fetched once per lane: +24 % FETCH_SIZE)
-        r.hdr = *(const u32x4*)(rp.sb + (uint32_t)(ch >> 2) * 16);
-        if constexpr (T == T_Q5_K) r.qh = ldw8(rp.hb + (uint32_t)ch * 8);
-    } else if constexpr (T == T_Q6_K) {
-        r.hdr = ldw(rp.hb + (uint32_t)ch * 16);
-        r.e0 = ldw4(rp.sb + (uint32_t)ch * 4);
-        r.e1 = *(const uint16_t*)(rp.db + (uint32_t)(ch >> 2) * 2);
+__host__ __device__ constexpr int unit_parts() { return T == T_Q8_0 ? 16 : 8; }
+template <int T>
+__host__ __device__ constexpr int unit_hparts() { return T == T_Q6_K ? 4 : T == T_Q5_K ? 2 : 1; }
+// plane bytes per unit (row strides are U times these)
+template <int T>
+__host__ __device__ constexpr uint32_t unit_abytes() { return T == T_Q8_0 ? 256u : 128u; }
+
+template <int T>
+struct UnitW {
+    u32x4 q[unit_parts<T>()];   // quant parts
+    u32x4 s;                    // Q4_K/Q5_K header; Q6_K 16 scales; Q8_0 eight fp16 d
+    u32x4 h[unit_hparts<T>()];  // Q5_K fifth bits (2 x 16 B); Q6_K 2-bit highs (4 x 16 B)
+    uint32_t d;                 // Q6_K fp16 d
+};
+
+// Unit u of row `row` of a segment.  Loads are unconditional (callers clamp row and
+// unit into the matrix and discard the terms of invalid lanes): straight-line code lets
+// the compiler count vmcnt exactly, so the next unit's loads stay in flight while this
+// one is reduced.  Offsets are 32-bit from the segment's (uniform) plane bases.
+template <int T>
+__device__ __forceinline__ UnitW<T> load_unit(const Seg& sg, uint32_t row, uint32_t u, uint32_t U) {
+    UnitW<T> w;
+    const uint32_t P = U * 16, ru = row * U + u;
+    const uint32_t oa = row * U * unit_abytes<T>() + u * 16;
+#pragma unroll
+    for (int p = 0; p < unit_parts<T>(); ++p) w.q[p] = ldw(sg.a + oa + (uint32_t)p * P);
+    if constexpr (T == T_Q8_0) {
+        w.s = ldw(sg.d + ru * 16);
     } else {
-        r.q2 = ldw(rp.qa + o + 2 * step);
-        r.q3 = ldw(rp.qa + o + 3 * step);
-        r.e0 = ldw4(rp.db + (uint32_t)ch * 4);
+        w.s = ldw(sg.s + ru * 16);
+        if constexpr (T == T_Q5_K || T == T_Q6_K) {
+            const uint32_t oh = row * U * (16u * unit_hparts<T>()) + u * 16;
+#pragma unroll
+            for (int c = 0; c < unit_hparts<T>(); ++c) w.h[c] = ldw(sg.h + oh + (uint32_t)c * P);
+        }
+        if constexpr (T == T_Q6_K) w.d = *(const uint16_t*)(sg.d + ru * 2);
     }
-    return r;
-}
-
-struct Act {
-    i32x4 a0, a1, a2, a3;  // K: lo part 0, lo part 1, hi part 0, hi part 1; Q8_0: parts 0..3
-    int bs[4];
-    float d0, d1;
-};
-template <int ACT>
-__device__ __forceinline__ Act load_act(const Lds& L, int ch, int nch) {
-    Act a;
-    const int step = nch * 16;
-    a.a0 = *(const i32x4*)(L.lo + 16 * ch);
-    a.a1 = *(const i32x4*)(L.lo + 16 * ch + step);
-    if constexpr (ACT == 0) {
-        a.a2 = *(const i32x4*)(L.hi + 16 * ch);
-        a.a3 = *(const i32x4*)(L.hi + 16 * ch + step);
-        const uint2 bw = *(const uint2*)(L.bs + 4 * ch);
-        a.bs[0] = (int16_t)(bw.x & 0xffff); a.bs[1] = (int16_t)(bw.x >> 16);
-        a.bs[2] = (int16_t)(bw.y & 0xffff); a.bs[3] = (int16_t)(bw.y >> 16);
-        a.d0 = L.d[ch >> 2];
-    } else {
-        a.a2 = *(const i32x4*)(L.lo + 16 * ch + 2 * step);
-        a.a3 = *(const i32x4*)(L.lo + 16 * ch + 3 * step);
-        const float2 dd = *(const float2*)(L.d + 2 * ch);
-        a.d0 = dd.x;
-        a.d1 = dd.y;
-    }
-    return a;
+    return w;
 }
 
 // ----------------------------------------------------------------------------------
@@ -476,196 +445,194 @@ __device__ __forceinline__ Act load_act(const Lds& L, int ch, int nch) {
 //   Q8_0:     sumf += (float)sumi(b) * (d_w(b) * d_a(b)) per 32-block b in order
 // Integer sums are exact in any grouping; the fp32 operations run exactly in this order.
 //
-// Device mapping.  Lane L of a wave holds chunk L (+64 j) of the wave's two rows.
-//   chunk_isum  the chunk's integer sums by residue l (the residue-order layout makes
-//               every sdot4 a same-residue dot: t[l] = sc0*dot(lo) + sc1*dot(hi))
-//   quad        the 4 chunks of block b are lanes 4b..4b+3; a reduce-scatter over the
-//               quad leaves residues 2c, 2c+1 of the block's aux32 in lane c
-//   item_terms  the block's fp32 terms d*(float)aux32[l] and -(dmin*(float)sumi) go to
-//               the wave's LDS fold buffer F[row][chain][block]
-//   fold_item   18 fold lanes (2 rows x 9 chains; Q8_0: 2 lanes, one chain) add the
-//               item's terms block after block onto their running chain
-//   fold_final  sumf chain + sums[0..7] in order, both rows, every lane
+// Device mapping.  A lane owns one unit (= one K-quant block) of one row, so a block's
+// integer sums never leave the lane:
+//   unit_terms  the residue-order layout makes every sdot4 a same-residue dot:
+//               aux32[l] = sum over chunks of sc_lo * dot(LO) + sc_hi * dot(HI); the
+//               block's fp32 terms d*(float)aux32[l] and -(dmin*(float)sumi) (Q8_0: the
+//               eight 32-block terms) go to the wave's fold buffer F[row][chain][unit]
+//   fold        fold lane f = (row, chain) adds its chain's terms unit after unit (the
+//               blocks in order) onto its running fp32 chain
+//   final       sumf chain + sums[0..7] in order, one lane per row
 // ----------------------------------------------------------------------------------
-struct PairSum {
-    float a, b;
-};
-constexpr int kFoldRow = 144;                     // floats per row: 9 chains x 16 blocks (Q8_0: 128 blocks)
-constexpr int kFoldFloats = 2 * kFoldRow + 32;   // + the chain results G[18] (padded)
-
-// LDS accesses of one wave handed between its own lanes: LDS executes a wave's
-// instructions in order, so only the compiler must not move accesses across this point
-__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-struct ISum {
-    int t[8];   // K-quants: per-residue sums of the chunk; Q8_0: t[0], t[1] = its two 32-block sums
-    int imin;   // Q4_K/Q5_K: min term of the chunk (m0*(bs0+bs1) + m1*(bs2+bs3)); else 0
-};
-
-// Q6_K high bits are stored XOR 2 (common.h): v_perm maps them straight to the signed
-// high part of q - 32 ({0x00, 0x10, 0xE0, 0xF0} for stored 0..3)
-__device__ __forceinline__ uint32_t q6_hi_bytes(uint32_t sel) { return __builtin_amdgcn_perm(0xF0E01000u, 0xF0E01000u, sel); }
-
 template <int T>
-__device__ __forceinline__ ISum chunk_isum(const Raw& r, const Act& a, int ch) {
-    ISum s;
-    s.imin = 0;
+__host__ __device__ constexpr int unit_chains() { return T == T_Q8_0 ? 8 : 9; }  // terms per unit
+template <int ACT>
+__host__ __device__ constexpr int row_chains() { return ACT ? 1 : 9; }            // fp32 chains per row
+
+// The unit's terms against activation record `rec` (kRec layout): K-quants tm[l] =
+// d*(float)aux32[l] (l < 8), tm[8] = -(dmin*(float)sumi) (Q6_K: +0, there is no min
+// chain and sumf starts at 0); Q8_0 tm[b] = (float)sumi_b * (d_w * d_a), b < 8.
+template <int T>
+__device__ __forceinline__ void unit_terms(const UnitW<T>& w, const uint8_t* rec, float (&tm)[9]) {
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
-        const int c = ch & 3;
-        int sc0, m0, sc1, m1;
-        scale_min(2 * c, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
-        scale_min(2 * c + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
+        u32x2 sc, mn;
+        scales_mins(w.s.y, w.s.z, w.s.w, sc, mn);
+        int t[8];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const u32x4 q = k ? r.q1 : r.q0;
-            const i32x4 al = k ? a.a1 : a.a0, ah = k ? a.a3 : a.a2;
+        for (int l = 0; l < 8; ++l) t[l] = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int c = p >> 1, k = p & 1;
+            // sub-blocks 2c (low nibbles) and 2c + 1 (high nibbles)
+            const uint32_t sw = c < 2 ? sc.x : sc.y;
+            const int slo = (int)((sw >> (16 * (c & 1))) & 0xffu), shi = (int)((sw >> (16 * (c & 1) + 8)) & 0xffu);
+            const i32x4 alo = *(const i32x4*)(rec + 32 * p), ahi = *(const i32x4*)(rec + 32 * p + 16);
+            uint32_t hlo = 0, hhi = 0;
+            if constexpr (T == T_Q5_K) {  // fifth bits of chunk c: byte i, bit l of the lo / hi word
+                hlo = w.h[c >> 1][2 * (c & 1)];
+                hhi = w.h[c >> 1][2 * (c & 1) + 1];
+            }
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                uint32_t l4 = q[m] & M4, h4 = (q[m] >> 4) & M4;
+                const int l = 4 * k + m;
+                uint32_t l4 = w.q[p][m] & M4, h4 = (w.q[p][m] >> 4) & M4;
                 if constexpr (T == T_Q5_K) {
-                    l4 |= spread4((r.qh.x >> (16 * k + 4 * m)) & 0xFu) << 4;
-                    h4 |= spread4((r.qh.y >> (16 * k + 4 * m)) & 0xFu) << 4;
+                    l4 |= (l <= 4 ? hlo << (4 - l) : hlo >> (l - 4)) & 0x10101010u;
+                    h4 |= (l <= 4 ? hhi << (4 - l) : hhi >> (l - 4)) & 0x10101010u;
                 }
-                // |dot| <= 4*31*127: 24-bit multiplies are exact
-                s.t[4 * k + m] = __mul24(sc0, dot4(l4, al[m], 0)) + __mul24(sc1, dot4(h4, ah[m], 0));
+                // |dot| <= 4*31*127, scales <= 63: exact 24-bit multiplies
+                t[l] = __mul24(slo, dot4(l4, alo[m], 0)) + t[l];
+                t[l] = __mul24(shi, dot4(h4, ahi[m], 0)) + t[l];
             }
         }
-        s.imin = m0 * (a.bs[0] + a.bs[1]) + m1 * (a.bs[2] + a.bs[3]);
-    } else if constexpr (T == T_Q6_K) {
-        // bytes 0,1 of a dword are elements l, l+8 (sub-block 4c + 2h), bytes 2,3 are
-        // l+16, l+24 (sub-block 4c + 2h + 1): one masked sdot4 per sub-block
-        const int c0 = (int)(int8_t)(r.e0 & 0xff), c1 = (int)(int8_t)((r.e0 >> 8) & 0xff),
-                  c2 = (int)(int8_t)((r.e0 >> 16) & 0xff), c3 = (int)(int8_t)(r.e0 >> 24);
+        // sumi = sum_j m_j * (bs[2j] + bs[2j+1]): int16 pairs against (m_j, m_j)
+        const i32x4 b0 = *(const i32x4*)(rec + kRecBs), b1 = *(const i32x4*)(rec + kRecBs + 16);
+        int sumi = 0;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const u32x4 q = k ? r.q1 : r.q0;
-            const i32x4 al = k ? a.a1 : a.a0, ah = k ? a.a3 : a.a2;
-            const uint32_t hl = r.hdr[k], hh = r.hdr[2 + k];
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t sel = 0x0c000c00u | (uint32_t)(j & 3) * 0x00010001u;
+            const uint32_t mm = __builtin_amdgcn_perm(0u, j < 4 ? mn.x : mn.y, sel);
+            const int bp = j < 4 ? b0[j] : b1[j - 4];
+            sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, bp), __builtin_bit_cast(short2_t, mm), sumi, false);
+        }
+        const float da = *(const float*)(rec + kRecD);
+        const float d = h2f(w.s.x) * da, dm = h2f(w.s.x >> 16) * da;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) tm[l] = d * (float)t[l];
+        tm[8] = -(dm * (float)sumi);
+    } else if constexpr (T == T_Q6_K) {
+        int t[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) t[l] = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int c = p >> 1, k = p & 1;
+            // sub-blocks 4c + 2h + (i >= 2): bytes 0,1 of a dword are elements l, l+8,
+            // bytes 2,3 are l+16, l+24 -> one masked sdot4 per sub-block
+            const uint32_t s4 = w.s[c];
+            const int c0 = (int)(int8_t)(s4 & 0xff), c1 = (int)(int8_t)((s4 >> 8) & 0xff),
+                      c2 = (int)(int8_t)((s4 >> 16) & 0xff), c3 = (int)(int8_t)(s4 >> 24);
+            const i32x4 alo = *(const i32x4*)(rec + 32 * p), ahi = *(const i32x4*)(rec + 32 * p + 16);
+            const uint32_t hl = w.h[c][k], hh = w.h[c][2 + k];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const uint32_t wl = (q[m] & M4) | q6_hi_bytes((hl >> (2 * m)) & M2);
-                const uint32_t wh = ((q[m] >> 4) & M4) | q6_hi_bytes((hh >> (2 * m)) & M2);
-                const int s0 = dot4(wl, al[m] & 0xffff, 0), s1 = dot4(wl, al[m] & (int)0xffff0000u, 0);
-                const int s2 = dot4(wh, ah[m] & 0xffff, 0), s3 = dot4(wh, ah[m] & (int)0xffff0000u, 0);
+                const uint32_t q = w.q[p][m];
+                const uint32_t wl = (q & M4) | q6_hi_bytes((hl >> (2 * m)) & M2);
+                const uint32_t wh = ((q >> 4) & M4) | q6_hi_bytes((hh >> (2 * m)) & M2);
                 // |s| <= 2*32*127, |c| <= 128: exact in 24-bit multiplies
-                s.t[4 * k + m] = __mul24(c0, s0) + __mul24(c1, s1) + __mul24(c2, s2) + __mul24(c3, s3);
+                int a = t[4 * k + m];
+                a = __mul24(c0, dot4(wl, alo[m] & 0xffff, 0)) + a;
+                a = __mul24(c1, dot4(wl, alo[m] & (int)0xffff0000u, 0)) + a;
+                a = __mul24(c2, dot4(wh, ahi[m] & 0xffff, 0)) + a;
+                a = __mul24(c3, dot4(wh, ahi[m] & (int)0xffff0000u, 0)) + a;
+                t[4 * k + m] = a;
             }
         }
-    } else {
-        int s0 = 0, s1 = 0;
+        const float d = h2f(w.d) * *(const float*)(rec + kRecD);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            s0 = dot4(r.q0[m], a.a0[m], s0);
-            s0 = dot4(r.q1[m], a.a1[m], s0);
-            s1 = dot4(r.q2[m], a.a2[m], s1);
-            s1 = dot4(r.q3[m], a.a3[m], s1);
-        }
-        s.t[0] = s0;
-        s.t[1] = s1;
-    }
-    return s;
-}
-
-// Quad reduce-scatter of the block's per-residue sums (lanes 4b..4b+3): lane c keeps
-// residues 2c, 2c+1 (a0, a1); the min term is summed into every lane of the quad.
-__device__ __forceinline__ void quad_scatter(ISum& s, int& a0, int& a1) {
-    const bool b0 = (threadIdx.x & 1) != 0, b1 = (threadIdx.x & 2) != 0;
-    // level 1 (lane ^ 1): keep residue pairs b0 and b0 + 2
-    int k[4];
-    {
-        const int s0 = b0 ? s.t[0] : s.t[2], s1 = b0 ? s.t[1] : s.t[3];
-        const int s2 = b0 ? s.t[4] : s.t[6], s3 = b0 ? s.t[5] : s.t[7];
-        k[0] = (b0 ? s.t[2] : s.t[0]) + xor_partner_i<1>(s0);
-        k[1] = (b0 ? s.t[3] : s.t[1]) + xor_partner_i<1>(s1);
-        k[2] = (b0 ? s.t[6] : s.t[4]) + xor_partner_i<1>(s2);
-        k[3] = (b0 ? s.t[7] : s.t[5]) + xor_partner_i<1>(s3);
-    }
-    // level 2 (lane ^ 2): keep pair b0 + 2*b1 = c
-    const int r0 = b1 ? k[0] : k[2], r1 = b1 ? k[1] : k[3];
-    a0 = (b1 ? k[2] : k[0]) + xor_partner_i<2>(r0);
-    a1 = (b1 ? k[3] : k[1]) + xor_partner_i<2>(r1);
-    s.imin += xor_partner_i<1>(s.imin);
-    s.imin += xor_partner_i<2>(s.imin);
-}
-
-// The item's fp32 terms of one row into its fold buffer Fr (chain ch, block bi at
-// Fr[ch * 16 + bi]; Q8_0: Fr[bi], 128 blocks).  Every lane calls it (cross-lane ops);
-// `valid` (the chunk exists) guards only the stores — chunks past the row come in whole
-// blocks (cols % 256 == 0).
-template <int T>
-__device__ __forceinline__ void item_terms(const Raw& r, const Act& a, int ch, bool valid, float* Fr) {
-    ISum s = chunk_isum<T>(r, a, ch);
-    const int lane = threadIdx.x & 63;
-    if constexpr (T == T_Q8_0) {
-        const float t0 = (float)s.t[0] * (h2f(r.e0) * a.d0), t1 = (float)s.t[1] * (h2f(r.e0 >> 16) * a.d1);
-        if (valid) *(float2*)(Fr + 2 * lane) = make_float2(t0, t1);
+        for (int l = 0; l < 8; ++l) tm[l] = d * (float)t[l];
+        tm[8] = 0.f;
     } else {
-        int a0, a1;
-        quad_scatter(s, a0, a1);
-        const int c = lane & 3, bi = lane >> 2;
-        const float d = (T == T_Q6_K ? h2f(r.e1) : h2f(r.hdr.x)) * a.d0;
-        const float p0 = d * (float)a0, p1 = d * (float)a1;
-        float nq = 0.f;
-        if constexpr (T != T_Q6_K) nq = -((h2f(r.hdr.x >> 16) * a.d0) * (float)s.imin);
-        if (valid) {
-            Fr[(2 * c) * 16 + bi] = p0;
-            Fr[(2 * c + 1) * 16 + bi] = p1;
-            if (c == 0) Fr[8 * 16 + bi] = nq;  // Q6_K: no min chain (+0 terms, as sumf = 0)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const i32x4 a0 = *(const i32x4*)(rec + 32 * b), a1 = *(const i32x4*)(rec + 32 * b + 16);
+            int si = 0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) si = dot4(w.q[2 * b][m], a0[m], si);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) si = dot4(w.q[2 * b + 1][m], a1[m], si);
+            const float dw = h2f(w.s[b >> 1] >> (16 * (b & 1))), da = *(const float*)(rec + kRecBs + 4 * b);
+            tm[b] = (float)si * (dw * da);
         }
+        tm[8] = 0.f;
     }
 }
 
-// blocks of item j of a row of `cols` weights (K-quants: 16 per item, Q8_0: 128)
-template <int ACT>
-__device__ __forceinline__ int item_blocks(int cols, int j) {
-    const int nb = ACT ? (cols >> 5) - 128 * j : (cols >> 8) - 16 * j;
-    const int per = ACT ? 128 : 16;
-    return nb < per ? nb : per;
+// ----------------------------------------------------------------------------------
+// Row tasks.  A matvec launch's rows are cut into TASKS of R rows (gate/up launches: R
+// gate rows then the same R up rows); lane L works on row r = L / Lr of the task, units
+// L % Lr + Lr j (Lr lanes per row, a multiple of 4; R = 64 / Lr rounded down to a power
+// of two).  A task is NJ = ceil(U / Lr) SUB-ITEMS (SwiGLU: 2 NJ, gate rows first), each
+// within one segment, so its plane bases are uniform.  The host fills MVGeom.
+// ----------------------------------------------------------------------------------
+struct TaskGeo {
+    int lr, R, nj, U;
+};
+__host__ __device__ inline TaskGeo task_geo(const MVArgs& A) {
+    TaskGeo g;
+    g.lr = A.lr;
+    g.R = A.rpt;
+    g.U = A.cols >> 8;
+    g.nj = (g.U + g.lr - 1) / g.lr;
+    return g;
 }
 
-// Fold lane f (< 18, Q8_0 < 2) adds chain f's terms of nb blocks in block order.
+// Fold buffer per wave: F[row][chain][Lr] terms + G[row][chain] chain results.
+constexpr int kFoldF = 9 * 64, kFoldFloats = kFoldF + 9 * 16;
+
+// Fold lane f (< R * chains) adds its chain's n terms of the sub-item (K-quants: chain f
+// = (row f / 9, chain f % 9), Lr terms apart; Q8_0: chain = row f, 8 terms per unit) in
+// unit order onto acc; on the task's last sub-item of the row set the chain result goes
+// to G[f] and acc restarts.  Only NJ == 1 geometries have more than 64 chains (then no
+// chain carries across sub-items).
 template <int ACT>
-__device__ __forceinline__ void fold_item(const float* F, int nb, float& acc) {
-    constexpr int NC = ACT ? 1 : 9, CS = ACT ? 128 : 16;
-    const int lane = threadIdx.x & 63;
-    if (lane < 2 * NC) {
-        const int r = lane >= NC ? 1 : 0;
-        const float* p = F + r * kFoldRow + (lane - r * NC) * CS;
-        for (int b = 0; b < nb; b += 4) {
-            const float4 v = *(const float4*)(p + b);
-            acc += v.x;
-            if (b + 1 < nb) acc += v.y;
-            if (b + 2 < nb) acc += v.z;
-            if (b + 3 < nb) acc += v.w;
+__device__ __forceinline__ void fold_sub(float* F, int R, int lr, int n, bool last, float& acc) {
+    constexpr int NC = row_chains<ACT>();
+    const int lane = threadIdx.x & 63, nf = R * NC;
+    const int len = ACT ? 8 * n : n, stride = ACT ? 8 * lr : lr;
+    for (int f = lane; f < nf; f += 64) {
+        float a = acc;
+        const float* q = F + f * stride;
+        for (int b = 0; b < len; b += 4) {
+            const float4 v = *(const float4*)(q + b);
+            a += v.x;
+            if (b + 1 < len) a += v.y;
+            if (b + 2 < len) a += v.z;
+            if (b + 3 < len) a += v.w;
         }
+        if (last) {
+            F[kFoldF + f] = a;
+            a = 0.f;
+        }
+        acc = a;
     }
 }
-
-// Both rows' final sums in every lane: sumf chain, then += sums[0..7] (K-quants).
+// final value of row r of the task from G (after a wave_lds_sync)
 template <int ACT>
-__device__ __forceinline__ PairSum fold_final(float* F, float acc) {
-    constexpr int NC = ACT ? 1 : 9;
-    float* G = F + 2 * kFoldRow;
-    const int lane = threadIdx.x & 63;
-    wave_lds_sync();
-    if (lane < 2 * NC) G[lane] = acc;
-    wave_lds_sync();
-    PairSum v;
+__device__ __forceinline__ float row_final(const float* F, int r) {
+    const float* g = F + kFoldF;
     if constexpr (ACT) {
-        v.a = G[0];
-        v.b = G[1];
+        return g[r];
     } else {
-        float sa = G[8], sb = G[17];
+        float v = g[9 * r + 8];
 #pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            sa += G[l];
-            sb += G[9 + l];
-        }
-        v.a = sa;
-        v.b = sb;
+        for (int l = 0; l < 8; ++l) v += g[9 * r + l];
+        return v;
     }
-    wave_lds_sync();
-    return v;
+}
+// the unit's terms into F (lane: row r, unit index ul of the sub-item)
+template <int T>
+__device__ __forceinline__ void store_terms(float* F, int r, int ul, int lr, const float (&tm)[9]) {
+    if constexpr (T == T_Q8_0) {
+        float* q = F + (r * lr + ul) * 8;
+        *(float4*)q = make_float4(tm[0], tm[1], tm[2], tm[3]);
+        *(float4*)(q + 4) = make_float4(tm[4], tm[5], tm[6], tm[7]);
+    } else {
+        float* q = F + r * 9 * lr + ul;
+#pragma unroll
+        for (int c = 0; c < 9; ++c) q[c * lr] = tm[c];
+    }
 }
 
 // (the descriptor type is a template parameter: the persistent step reads its phase
@@ -716,36 +683,6 @@ __device__ __forceinline__ PairRef pair_ref(const MA& A, int p) {
     r.type = r.sa.type == r.sb.type ? r.sa.type : -1;
     return r;
 }
-
-template <int T>
-struct PairRaw {
-    Raw a, b;
-};
-template <int T>
-struct PairRows {
-    RowPtr a, b;
-};
-
-template <int T>
-__device__ __forceinline__ PairRows<T> pair_rows(const PairRef& r, int cols) {
-    PairRows<T> pr;
-    pr.a = row_ptr<T>(r.sa, r.ra, cols);
-    pr.b = row_ptr<T>(r.sb, r.vb ? r.rb : r.ra, cols);
-    return pr;
-}
-
-// Unconditional loads (the chunk index is clamped to a valid one; callers discard the
-// contribution of out-of-range lanes): straight-line code lets the compiler count
-// vmcnt exactly, so the next item's loads stay in flight while this one is reduced.
-template <int T>
-__device__ __forceinline__ PairRaw<T> load_item(const PairRows<T>& pr, int ch, int nch) {
-    PairRaw<T> w;
-    const int c = ch < nch ? ch : nch - 1;
-    w.a = load_chunk<T>(pr.a, c, nch);
-    w.b = load_chunk<T>(pr.b, c, nch);
-    return w;
-}
-
 
 // ordered key of (logit, row): larger logit wins, ties -> smaller row (first max wins,
 // as upstream llama_sampler_greedy's strict '>' scan)
@@ -838,82 +775,153 @@ __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, P
     }
 }
 
-// Non-pipelined fallback for pairs whose type is not the kernel's primary type (the
-// Q6_K attn_v segment inside a Q4_K QKV launch, mixed-type gate/up pairs): the same
-// terms and fold, one item at a time, each row in its own type.
-template <int ACT, int T>
-__device__ __forceinline__ void row_terms(const Seg& s, int row, int cols, int ch, const Act& act, float* Fr) {
-    const int nch = cols >> 6;
-    const RowPtr rp = row_ptr<T>(s, row, cols);
-    const int chc = ch < nch ? ch : nch - 1;
-    item_terms<T>(load_chunk<T>(rp, chc, nch), act, chc, ch < nch, Fr);
-}
-template <int ACT>
-__device__ __forceinline__ void row_terms_any(int type, const Seg& s, int row, int cols, int ch, const Act& act,
-                                              float* Fr) {
-    if constexpr (ACT == 1) {
-        row_terms<1, T_Q8_0>(s, row, cols, ch, act, Fr);
+// Sub-item s of a task: its segment, the segment-local row of the task's row 0 and the
+// unit block j (units Lr j .. Lr j + Lr - 1).  Uniform per wave.
+struct Sub {
+    int si, row0, j;
+};
+template <int EPI, class MA>
+__device__ __forceinline__ Sub sub_of(const MA& A, const TaskGeo& g, int task, int s) {
+    Sub b;
+    if constexpr (EPI == EPI_SWIGLU) {  // gate rows (segment 0) for s < NJ, then the same up rows
+        b.si = s >= g.nj ? 1 : 0;
+        b.j = s - b.si * g.nj;
+        b.row0 = task * g.R;
     } else {
-        switch (type) {
-            case T_Q4_K: row_terms<0, T_Q4_K>(s, row, cols, ch, act, Fr); break;
-            case T_Q5_K: row_terms<0, T_Q5_K>(s, row, cols, ch, act, Fr); break;
-            case T_Q6_K: row_terms<0, T_Q6_K>(s, row, cols, ch, act, Fr); break;
-            default: break;
+        // (the starts pass through readfirstlane so that the select below stays a select
+        // of values: folded into A.seg[si] it copies the kernel arguments to scratch)
+        const int r0 = uniform(A.seg[0].row0), r1 = uniform(A.seg[1].row0), r2 = uniform(A.seg[2].row0);
+        const int q = r0 + task * g.R;
+        int si = 0;
+        if (A.nseg > 1 && q >= r1) si = 1;
+        if (A.nseg > 2 && q >= r2) si = 2;
+        b.si = si;
+        b.j = s;
+        b.row0 = q - (si == 0 ? r0 : si == 1 ? r1 : r2);
+    }
+    return b;
+}
+// is every sub-item of the task of type T (the pipelined type)?
+template <int EPI, int T, class MA>
+__device__ __forceinline__ bool task_is(const MA& A, const TaskGeo& g, int task) {
+    if constexpr (EPI == EPI_SWIGLU) return A.seg[0].type == T && A.seg[1].type == T;
+    else return pick(A, sub_of<EPI>(A, g, task, 0).si).type == T;
+}
+
+// The lane's row / unit of a sub-item, clamped into the matrix (loads stay unconditional).
+struct LaneUnit {
+    uint32_t row, u;
+    bool valid;
+};
+__device__ __forceinline__ LaneUnit lane_unit(const TaskGeo& g, const Sub& b, const Seg& sg, int r, int ul) {
+    LaneUnit x;
+    const int row = b.row0 + r, u = ul + g.lr * b.j;
+    x.valid = r < g.R && row < sg.rows && u < g.U;
+    x.row = (uint32_t)(row < sg.rows ? row : sg.rows - 1);
+    x.u = (uint32_t)(u < g.U ? u : g.U - 1);
+    return x;
+}
+
+// After the lanes' unit terms: store, fold, and on the row set's last sub-item the row
+// results and the epilogue (lane r' < R handles row r' of the task).
+template <int ACT, int EPI, class MA>
+__device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo& g, int s, const Sub& b, const Seg& sg,
+                                           const float (&tm)[9], const LaneUnit& lu, int r, int ul, float& acc,
+                                           float& vg, int pos, unsigned long long& best) {
+    if (lu.valid) store_terms<ACT ? T_Q8_0 : T_Q4_K>(F, r, ul, g.lr, tm);
+    wave_lds_sync();
+    const int n = min(g.lr, g.U - g.lr * b.j);
+    const bool last = b.j == g.nj - 1;
+    fold_sub<ACT>(F, g.R, g.lr, n, last, acc);
+    if (last) {
+        wave_lds_sync();
+        const int lane = threadIdx.x & 63;
+        const int row = b.row0 + lane;
+        if (lane < g.R && row < sg.rows) {
+            const float v = row_final<ACT>(F, lane);
+            PairRef ref;
+            ref.sa = ref.sb = sg;
+            ref.ra = row;
+            ref.rb = row + 1;
+            ref.vb = 0;
+            ref.type = sg.type;
+            if constexpr (EPI == EPI_SWIGLU) {
+                if (s < g.nj) vg = v;
+                else epilogue<EPI, false, MA, true>(A, ref, row, PairSum{vg, v}, pos, best);
+            } else if constexpr (EPI == EPI_QKV) {
+                ref.vb = 1;  // RoPE pairs (row, row + 1): R and every segment start are even
+                if ((lane & 1) == 0) epilogue<EPI, false, MA, true>(A, ref, row, PairSum{v, row_final<ACT>(F, lane + 1)}, pos, best);
+            } else {
+                epilogue<EPI, false, MA, true>(A, ref, row, PairSum{v, 0.f}, pos, best);
+            }
         }
     }
+    wave_lds_sync();  // the fold / final reads before the next sub-item's stores
 }
-template <int ACT>
-__device__ __forceinline__ PairSum pair_any(const PairRef& r, int cols, const Lds& L, float* F) {
-    const int nch = cols >> 6, NJ = (nch + 63) >> 6;
-    const int lane = threadIdx.x & 63;
-    float acc = 0.f;
-    for (int j = 0; j < NJ; ++j) {
-        const int ch = lane + 64 * j, chc = ch < nch ? ch : nch - 1;
-        const Act act = load_act<ACT>(L, chc, nch);
-        row_terms_any<ACT>(r.sa.type, r.sa, r.ra, cols, ch, act, F);
-        row_terms_any<ACT>(r.sb.type, r.sb, r.vb ? r.rb : r.ra, cols, ch, act, F + kFoldRow);
-        wave_lds_sync();
-        fold_item<ACT>(F, item_blocks<ACT>(cols, j), acc);
-        wave_lds_sync();
+
+// One task of any type, not pipelined (tasks whose type is not the kernel's primary type:
+// the Q6_K attn_v rows of a Q4_K QKV launch, mixed-type gate/up).
+template <int ACT, int EPI, class MA>
+__device__ __forceinline__ void task_any(const MA& A, const Lds& L, float* F, const TaskGeo& g, int task, int r, int ul,
+                                         int pos, unsigned long long& best) {
+    const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
+    float acc = 0.f, vg = 0.f;
+    for (int s = 0; s < S; ++s) {
+        const Sub b = sub_of<EPI>(A, g, task, s);
+        const Seg sg = pick(A, b.si);
+        const LaneUnit lu = lane_unit(g, b, sg, r, ul);
+        const uint8_t* rec = L.act + (size_t)lu.u * kRec;
+        float tm[9];
+        if constexpr (ACT == 1) {
+            unit_terms<T_Q8_0>(load_unit<T_Q8_0>(sg, lu.row, lu.u, g.U), rec, tm);
+        } else {
+            switch (sg.type) {
+                case T_Q4_K: unit_terms<T_Q4_K>(load_unit<T_Q4_K>(sg, lu.row, lu.u, g.U), rec, tm); break;
+                case T_Q5_K: unit_terms<T_Q5_K>(load_unit<T_Q5_K>(sg, lu.row, lu.u, g.U), rec, tm); break;
+                default: unit_terms<T_Q6_K>(load_unit<T_Q6_K>(sg, lu.row, lu.u, g.U), rec, tm); break;
+            }
+        }
+        sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
     }
-    return fold_final<ACT>(F, acc);
 }
 
 // get_rows: element e of row `row` dequantized from the device layout (bit-exact with
 // upstream dequantize_row_*)
 __device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int cols) {
+    const size_t U = (size_t)(cols >> 8), u = (size_t)(e >> 8), ru = (size_t)row * U + u;
     switch (w.type) {
         case T_F32: return ((const float*)w.a)[(size_t)row * cols + e];
         case T_F16: return h2f(((const uint16_t*)w.a)[(size_t)row * cols + e]);
         case T_Q4_K:
         case T_Q5_K:
         case T_Q6_K: {
-            // residue order (common.h): chunk element t = 32 hi + l + 8 i sits in part
-            // k = l / 4, byte 4 (l % 4) + i (low nibble: hi = 0, high nibble: hi = 1)
-            const int nch = cols >> 6, nbr = cols >> 8;
-            const int ch = e >> 6, t = e & 63, hi = t >= 32, l = t & 7, i = (t & 31) >> 3, k = l >> 2, m = l & 3;
-            const size_t gb = (size_t)row * nbr + (e >> 8);
-            const uint8_t qb = w.a[(size_t)row * nch * 32 + (size_t)(k * nch + ch) * 16 + 4 * m + i];
+            // residue order (common.h): element 64c + 32hi + l + 8i of the unit sits in
+            // part 2c + l/4, byte 4 (l % 4) + i (low nibble: hi = 0, high nibble: hi = 1)
+            const int t = e & 255, c = t >> 6, hi = (t >> 5) & 1, l = t & 7, i = (t & 31) >> 3, k = l >> 2, m = l & 3;
+            const uint8_t qb = w.a[(size_t)row * U * 128 + ((size_t)(2 * c + k) * U + u) * 16 + 4 * m + i];
             int q = hi ? (qb >> 4) : (qb & 0xF);
-            if (w.type == T_Q6_K) {  // H dword (2*hi + k), byte i, bits 2m: the 2 high bits XOR 2
-                const uint8_t hb = w.h[((size_t)row * nch + ch) * 16 + (2 * hi + k) * 4 + i];
+            if (w.type == T_Q6_K) {  // H part c: dword (2*hi + k), byte i, bits 2m: the 2 high bits XOR 2
+                const uint8_t hb = w.h[(size_t)row * U * 64 + ((size_t)c * U + u) * 16 + (2 * hi + k) * 4 + i];
                 q |= (((hb >> (2 * m)) & 3) ^ 2) << 4;
-                const float d = h2f(*(const uint16_t*)(w.d + gb * 2));
-                const int sc = (int8_t)w.s[gb * 16 + ((e & 255) >> 4)];
+                const float d = h2f(*(const uint16_t*)(w.d + ru * 2));
+                const int sc = (int8_t)w.s[ru * 16 + (t >> 4)];
                 return d * (float)sc * (float)(q - 32);
             }
-            const uint32_t* s32 = (const uint32_t*)(w.s + gb * 16);
+            const uint32_t* s32 = (const uint32_t*)(w.s + ru * 16);
             int sc, mn;
-            scale_min(2 * (ch & 3) + hi, s32[1], s32[2], s32[3], sc, mn);
-            if (w.type == T_Q5_K) q += ((ldw4(w.h + ((size_t)row * nch + ch) * 8 + 4 * hi) >> (4 * l + i)) & 1) << 4;
+            scale_min(2 * c + hi, s32[1], s32[2], s32[3], sc, mn);
+            if (w.type == T_Q5_K) {  // H part c/2: chunk c's lo / hi word, byte i, bit l
+                const uint8_t hb = w.h[(size_t)row * U * 32 + ((size_t)(c >> 1) * U + u) * 16 + 8 * (c & 1) + 4 * hi + i];
+                q += ((hb >> l) & 1) << 4;
+            }
             const float d = h2f(s32[0]), dmin = h2f(s32[0] >> 16);
             const float d1 = d * (float)sc, m1 = dmin * (float)mn;
             return d1 * (float)q - m1;
         }
         case T_Q8_0: {
-            const int nch = cols >> 6, ch = e >> 6, t = e & 63;
-            const uint8_t qb = w.a[(size_t)row * nch * 64 + (size_t)((t >> 4) * nch + ch) * 16 + (t & 15)];
-            return (float)(int8_t)qb * h2f(*(const uint16_t*)(w.d + ((size_t)row * (cols / 32) + e / 32) * 2));
+            const int t = e & 255;
+            const uint8_t qb = w.a[(size_t)row * U * 256 + ((size_t)(t >> 4) * U + u) * 16 + (t & 15)];
+            return (float)(int8_t)qb * h2f(*(const uint16_t*)(w.d + ru * 16 + 2 * (t >> 5)));
         }
         default: return 0.f;
     }

@@ -27,6 +27,8 @@ class FakeEngine:
     def __init__(self, rank):
         self.rank = rank
         self.runs = []
+        self.pos = 128  # after the C2 prompt
+
 
     def warmup(self, n):
         self.runs.append(("warmup", n))
@@ -68,7 +70,13 @@ def test_two_rank_timed_region_gloo():
     (r0, dt0, max0, runs0, uid0), (r1, dt1, max1, runs1, uid1) = res
     assert max0 == max1 == pytest.approx(max(dt0, dt1))
     assert max0 >= 0.02  # the slower rank's 20 ms dominates the job time
-    assert runs0 == runs1 == [("warmup", 3), ("run", 7)]
+    # untimed steps up to the C2 trajectory's mid window (bench.window_start), then K
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pre = bench.window_start(128, 7, 3) - 128
+    assert pre >= 3
+    assert runs0 == runs1 == [("warmup", pre), ("run", 7)]
     assert uid0 == uid1 == b"unique-id-from-rank0"
 
 
