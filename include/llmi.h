@@ -113,8 +113,27 @@ const struct llama_vocab* llama_model_get_vocab(const struct llama_model* model)
 int32_t llama_vocab_n_tokens(const struct llama_vocab* vocab);
 llama_token llama_vocab_bos(const struct llama_vocab* vocab);
 llama_token llama_vocab_eos(const struct llama_vocab* vocab);
-/* raw GGUF token text of `token` (no byte-fallback decoding yet: SURVEY.md §8f row 2) */
+/* raw GGUF token text of `token` */
 const char* llama_vocab_get_text(const struct llama_vocab* vocab, llama_token token);
+bool llama_vocab_get_add_bos(const struct llama_vocab* vocab);
+/* ---------- tokenizer (upstream llama-vocab.cpp, reached through llama-server's prompt
+ * tokenization and streamed detokenization, scripts/gateway.py:699-804 -> upstream).
+ * The GGUF's own tokenizer: tokenizer.ggml.model "llama" + scores -> SPM, "gpt2" +
+ * merges -> byte-level BPE (llama3 / gpt-2 pre-tokenizer), otherwise greedy longest
+ * match; special tokens partitioned first when parse_special (csrc/tokenizer.h). ---------- */
+/* upstream llama_tokenize: writes the ids and returns their count, or -(count) when
+ * n_tokens_max is too small (nothing written); INT32_MIN on bad arguments */
+int32_t llama_tokenize(const struct llama_vocab* vocab, const char* text, int32_t text_len, llama_token* tokens,
+                       int32_t n_tokens_max, bool add_special, bool parse_special);
+/* upstream llama_token_to_piece: the token's bytes (no NUL) and their count, or -(count)
+ * when length is too small; up to lstrip leading spaces skipped; special: CONTROL
+ * tokens render their text (else nothing) */
+int32_t llama_token_to_piece(const struct llama_vocab* vocab, llama_token token, char* buf, int32_t length,
+                             int32_t lstrip, bool special);
+/* upstream llama_detokenize: the pieces concatenated (remove_special: without a leading
+ * BOS / trailing EOS; unparse_special: CONTROL text kept); count or -(count needed) */
+int32_t llama_detokenize(const struct llama_vocab* vocab, const llama_token* tokens, int32_t n_tokens, char* text,
+                         int32_t text_len_max, bool remove_special, bool unparse_special);
 int32_t llama_model_n_embd(const struct llama_model* model);
 int32_t llama_model_n_layer(const struct llama_model* model);
 int32_t llama_model_n_head(const struct llama_model* model);
@@ -189,7 +208,9 @@ int32_t llmi_prefill_supported(const struct llama_model* model);
 /* Device weight arena (for RCCL broadcast by a caller that owns the communicator). */
 int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64_t* bytes);
 /* In-process replica fan-out: copies model's arena to devices[0..n) with an RCCL
- * broadcast over xGMI and returns one model handle per device (out[i]). 0 on success. */
+ * broadcast over xGMI and returns one model handle per device (out[i]). 0 on success;
+ * -1 (nothing allocated) for bad arguments, an out-of-range device, or a device listed
+ * twice or equal to the source model's device. */
 int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_t n, struct llama_model** out);
 
 /* Multi-process replica fan-out (one process per GPU): rank 0 holds the
@@ -199,6 +220,12 @@ int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_
  * from rank 0 over xGMI with one ncclBroadcast.  Returns 0 on success. */
 int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n);
 int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank);
+
+/* A tokenizer-only vocabulary handle from a GGUF's tokenizer.* metadata (no tensors
+ * or device needed); free with llmi_vocab_free (handles from llama_model_get_vocab are
+ * owned by their model).  NULL on error. */
+struct llama_vocab* llmi_vocab_load_from_file(const char* path);
+void llmi_vocab_free(struct llama_vocab* vocab);
 
 /* Synthetic GGUF writer: preset = "llama3-8b-q4km", "tinyllama-q8_0",
  * "mistral7b-q6k", "mistral7b-q5km", "llama3-70b-q4km", or "tiny-mixed" (2 layers, E=256,

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -21,7 +22,9 @@ struct llama_model {
     Model m;
 };
 struct llama_vocab {
-    const Model* m;
+    const Model* m;                      // null for llmi_vocab_load_from_file handles
+    const Tokenizer* tok;
+    std::unique_ptr<Tokenizer> owned;
 };
 struct llama_context {
     Context c;
@@ -52,7 +55,10 @@ llama_vocab* vocab_handle(const llama_model* m) {
     static thread_local std::vector<std::unique_ptr<llama_vocab>> pool;
     for (auto& v : pool)
         if (v->m == &m->m) return v.get();
-    pool.push_back(std::make_unique<llama_vocab>(llama_vocab{&m->m}));
+    auto v = std::make_unique<llama_vocab>();
+    v->m = &m->m;
+    v->tok = m->m.tok.get();
+    pool.push_back(std::move(v));
     return pool.back().get();
 }
 
@@ -657,6 +663,21 @@ int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64
 int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_t n, struct llama_model** out) {
     API_TRY
     if (!model || !devices || n <= 0 || !out) { set_err("llmi_replicate: bad arguments"); return -1; }
+    // one RCCL rank per device: a device listed twice (or the source's own device) would
+    // put two ranks of the communicator on one GPU
+    {
+        const int nd = llmi_device_count();
+        std::vector<int> seen{model->m.device};
+        for (int i = 0; i < n; ++i) {
+            if (devices[i] < 0 || devices[i] >= nd) { set_err("llmi_replicate: device index out of range"); return -1; }
+            if (std::find(seen.begin(), seen.end(), devices[i]) != seen.end()) {
+                set_err("llmi_replicate: device " + std::to_string(devices[i]) +
+                        " listed twice (or the source model's own device)");
+                return -1;
+            }
+            seen.push_back(devices[i]);
+        }
+    }
     std::vector<llama_model*> reps((size_t)n, nullptr);
     std::string err;
     for (int i = 0; i < n; ++i) {
@@ -735,12 +756,91 @@ int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t
 const struct llama_vocab* llama_model_get_vocab(const struct llama_model* model) {
     return model ? vocab_handle(model) : nullptr;
 }
-int32_t llama_vocab_n_tokens(const struct llama_vocab* v) { return v ? v->m->hp.n_vocab : 0; }
-llama_token llama_vocab_bos(const struct llama_vocab* v) { return v ? v->m->bos : -1; }
-llama_token llama_vocab_eos(const struct llama_vocab* v) { return v ? v->m->eos : -1; }
+int32_t llama_vocab_n_tokens(const struct llama_vocab* v) {
+    return !v ? 0 : v->m ? v->m->hp.n_vocab : (int32_t)v->tok->tokens.size();
+}
+llama_token llama_vocab_bos(const struct llama_vocab* v) { return v ? v->tok->bos : -1; }
+llama_token llama_vocab_eos(const struct llama_vocab* v) { return v ? v->tok->eos : -1; }
 const char* llama_vocab_get_text(const struct llama_vocab* v, llama_token t) {
-    if (!v || t < 0 || t >= (int)v->m->vocab.size()) return nullptr;
-    return v->m->vocab[(size_t)t].c_str();
+    if (!v || t < 0 || t >= (int)v->tok->tokens.size()) return nullptr;
+    return v->tok->tokens[(size_t)t].c_str();
+}
+bool llama_vocab_get_add_bos(const struct llama_vocab* v) { return v && v->tok->add_bos; }
+
+// upstream llama_tokenize: the count, or -(count) when n_tokens_max is too small
+int32_t llama_tokenize(const struct llama_vocab* v, const char* text, int32_t text_len, llama_token* tokens,
+                       int32_t n_tokens_max, bool add_special, bool parse_special) {
+    if (!v || (!text && text_len > 0) || text_len < 0) {
+        set_err("llama_tokenize: bad arguments");
+        return INT32_MIN;
+    }
+    try {
+        const std::vector<int32_t> ids = v->tok->tokenize(std::string(text ? text : "", (size_t)text_len), add_special,
+                                                          parse_special);
+        if ((int64_t)ids.size() > (int64_t)INT32_MAX) {
+            set_err("llama_tokenize: too many tokens");
+            return INT32_MIN;
+        }
+        const int32_t n = (int32_t)ids.size();
+        if (n > n_tokens_max) return -n;
+        for (int32_t i = 0; i < n; ++i) tokens[i] = ids[(size_t)i];
+        return n;
+    } catch (const std::exception& e) {
+        set_err(std::string("llama_tokenize: ") + e.what());
+        return INT32_MIN;
+    }
+}
+
+// upstream llama_token_to_piece: bytes written (no NUL), or -(bytes needed); up to
+// lstrip leading spaces are skipped; special renders CONTROL tokens as their text
+int32_t llama_token_to_piece(const struct llama_vocab* v, llama_token token, char* buf, int32_t length, int32_t lstrip,
+                             bool special) {
+    if (!v) return 0;
+    std::string p = v->tok->piece(token, special);
+    size_t k = 0;
+    while (lstrip > 0 && k < p.size() && p[k] == ' ') {
+        ++k;
+        --lstrip;
+    }
+    const int32_t n = (int32_t)(p.size() - k);
+    if (n > length) return -n;
+    if (n > 0) memcpy(buf, p.data() + k, (size_t)n);
+    return n;
+}
+
+// upstream llama_detokenize: the pieces concatenated; remove_special drops a leading BOS
+// (when the vocabulary adds one) and a trailing EOS; unparse_special renders CONTROL text.
+// Bytes written, or -(bytes needed).
+int32_t llama_detokenize(const struct llama_vocab* v, const llama_token* tokens, int32_t n_tokens, char* text,
+                         int32_t text_len_max, bool remove_special, bool unparse_special) {
+    if (!v || n_tokens < 0 || (!tokens && n_tokens > 0)) return INT32_MIN;
+    int32_t b = 0, e = n_tokens;
+    if (remove_special && e > b && v->tok->add_bos && tokens[b] == v->tok->bos) ++b;
+    if (remove_special && e > b && tokens[e - 1] == v->tok->eos) --e;
+    std::string out;
+    for (int32_t i = b; i < e; ++i) out += v->tok->piece(tokens[i], unparse_special);
+    if ((int64_t)out.size() > (int64_t)text_len_max) return -(int32_t)out.size();
+    if (!out.empty()) memcpy(text, out.data(), out.size());
+    return (int32_t)out.size();
+}
+
+// a tokenizer-only handle from a GGUF's metadata (no tensors needed)
+struct llama_vocab* llmi_vocab_load_from_file(const char* path) {
+    GgufFile f;
+    std::string err;
+    if (!path || !f.open(path, err)) {
+        set_err(err.empty() ? "llmi_vocab_load_from_file: no path" : err);
+        return nullptr;
+    }
+    const GgufTensor* te = f.tensor("token_embd.weight");
+    auto v = std::make_unique<llama_vocab>();
+    v->m = nullptr;
+    v->owned = Tokenizer::from_gguf(f, te ? (int)te->ne[1] : 0);
+    v->tok = v->owned.get();
+    return v.release();
+}
+void llmi_vocab_free(struct llama_vocab* v) {
+    if (v && v->owned) delete v;
 }
 int32_t llama_model_n_embd(const struct llama_model* m) { return m ? m->m.hp.n_embd : 0; }
 int32_t llama_model_n_layer(const struct llama_model* m) { return m ? m->m.hp.n_layer : 0; }

@@ -132,6 +132,7 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
     if (M.vocab.empty()) {
         M.vocab.resize((size_t)hp.n_vocab);
     }
+    M.tok = Tokenizer::from_gguf(f, hp.n_vocab);
     M.layers.resize((size_t)hp.n_layer);
     for (int l = 0; l < hp.n_layer; ++l) {
         Layer& L = M.layers[(size_t)l];
@@ -322,7 +323,7 @@ bool model_clone_layout(const Model& src, int device, Model& dst, std::string& e
     dst.hp = src.hp;
     dst.tok_embd = src.tok_embd; dst.out_norm = src.out_norm; dst.output = src.output;
     dst.layers = src.layers;
-    dst.vocab = src.vocab; dst.bos = src.bos; dst.eos = src.eos;
+    dst.vocab = src.vocab; dst.tok = src.tok; dst.bos = src.bos; dst.eos = src.eos;
     dst.rope_freq_host = src.rope_freq_host; dst.has_rope_freqs = src.has_rope_freqs;
     dst.arena_bytes = src.arena_bytes;
     HIPC(hipSetDevice(device));

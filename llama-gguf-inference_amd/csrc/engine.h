@@ -11,6 +11,7 @@
 #include "common.h"
 #include "gguf.h"
 #include "kernels.h"
+#include "tokenizer.h"
 
 namespace llmi {
 
@@ -36,6 +37,7 @@ struct Model {
     size_t arena_bytes = 0;
     bool owns_arena = true;
     std::vector<std::string> vocab;
+    std::shared_ptr<Tokenizer> tok;      // llama_tokenize / llama_token_to_piece (tokenizer.h)
     int bos = -1, eos = -1;
     std::vector<float> rope_freq_host;  // rope_freqs.weight, if present
     double upload_s = 0;                 // chunked pinned upload + repack time (model_load)

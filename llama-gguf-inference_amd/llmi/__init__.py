@@ -55,6 +55,77 @@ def write_synthetic_gguf(path: str, preset: str, seed: int = 3, n_layer: int = 0
     return int(n)
 
 
+class Vocab:
+    """The native tokenizer (llama_tokenize / llama_token_to_piece / llama_detokenize of
+    the C ABI, csrc/tokenizer.cpp).  From a model (Model.vocab) or, tokenizer only, from
+    any GGUF's metadata (Vocab.from_file)."""
+
+    def __init__(self, handle, owned: bool = False, keep=None):
+        if not handle:
+            raise LlmiError(f"vocab: {last_error()}")
+        self._h, self._owned, self._keep = handle, owned, keep
+
+    @classmethod
+    def from_file(cls, path: str) -> "Vocab":
+        return cls(lib().llmi_vocab_load_from_file(path.encode()), owned=True)
+
+    @property
+    def n_tokens(self) -> int:
+        return lib().llama_vocab_n_tokens(self._h)
+
+    @property
+    def bos(self) -> int:
+        return lib().llama_vocab_bos(self._h)
+
+    @property
+    def eos(self) -> int:
+        return lib().llama_vocab_eos(self._h)
+
+    def tokenize(self, text: str, add_special: bool = True, parse_special: bool = True) -> list[int]:
+        L = lib()
+        b = text.encode("utf-8")
+        cap = len(b) + 8
+        while True:
+            buf = (C.c_int32 * cap)()
+            n = L.llama_tokenize(self._h, b, len(b), buf, cap, add_special, parse_special)
+            if n == -(2 ** 31):
+                raise LlmiError(f"llama_tokenize: {last_error()}")
+            if n >= 0:
+                return list(buf[:n])
+            cap = -n
+
+    def piece(self, tid: int, special: bool = False, lstrip: int = 0) -> bytes:
+        L = lib()
+        buf = C.create_string_buffer(64)
+        n = L.llama_token_to_piece(self._h, int(tid), buf, 64, lstrip, special)
+        if n < 0:
+            buf = C.create_string_buffer(-n)
+            n = L.llama_token_to_piece(self._h, int(tid), buf, -n, lstrip, special)
+        return buf.raw[:n]
+
+    def detokenize(self, ids: Sequence[int], remove_special: bool = False, unparse_special: bool = False) -> bytes:
+        L = lib()
+        arr = (C.c_int32 * max(1, len(ids)))(*ids)
+        cap = 16 * len(ids) + 16
+        buf = C.create_string_buffer(cap)
+        n = L.llama_detokenize(self._h, arr, len(ids), buf, cap, remove_special, unparse_special)
+        if n < 0:
+            buf = C.create_string_buffer(-n)
+            n = L.llama_detokenize(self._h, arr, len(ids), buf, -n, remove_special, unparse_special)
+        return buf.raw[:n]
+
+    def close(self) -> None:
+        if self._owned and self._h:
+            lib().llmi_vocab_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Model:
     """llama_model_load_from_file: GGUF -> HBM arena on `main_gpu`."""
 
@@ -103,6 +174,11 @@ class Model:
         self.size = int(L.llama_model_size(h))
         self.desc = ""
         return self
+
+    @property
+    def vocab(self) -> Vocab:
+        """The model's native tokenizer (owned by the model)."""
+        return Vocab(self._vocab, owned=False, keep=self)
 
     def token_text(self, t: int) -> str:
         s = lib().llama_vocab_get_text(self._vocab, int(t))

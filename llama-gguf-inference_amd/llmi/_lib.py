@@ -74,6 +74,12 @@ SIGNATURES = {
     "llama_vocab_bos": (C.c_int32, [_P]),
     "llama_vocab_eos": (C.c_int32, [_P]),
     "llama_vocab_get_text": (C.c_char_p, [_P, C.c_int32]),
+    "llama_vocab_get_add_bos": (C.c_bool, [_P]),
+    "llama_tokenize": (C.c_int32, [_P, C.c_char_p, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.c_bool, C.c_bool]),
+    "llama_token_to_piece": (C.c_int32, [_P, C.c_int32, C.c_char_p, C.c_int32, C.c_int32, C.c_bool]),
+    "llama_detokenize": (C.c_int32, [_P, C.POINTER(C.c_int32), C.c_int32, C.c_char_p, C.c_int32, C.c_bool, C.c_bool]),
+    "llmi_vocab_load_from_file": (_P, [C.c_char_p]),
+    "llmi_vocab_free": (None, [_P]),
     "llama_model_n_embd": (C.c_int32, [_P]),
     "llama_model_n_layer": (C.c_int32, [_P]),
     "llama_model_n_head": (C.c_int32, [_P]),
