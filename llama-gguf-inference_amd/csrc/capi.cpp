@@ -883,6 +883,7 @@ static Seg seg_at(int32_t type, const void* w, int64_t rows, int64_t cols) {
     s.type = type;
     s.rows = (int)rows;
     s.row0 = 0;
+    s.rgs = dm.rgs;
     return s;
 }
 
@@ -901,7 +902,7 @@ int32_t llmi_repack(int32_t type, const void* raw, void* w, int64_t rows, int64_
     hipError_t e;
     if (needs_repack(type)) {
         e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_h, (uint8_t*)w + dm.off_s,
-                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), cols, nullptr);
+                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), cols, dm.rgs, nullptr);
     } else {
         e = hipMemcpy(w, raw, dm.bytes, hipMemcpyDeviceToDevice);
     }
@@ -1001,7 +1002,7 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     }
     MVArgs a;
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
-    a.nw = nw; a.eps = 1e-5f;
+    a.nw = nw; a.eps = 1e-5f; a.xfirst = (mode & 4) ? 1 : 0;  // mode bit 2: weights issued after x arrives
     if (logits) { a.st = st; a.argmax = &st->key[0][0]; }
     const int epi = logits ? EPI_LOGITS : EPI_STORE;
     // one graph of n_mats launches (one per weight copy), replayed: no host launch cost

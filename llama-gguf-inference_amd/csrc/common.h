@@ -68,9 +68,30 @@ inline size_t tensor_bytes(int t, int64_t rows, int64_t cols) {
     return (size_t)rows * (size_t)(cols / block_elems(t)) * (size_t)block_bytes(t);
 }
 
+// ROW GROUPS.  Rows are stored in groups of RG = 2^rgs consecutive rows; inside a group
+// every part of the A and H planes holds the RG rows back to back, so 16-B piece
+// (row, part p, unit u) of a plane with np parts per unit sits at
+//     (((g np + p) RG + r) U + u) * 16      g = row / RG, r = row % RG
+// (piece_off, mv_device.h).  RG is the matvec's rows per task at this width (kernels.hip
+// mv_geometry: Lr = U lanes per row, R = 64 / Lr rows), so one wave load instruction of a
+// task (R rows x U units of part p) reads R * U * 16 = 1 KiB of consecutive bytes, where
+// the plain row-major form (RG = 1) gives R separate runs of U * 16 B.  The S and D planes
+// are row-major per unit, which is already contiguous over a group.
+inline int layout_rgs(int type, int64_t rows, int64_t cols) {
+    if (!(type == T_Q4_K || type == T_Q5_K || type == T_Q6_K || type == T_Q8_0) || cols % 256) return 0;
+    const int64_t U = cols / 256;
+    int64_t lr = ((U < 64 ? U : 64) + 3) & ~(int64_t)3;
+    if (lr < 4) lr = 4;
+    int R = 1, s = 0;
+    while (2 * R * lr <= 64) { R *= 2; ++s; }
+    while (s > 0 && rows % R) { R >>= 1; --s; }
+    return s;
+}
+
 // Placement of one matrix inside the device arena.
 struct DevMat {
     int type = -1;
+    int rgs = 0;                               // log2 of the row group (layout_rgs)
     int64_t rows = 0, cols = 0;
     size_t off_a = 0, off_h = 0, off_s = 0, off_d = 0;  // plane offsets (arena-relative)
     size_t bytes = 0;                          // algorithmic bytes
@@ -80,6 +101,7 @@ struct DevMat {
 inline size_t plan_planes(DevMat& m, size_t base) {
     const size_t nblk = (size_t)m.rows * (size_t)(m.cols / block_elems(m.type));
     m.bytes = tensor_bytes(m.type, m.rows, m.cols);
+    m.rgs = layout_rgs(m.type, m.rows, m.cols);
     m.off_a = align_up(base, 256);
     m.off_h = m.off_s = m.off_d = m.off_a;
     switch (m.type) {

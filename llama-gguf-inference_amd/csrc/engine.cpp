@@ -274,7 +274,8 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
         if (needs_repack(m.type)) {
             const int64_t bpr = m.cols / block_elems(m.type);  // blocks per row
             const size_t row_raw = (size_t)bpr * block_bytes(m.type);
-            const int64_t rows_per = std::max<int64_t>(1, (int64_t)(kChunk / row_raw));
+            // chunks of whole row groups (common.h): a multiple of 64 rows
+            const int64_t rows_per = std::max<int64_t>(64, (int64_t)(kChunk / row_raw) / 64 * 64);
             const size_t pa = m.type == T_Q8_0 ? 32 : 128, ph = m.type == T_Q5_K ? 32 : m.type == T_Q6_K ? 64 : 0,
                          ps = m.type == T_Q8_0 ? 0 : 16, pd = (m.type == T_Q6_K || m.type == T_Q8_0) ? 2 : 0;
             for (int64_t r0 = 0; r0 < m.rows && e == hipSuccess; r0 += rows_per) {
@@ -287,7 +288,7 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
                 e = hipMemcpyAsync(dstage[slot], pin[slot], n, hipMemcpyHostToDevice, us);
                 if (e == hipSuccess)
                     e = launch_repack(m.type, dstage[slot], M.arena + m.off_a + b0 * pa, M.arena + m.off_h + b0 * ph,
-                                      M.arena + m.off_s + b0 * ps, M.arena + m.off_d + b0 * pd, nr * bpr, m.cols, us);
+                                      M.arena + m.off_s + b0 * ps, M.arena + m.off_d + b0 * pd, nr * bpr, m.cols, m.rgs, us);
                 if (e == hipSuccess) e = hipEventRecord(ev[slot], us);
                 used[slot] = true;
                 slot ^= 1;
@@ -501,6 +502,7 @@ Seg seg_of(const Model& m, const DevMat& d, int row0) {
     s.type = d.type;
     s.rows = (int)d.rows;
     s.row0 = row0;
+    s.rgs = d.rgs;
     return s;
 }
 

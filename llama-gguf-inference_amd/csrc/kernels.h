@@ -49,6 +49,7 @@ struct Seg {
     int type = -1;
     int rows = 0;
     int row0 = 0;                // first row of this segment in the launch's output space
+    int rgs = 0;                 // log2 of the row group of the A / H planes (common.h)
 };
 
 struct MVArgs {
@@ -184,7 +185,7 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
-hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, int64_t cols,
+hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, int64_t cols, int rgs,
                          hipStream_t stream);
 // writes the prologue's quantized activation in ggml block form (test hook)
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);

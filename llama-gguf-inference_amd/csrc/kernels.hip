@@ -68,6 +68,17 @@ size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + 
 // every lane's unit terms into the wave's fold buffer F, the fold lanes add them onto
 // their chains; after a row set's last sub-item the row sums (ggml's generic order,
 // mv_device.h) go to the epilogue.  The next sub-item's units are in flight meanwhile.
+#if defined(LLMI_EXP_TRACE)
+// per-wave stamps (tools/mvtrace.py): [block][wave][16] = {entry, prologue done, first
+// sub-item done, exit, -, XCC << 32 | sub-items, x arrived, -, end of sub-items 2..9}
+#define MV_STAMP(I, V)                                                                                    \
+    if (A.trace && (threadIdx.x & 63) == 0)                                                               \
+        A.trace[((size_t)blockIdx.x * kMVWaves + (threadIdx.x >> 6)) * 16 + (I)] = (V);
+#define MV_NOW __builtin_amdgcn_s_memrealtime()
+#else
+#define MV_STAMP(I, V)
+#endif
+
 template <int ACT, bool NORM, int EPI, int T, int NP>
 __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
                                                       int tend) {
@@ -80,6 +91,8 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     const int r = lane / g.lr, ul = lane - r * g.lr;
 
     int task = t0;
+    MV_STAMP(0, MV_NOW)
+    [[maybe_unused]] int nsub_done = 0;
     ProRegs<NORM, NP> R;
     mv_prologue_issue<NORM, NP>(A, R);  // activation loads first ...
     // Single-round launches (every wave owns at most one task: QKV, attn_output) issue
@@ -96,6 +109,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
     mv_prologue_finish<ACT, NORM, NP>(A, L, R);
     __syncthreads();
+    MV_STAMP(1, MV_NOW)
 
     if (pipe) {
         int s = 0;
@@ -121,6 +135,11 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             float tm[9];
             unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
             sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
+#if defined(LLMI_EXP_TRACE)
+            ++nsub_done;
+            if (nsub_done == 1) { MV_STAMP(2, MV_NOW) }
+            else if (nsub_done <= 9) { MV_STAMP(6 + nsub_done, MV_NOW) }
+#endif
             if (!has_next) {
                 task = tn;
                 break;
@@ -135,6 +154,8 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     }
     // remaining tasks of other types (or all tasks if the first was not of type T)
     for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
+    MV_STAMP(3, MV_NOW)
+    MV_STAMP(5, ((unsigned long long)(__builtin_amdgcn_s_getreg(6164) & 15) << 32) | (unsigned)nsub_done)
     return best;
 }
 
@@ -963,13 +984,14 @@ __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
 // One thread per (block, chunk c in 0..3); nbr = blocks (units) per row.
 // ----------------------------------------------------------------------------------
 __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H, uint8_t* S, uint8_t* Dp, int64_t nblk,
-                            int nbr) {
+                            int nbr, int rgs) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t b = gid >> 2;
     const int c = (int)(gid & 3);
     if (b >= nblk) return;
     const int64_t row = b / nbr, u = b % nbr, U = nbr;
-    uint8_t* arow = A + row * U * 128;
+    // piece (row, part p, unit u) at A + piece_off(row, p, u, U, 8, rgs) (common.h ROW GROUPS)
+    auto apiece = [&](int p) { return A + piece_off((uint32_t)row, (uint32_t)p, (uint32_t)u, (uint32_t)U, 8, rgs); };
     // residue order: byte 4m + i of part 2c + k holds chunk elements t = l + 8i (low
     // nibble) and 32 + t (high nibble), l = 4k + m
     if (type == T_Q4_K || type == T_Q5_K) {
@@ -978,12 +1000,12 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
         const uint8_t* qs = x + (type == T_Q4_K ? 16 : 48);
         for (int k = 0; k < 2; ++k)
             for (int m = 0; m < 4; ++m)
-                for (int i = 0; i < 4; ++i) arow[((2 * c + k) * U + u) * 16 + 4 * m + i] = qs[32 * c + 4 * k + m + 8 * i];
+                for (int i = 0; i < 4; ++i) apiece(2 * c + k)[4 * m + i] = qs[32 * c + 4 * k + m + 8 * i];
         if (c == 0)
             for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[i];
         if (type == T_Q5_K) {  // byte i, bit l of the lo word: qh[l + 8i] bit 2c; hi word: bit 2c+1
             const uint8_t* qh = x + 16;
-            uint8_t* h = H + row * U * 32 + ((c >> 1) * U + u) * 16 + 8 * (c & 1);
+            uint8_t* h = H + piece_off((uint32_t)row, (uint32_t)(c >> 1), (uint32_t)u, (uint32_t)U, 2, rgs) + 8 * (c & 1);
             for (int i = 0; i < 4; ++i) {
                 uint8_t lo = 0, hi = 0;
                 for (int l = 0; l < 8; ++l) {
@@ -1009,12 +1031,12 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
             for (int m = 0; m < 4; ++m)
                 for (int i = 0; i < 4; ++i) {
                     const int t = 4 * k + m + 8 * i;
-                    arow[((2 * c + k) * U + u) * 16 + 4 * m + i] =
+                    apiece(2 * c + k)[4 * m + i] =
                         (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
                 }
         // H part c, dword g = 2*hi + k: byte i bits [2m, 2m+1] = (high 2 bits of chunk
         // element 32*hi + 4k + m + 8i) XOR 2, which v_perm turns into the high part of q - 32
-        uint8_t* h = H + row * U * 64 + (c * U + u) * 16;
+        uint8_t* h = H + piece_off((uint32_t)row, (uint32_t)c, (uint32_t)u, (uint32_t)U, 4, rgs);
         for (int g = 0; g < 4; ++g)
             for (int i = 0; i < 4; ++i) {
                 uint8_t v = 0;
@@ -1028,14 +1050,14 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
 }
 
 // Q8_0: one thread per 32-block; unit u = 8 blocks, block b of the unit in parts 2b, 2b+1
-__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nblk, int nb_row) {
+__global__ void k_repack_q80(const uint8_t* raw, uint8_t* A, uint8_t* Dp, int64_t nblk, int nb_row, int rgs) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nblk) return;
     const int64_t row = g / nb_row, bi = g % nb_row, U = nb_row / 8, u = bi >> 3, b = bi & 7;
     const uint8_t* x = raw + g * 34;
-    uint8_t* arow = A + row * U * 256;
     for (int h = 0; h < 2; ++h)
-        for (int i = 0; i < 16; ++i) arow[((2 * b + h) * U + u) * 16 + i] = x[2 + 16 * h + i];
+        for (int i = 0; i < 16; ++i)
+            A[piece_off((uint32_t)row, (uint32_t)(2 * b + h), (uint32_t)u, (uint32_t)U, 16, rgs) + i] = x[2 + 16 * h + i];
     Dp[(row * U + u) * 16 + 2 * b] = x[0];
     Dp[(row * U + u) * 16 + 2 * b + 1] = x[1];
 }
@@ -1480,16 +1502,16 @@ hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream
 }
 
 hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* sp, uint8_t* d, int64_t nblk,
-                         int64_t cols, hipStream_t s) {
+                         int64_t cols, int rgs, hipStream_t s) {
     if (nblk <= 0) return hipSuccess;
     if (cols % 256) return hipErrorInvalidValue;
     if (type == T_Q4_K || type == T_Q5_K || type == T_Q6_K) {
         const int64_t thr = nblk * 4;
         hipLaunchKernelGGL(k_repack_kq, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, type, (const uint8_t*)raw, a,
-                           h, sp, d, nblk, (int)(cols / 256));
+                           h, sp, d, nblk, (int)(cols / 256), rgs);
     } else if (type == T_Q8_0) {
         hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d,
-                           nblk, (int)(cols / 32));
+                           nblk, (int)(cols / 32), rgs);
     } else {
         return hipErrorInvalidValue;
     }

@@ -401,6 +401,14 @@ __host__ __device__ constexpr int unit_hparts() { return T == T_Q6_K ? 4 : T == 
 template <int T>
 __host__ __device__ constexpr uint32_t unit_abytes() { return T == T_Q8_0 ? 256u : 128u; }
 
+// byte offset of 16-B piece (row, part p, unit u) of an A / H plane with np parts per
+// unit, rows in groups of 2^rgs (common.h ROW GROUPS)
+__host__ __device__ __forceinline__ uint32_t piece_off(uint32_t row, uint32_t p, uint32_t u, uint32_t U, uint32_t np,
+                                                       int rgs) {
+    const uint32_t g = row >> rgs, r = row & ((1u << rgs) - 1u);
+    return ((((g * np + p) << rgs) + r) * U + u) * 16u;
+}
+
 template <int T>
 struct UnitW {
     u32x4 q[unit_parts<T>()];   // quant parts
@@ -416,8 +424,8 @@ struct UnitW {
 template <int T>
 __device__ __forceinline__ UnitW<T> load_unit(const Seg& sg, uint32_t row, uint32_t u, uint32_t U) {
     UnitW<T> w;
-    const uint32_t P = U * 16, ru = row * U + u;
-    const uint32_t oa = row * U * unit_abytes<T>() + u * 16;
+    const uint32_t P = (U * 16) << sg.rgs, ru = row * U + u;
+    const uint32_t oa = piece_off(row, 0, u, U, unit_parts<T>(), sg.rgs);
 #pragma unroll
     for (int p = 0; p < unit_parts<T>(); ++p) w.q[p] = ldw(sg.a + oa + (uint32_t)p * P);
     if constexpr (T == T_Q8_0) {
@@ -425,7 +433,7 @@ __device__ __forceinline__ UnitW<T> load_unit(const Seg& sg, uint32_t row, uint3
     } else {
         w.s = ldw(sg.s + ru * 16);
         if constexpr (T == T_Q5_K || T == T_Q6_K) {
-            const uint32_t oh = row * U * (16u * unit_hparts<T>()) + u * 16;
+            const uint32_t oh = piece_off(row, 0, u, U, unit_hparts<T>(), sg.rgs);
 #pragma unroll
             for (int c = 0; c < unit_hparts<T>(); ++c) w.h[c] = ldw(sg.h + oh + (uint32_t)c * P);
         }
@@ -647,6 +655,7 @@ __device__ __forceinline__ Seg pick(const MA& A, int si) {
     s.type = si == 0 ? A.seg[0].type : si == 1 ? A.seg[1].type : A.seg[2].type;
     s.rows = si == 0 ? A.seg[0].rows : si == 1 ? A.seg[1].rows : A.seg[2].rows;
     s.row0 = si == 0 ? A.seg[0].row0 : si == 1 ? A.seg[1].row0 : A.seg[2].row0;
+    s.rgs = si == 0 ? A.seg[0].rgs : si == 1 ? A.seg[1].rgs : A.seg[2].rgs;
     return s;
 }
 
@@ -898,10 +907,10 @@ __device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int 
             // residue order (common.h): element 64c + 32hi + l + 8i of the unit sits in
             // part 2c + l/4, byte 4 (l % 4) + i (low nibble: hi = 0, high nibble: hi = 1)
             const int t = e & 255, c = t >> 6, hi = (t >> 5) & 1, l = t & 7, i = (t & 31) >> 3, k = l >> 2, m = l & 3;
-            const uint8_t qb = w.a[(size_t)row * U * 128 + ((size_t)(2 * c + k) * U + u) * 16 + 4 * m + i];
+            const uint8_t qb = w.a[piece_off(row, 2 * c + k, u, U, 8, w.rgs) + 4 * m + i];
             int q = hi ? (qb >> 4) : (qb & 0xF);
             if (w.type == T_Q6_K) {  // H part c: dword (2*hi + k), byte i, bits 2m: the 2 high bits XOR 2
-                const uint8_t hb = w.h[(size_t)row * U * 64 + ((size_t)c * U + u) * 16 + (2 * hi + k) * 4 + i];
+                const uint8_t hb = w.h[piece_off(row, c, u, U, 4, w.rgs) + (2 * hi + k) * 4 + i];
                 q |= (((hb >> (2 * m)) & 3) ^ 2) << 4;
                 const float d = h2f(*(const uint16_t*)(w.d + ru * 2));
                 const int sc = (int8_t)w.s[ru * 16 + (t >> 4)];
@@ -911,7 +920,7 @@ __device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int 
             int sc, mn;
             scale_min(2 * c + hi, s32[1], s32[2], s32[3], sc, mn);
             if (w.type == T_Q5_K) {  // H part c/2: chunk c's lo / hi word, byte i, bit l
-                const uint8_t hb = w.h[(size_t)row * U * 32 + ((size_t)(c >> 1) * U + u) * 16 + 8 * (c & 1) + 4 * hi + i];
+                const uint8_t hb = w.h[piece_off(row, c >> 1, u, U, 2, w.rgs) + 8 * (c & 1) + 4 * hi + i];
                 q += ((hb >> l) & 1) << 4;
             }
             const float d = h2f(s32[0]), dmin = h2f(s32[0] >> 16);
@@ -920,7 +929,7 @@ __device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int 
         }
         case T_Q8_0: {
             const int t = e & 255;
-            const uint8_t qb = w.a[(size_t)row * U * 256 + ((size_t)(t >> 4) * U + u) * 16 + (t & 15)];
+            const uint8_t qb = w.a[piece_off(row, t >> 4, u, U, 16, w.rgs) + (t & 15)];
             return (float)(int8_t)qb * h2f(*(const uint16_t*)(w.d + ru * 16 + 2 * (t >> 5)));
         }
         default: return 0.f;

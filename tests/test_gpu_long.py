@@ -1,4 +1,4 @@
-"""Long and full-width parity runs against the oracle (device order), through the C ABI
+"""Long and full-width parity runs against the oracle (ggml's generic order), through the C ABI
 and the HTTP front end — the BASELINE.json configs the shorter tests do not reach:
 
 - C1: TinyLlama-1.1B Q8_0 (exact widths, all 22 layers), 16-token greedy decode driven
@@ -13,9 +13,10 @@ and the HTTP front end — the BASELINE.json configs the shorter tests do not re
   limit continues as decode steps, bit-identical;
 - the fault path: a bounded in-kernel wait that gives up makes llama_decode return -6
   instead of NaN logits;
-- the north star's "within 1e-3 of the CPU path" against ggml's GENERIC fp32 order at
-  the 8B / TinyLlama / 70B widths, reported (fraction of steps within 1e-3, worst |d|,
-  first greedy divergence and its top-2 margin) into $LLMI_REPORT_DIR/parity_generic.json.
+- the north star's "within 1e-3 of the CPU path" on the configs' real trajectories (8B:
+  128-token prompt -> 512 steps; 70B widths: 8 -> 128; TinyLlama; Mistral Q5_K_M), asserted
+  bit-identical to the oracle (ggml's generic order) at every step and reported into
+  $LLMI_REPORT_DIR/parity_generic.jsonl.
 """
 from __future__ import annotations
 
@@ -251,47 +252,56 @@ def test_bounded_wait_fault_is_reported(gpu, tiny_models, monkeypatch):
     llmi.Context(m, n_ctx=32).close()
 
 
-# ---- north star tolerance against ggml's generic fp32 order (reported) ----------------
-@pytest.mark.parametrize("preset,n_vocab", [("llama3-8b-q4km", 0), ("tinyllama-q8_0", 0), ("llama3-70b-q4km", 32000)])
-def test_generic_order_tolerance_report(gpu, synth_dir, preset, n_vocab):
-    """GPU logits vs the oracle in ggml's GENERIC fp32 order (the restatement of the
-    reference's CPU numerics; the GPU is bit-identical to the DEVICE order): per step
-    max |d|; reported, with loose sanity bounds only (the drift is activation-requant
-    flips)."""
-    path = str(synth_dir / f"{preset}-L2-rep.gguf")
+# ---- north star: the configs' real trajectories against ggml's generic fp32 order ------
+# (BASELINE.json north_star: "within 1e-3 of the NGL=0 path ... bit-exact token ids"; the
+# oracle restates ggml's generic scalar order, SURVEY.md §8c, and the GPU computes in that
+# order, so the bar asserted here is stricter: bit-identical logits at every step.)
+@pytest.mark.parametrize("preset,n_vocab,n_prompt,n_gen", [
+    ("llama3-8b-q4km", 0, 128, 512),      # C2: 128-token prompt -> 512-token decode (ctx 640)
+    ("llama3-70b-q4km", 32000, 8, 128),   # C5 widths (8192 / 28672 / GQA 8), decode-only
+    ("tinyllama-q8_0", 0, 16, 128),       # C1 widths
+    ("mistral7b-q5km", 0, 64, 64),        # C4 widths, mixed Q5_K / Q6_K table
+])
+def test_generic_order_trajectory(gpu, synth_dir, preset, n_vocab, n_prompt, n_gen):
+    """Prompt through the batched prefill, then n_gen greedy steps, in lockstep with the
+    oracle: logits bit-identical at every step (so every step is within 1e-3) and the
+    same greedy ids.  2 layers at the preset's exact widths; reported into
+    $LLMI_REPORT_DIR/parity_generic.jsonl."""
+    path = str(synth_dir / f"{preset}-L2-v{n_vocab}.gguf")
     if not os.path.exists(path):
         llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=2, n_vocab=n_vocab)
     rng = np.random.default_rng(21)
-    prompt = [1] + [int(t) for t in rng.integers(3, 30000, 7)]
-    n_gen = 12
-    om = po.OracleModel(path, n_ctx=64)
+    prompt = [1] + [int(t) for t in rng.integers(3, 30000, n_prompt - 1)]
+    n_ctx = (n_prompt + n_gen + 255) // 256 * 256
+    om = po.OracleModel(path, n_ctx=n_ctx)
     m = llmi.Model(path)
-    c = llmi.Context(m, n_ctx=64)
-    diffs, margins, first_div = [], [], None
-    cur_g = cur_o = prompt[0]
-    for step in range(len(prompt) + n_gen - 1):
-        lo = om.decode(cur_o, step)
-        assert c.decode([cur_g], pos=[step]) == 0
+    c = llmi.Context(m, n_ctx=n_ctx)
+    if len(prompt) > 1:
+        om.prefill(prompt[:-1])
+    lo = om.decode(prompt[-1], len(prompt) - 1)
+    assert c.decode(prompt) == 0
+    lg = c.logits(-1)
+    diffs, pos = [], len(prompt)
+    for step in range(n_gen + 1):
+        d = float(np.abs(lg - lo).max())
+        diffs.append(d)
+        assert np.array_equal(lg, lo), f"{preset} step {step} (pos {pos - 1}): max |d| {d:.3g}"
+        if step == n_gen:
+            break
+        t = int(np.argmax(lo))
+        assert c.greedy(-1) == t
+        lo = om.decode(t, pos)
+        assert c.decode([t], pos=[pos]) == 0
         lg = c.logits(-1)
-        diffs.append(float(np.abs(lg - lo).max()))
-        srt = np.sort(lo)
-        margins.append(float(srt[-1] - srt[-2]))
-        if step + 1 < len(prompt):
-            cur_g = cur_o = prompt[step + 1]
-        else:
-            cur_g, cur_o = int(np.argmax(lg)), int(np.argmax(lo))
-            if cur_g != cur_o and first_div is None:
-                first_div = {"step": step, "gpu": cur_g, "oracle": cur_o, "top2_margin": margins[-1]}
-            cur_g = cur_o  # follow the oracle's sequence so every step compares the same context
+        pos += 1
     om.close()
-    within = float(np.mean(np.array(diffs) <= 1e-3))
-    rep = {"preset": preset, "n_layer": 2, "steps": len(diffs), "frac_within_1e-3": within,
-           "worst_abs_diff": max(diffs), "median_abs_diff": float(np.median(diffs)),
-           "first_greedy_divergence": first_div, "min_top2_margin": min(margins)}
+    c.close()
+    rep = {"preset": preset, "n_layer": 2, "n_vocab": n_vocab or "full", "prompt": n_prompt,
+           "steps": len(diffs), "ctx_end": pos, "frac_within_1e-3": float(np.mean(np.array(diffs) <= 1e-3)),
+           "worst_abs_diff": max(diffs), "bit_identical": True}
     print(json.dumps(rep))
     out_dir = os.environ.get("LLMI_REPORT_DIR")
     if out_dir:
         os.makedirs(out_dir, exist_ok=True)
         with open(os.path.join(out_dir, "parity_generic.jsonl"), "a") as f:
             f.write(json.dumps(rep) + "\n")
-    assert max(diffs) < 1.0  # sanity: an O(1) error would be a bug, not association

@@ -45,7 +45,9 @@ for qt, rows, cols in shapes:
     tgt = (n - 2) if hot else (n - 1)
     tr = torch.zeros(2048 * 16 * 8, dtype=torch.int64, device="cuda")
     g = L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * tgt), rows, cols, P(x), P(y), 0, P(tr))
-    t = tr.cpu().numpy().reshape(-1, 8)
+    t = tr.cpu().numpy().reshape(-1, 16)
+    if os.environ.get("MV_DUMP"):
+        np.save(os.path.join(os.environ["MV_DUMP"], f"trace_{qt}_{rows}x{cols}.npy"), t)
     t = t[t[:, 0] != 0].astype(np.int64)
     t0 = t[:, 0].min()
     start, pro, first, end = t[:, 0] - t0, t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t0
@@ -54,13 +56,16 @@ for qt, rows, cols in shapes:
           f"({lb / (end.max() * 10e-9) / 1e9:.0f} GB/s over the wave span)")
     print("  start offset us :", pct(start))
     print("  prologue us     :", pct(pro))
-    if (t[:, 6] != 0).any():
-        print("    x arrived     :", pct(t[:, 6] - t[:, 0]))
-        print("    quantized     :", pct(t[:, 7] - t[:, 6]))
-        print("    barrier wait  :", pct(t[:, 1] - t[:, 7]))
-    print("  first pair us   :", pct(first[items > 0]))
+    print("  first sub us    :", pct(first[items > 0]))
+    prev = t[:, 2]
+    for k in range(2, 10):  # steady state: end of sub-item k - end of sub-item k-1
+        m = (items >= k)
+        if not m.any():
+            break
+        print(f"  sub {k} us       :", pct((t[m, 6 + k] - prev[m])))
+        prev = np.where(items >= k, t[:, 6 + k], prev)
     print("  exit offset us  :", pct(end))
-    print("  pairs per wave  :", np.bincount(items).tolist())
+    print("  subs per wave   :", np.bincount(items).tolist())
     xcc = (t[:, 5] >> 32) & 0xff
     for xc in range(8):
         m = xcc == xc
