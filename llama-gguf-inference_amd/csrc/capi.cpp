@@ -990,7 +990,7 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     const int mb = std::max(64, prop.multiProcessorCount * wg_per_cu());
     float* nw = nullptr;
     StepState* st = nullptr;
-    const bool norm = mode & 1, logits = mode & 2;
+    const bool norm = mode & 1, logits = mode & 2, img = mode & 8;
     if (norm) {
         std::vector<float> ones((size_t)cols, 1.0f);
         if (hipMalloc(&nw, (size_t)cols * 4) != hipSuccess) { set_err("out of device memory"); return -1.0; }
@@ -1003,7 +1003,14 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     MVArgs a;
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
     a.nw = nw; a.eps = 1e-5f; a.xfirst = (mode & 4) ? 1 : 0;  // mode bit 2: weights issued after x arrives
+    if (mode & 16) a.prio_alt = prop.multiProcessorCount;  // mode bit 4 (experiment builds): alternating priority
     if (logits) { a.st = st; a.argmax = &st->key[0][0]; }
+    uint8_t* xq = nullptr;  // mode bit 3: timing with a pre-quantized activation image (zeros)
+    if (img) {
+        if (hipMalloc(&xq, (size_t)(cols / 256) * 304) != hipSuccess) { set_err("out of device memory"); return -1.0; }
+        (void)hipMemset(xq, 0, (size_t)(cols / 256) * 304);
+        a.xq = xq;
+    }
     const int epi = logits ? EPI_LOGITS : EPI_STORE;
     // one graph of n_mats launches (one per weight copy), replayed: no host launch cost
     hipStream_t s = nullptr;
@@ -1039,6 +1046,7 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     (void)hipStreamDestroy(s);
     (void)hipFree(nw);
     (void)hipFree(st);
+    (void)hipFree(xq);
     return res;
 }
 
@@ -1182,8 +1190,14 @@ int32_t llmi_trace_matvec(int32_t type, const void* w, int64_t rows, int64_t col
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
     a.seg[0] = seg_at(type, w, rows, cols);
     a.trace = (unsigned long long*)trace_dev;
-    (void)mode;
-    if (launch_matvec(a, EPI_STORE, mb, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    uint8_t* xq = nullptr;  // mode bit 3: pre-quantized activation image (zeros)
+    if ((mode & 8) && hipMalloc(&xq, (size_t)(cols / 256) * 304) == hipSuccess) {
+        (void)hipMemset(xq, 0, (size_t)(cols / 256) * 304);
+        a.xq = xq;
+    }
+    const bool ok = launch_matvec(a, EPI_STORE, mb, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    (void)hipFree(xq);
+    if (!ok) {
         set_err("llmi_trace_matvec: launch failed");
         return -1;
     }

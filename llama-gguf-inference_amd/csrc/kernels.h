@@ -59,6 +59,9 @@ struct MVArgs {
     int npairs = 0;              // row pairs (SWIGLU: gate/up pairs) — sizes the launch
     const float* x = nullptr;    // f32[cols] input
     const float* nw = nullptr;   // RMSNorm weight (nullptr: quantize x as is)
+    const uint8_t* xq = nullptr; // pre-quantized activation image [cols/256][kRec] (mv_device.h):
+                                 // when set, the prologue copies it into LDS instead of
+                                 // normalising and quantizing x
     float eps = 0.f;
     float* y = nullptr;          // STORE/ADD/LOGITS: f32[rows]; SWIGLU: h; QKV: q
     // QKV epilogue: RoPE + f16 KV-cache write
@@ -76,6 +79,7 @@ struct MVArgs {
     int split_tasks = 0;                   // two-type launches: tasks of the first type group ...
     int split_wgs = 0;                     // ... and the workgroups that run them
     int xfirst = 0;                        // experiment: multi-round launches also wait for x before weights
+    int prio_alt = 0;                      // experiment builds: alternate s_setprio per sub-item (blocks >= prio_alt: other phase)
     // batched decode (batch.hip, k_mvn): token t of the batch is one decode step of
     // sequence tseq[t] at position tpos[t]; x / y rows are x_stride / y_stride floats
     // apart; the sequence's KV cache is kv_stride elements past the first one; LOGITS

@@ -79,6 +79,9 @@ size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + 
 #define MV_STAMP(I, V)
 #endif
 
+#ifndef LLMI_MV_DIST2
+#define LLMI_MV_DIST2 0
+#endif
 template <int ACT, bool NORM, int EPI, int T, int NP>
 __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
                                                       int tend) {
@@ -92,9 +95,12 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
 
     int task = t0;
     MV_STAMP(0, MV_NOW)
-    [[maybe_unused]] int nsub_done = 0;
+    [[maybe_unused]] int nsub_done = 0, nsub_alt = 0;
     ProRegs<NORM, NP> R;
-    mv_prologue_issue<NORM, NP>(A, R);  // activation loads first ...
+    ImgRegs<2 * NP + 1> RI;
+    const bool img = A.xq != nullptr;
+    if (img) mv_img_issue<2 * NP + 1>(A, RI);  // activation loads first ...
+    else mv_prologue_issue<NORM, NP>(A, R);
     // Single-round launches (every wave owns at most one task: QKV, attn_output) issue
     // their weights only once the activation has arrived: the activation loads then do
     // not queue behind the chip-wide weight burst, and the weight latency overlaps the
@@ -106,11 +112,68 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     LaneUnit lu = lane_unit(g, b, sg, r, ul);
     // ... then the first units, in flight during the prologue (issued on every path: an
     // idle wave re-reads row 0, so the prologue's first wait counts only the activation)
+    // (prefetch distance 2 -- three rotating register buffers in a 3x unrolled loop --
+    // measured slower on every shape: gate+up 16.9 -> 21.2 us, 516 -> 433 tok/s)
     UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
-    mv_prologue_finish<ACT, NORM, NP>(A, L, R);
+    if (img) mv_img_finish<2 * NP + 1>(A, L, RI);
+    else mv_prologue_finish<ACT, NORM, NP>(A, L, R);
     __syncthreads();
     MV_STAMP(1, MV_NOW)
 
+#if LLMI_MV_DIST2
+    // Ping-pong: two register buffers alternate through a 2x unrolled loop, so a unit's
+    // registers are never copied (the `cur = nxt` copy of the plain loop waits for the
+    // prefetch, vmcnt(0), before the next one is issued).  Sub-item descriptors are
+    // slim (segment by index); an invalid one (past the wave's last pipelined sub-item)
+    // keeps a valid address (loads stay unconditional) and the next task index.
+    struct SubRef {
+        int task, s, valid;
+        Sub b;
+        LaneUnit lu;
+    };
+    auto make = [&](int tk, int sj, bool v) {
+        SubRef c;
+        c.task = tk;
+        c.s = sj;
+        c.valid = v;
+        c.b = sub_of<EPI>(A, g, tk < tend ? tk : tend - 1, v ? sj : 0);
+        c.lu = lane_unit(g, c.b, pick(A, c.b.si), r, ul);
+        return c;
+    };
+    auto advance = [&](const SubRef& c) {
+        if (!c.valid) return c;
+        if (c.s + 1 < S) return make(c.task, c.s + 1, true);
+        const int tn = c.task + G;
+        if (tn < tend && task_is<EPI, T>(A, g, tn)) return make(tn, 0, true);
+        SubRef x = c;
+        x.task = tn;
+        x.valid = 0;
+        return x;
+    };
+    auto issue = [&](const SubRef& c) { return load_unit<T>(pick(A, c.b.si), c.lu.row, c.lu.u, g.U); };
+    if (pipe) {
+        float acc = 0.f, vg = 0.f;
+        auto process = [&](const UnitW<T>& w, const SubRef& c) {
+            float tm[9];
+            unit_terms<T>(w, L.act + (size_t)c.lu.u * kRec, tm);
+            sub_finish<ACT, EPI>(A, F, g, c.s, c.b, pick(A, c.b.si), tm, c.lu, r, ul, acc, vg, pos, best);
+        };
+        SubRef d0 = make(task, 0, true);
+        SubRef d1 = advance(d0);
+        UnitW<T> w0 = cur;
+        UnitW<T> w1 = issue(d1);
+        for (;;) {
+            process(w0, d0);
+            if (!d1.valid) { task = d1.task; break; }
+            d0 = advance(d1);
+            w0 = issue(d0);
+            process(w1, d1);
+            if (!d0.valid) { task = d0.task; break; }
+            d1 = advance(d0);
+            w1 = issue(d1);
+        }
+    }
+#else
     if (pipe) {
         int s = 0;
         float acc = 0.f, vg = 0.f;
@@ -132,6 +195,15 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
             // always issue the prefetch (a valid re-load of the current unit if none)
             const UnitW<T> nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
+#if defined(LLMI_EXPERIMENTS)
+            // experiment: alternate the wave priority per sub-item, opposite phases for the
+            // first and second dispatch round of workgroups (co-resident pairs), so that
+            // neither workgroup of a CU loses every VALU arbitration to the older one
+            if (A.prio_alt) {
+                if (((nsub_alt++) + ((int)blockIdx.x >= A.prio_alt ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
             float tm[9];
             unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
             sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
@@ -152,6 +224,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             lu = lun;
         }
     }
+#endif
     // remaining tasks of other types (or all tasks if the first was not of type T)
     for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
     MV_STAMP(3, MV_NOW)

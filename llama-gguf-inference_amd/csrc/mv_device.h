@@ -349,6 +349,27 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
         quant_sub<ACT>(L, cols, sb, v);
     }
 }
+// Pre-quantized activation (MVArgs::xq): the LDS image is copied from global memory.
+// NI 16-B pieces per thread, loaded unconditionally (clamped) like the x loads above.
+template <int NI>
+struct ImgRegs {
+    u32x4 v[NI];
+};
+template <int NI, int NT = kMVThreads>
+__device__ __forceinline__ void mv_img_issue(const MVArgs& A, ImgRegs<NI>& R) {
+    const int n16 = (A.cols >> 8) * (kRec / 16);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) R.v[i] = *(const u32x4*)(A.xq + 16 * min((int)threadIdx.x + i * NT, n16 - 1));
+}
+template <int NI, int NT = kMVThreads>
+__device__ __forceinline__ void mv_img_finish(const MVArgs& A, const Lds& L, const ImgRegs<NI>& R) {
+    const int n16 = (A.cols >> 8) * (kRec / 16);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+        if ((int)threadIdx.x + i * NT < n16) ((u32x4*)L.act)[threadIdx.x + i * NT] = R.v[i];
+    for (int i = (int)threadIdx.x + NI * NT; i < n16; i += NT) ((u32x4*)L.act)[i] = *(const u32x4*)(A.xq + 16 * i);
+}
+
 template <int ACT, bool NORM>
 __device__ __forceinline__ void mv_prologue(const MVArgs& A, const Lds& L) {
     ProRegs<NORM, 1> R;

@@ -41,10 +41,10 @@ for qt, rows, cols in shapes:
     y = torch.empty(rows, device="cuda")
     hot = os.environ.get("MV_HOT") == "1"  # trace a copy just read by the previous launch
     for k in range(n - 1):  # warm code / TLB, leave copy n-1 cold
-        L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * k), rows, cols, P(x), P(y), 0, None)
+        L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * k), rows, cols, P(x), P(y), int(os.environ.get("MV_MODE", "0")), None)
     tgt = (n - 2) if hot else (n - 1)
     tr = torch.zeros(2048 * 16 * 8, dtype=torch.int64, device="cuda")
-    g = L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * tgt), rows, cols, P(x), P(y), 0, P(tr))
+    g = L.llmi_trace_matvec(qt, C.c_void_p(w.data_ptr() + stride * tgt), rows, cols, P(x), P(y), int(os.environ.get("MV_MODE", "0")), P(tr))
     t = tr.cpu().numpy().reshape(-1, 16)
     if os.environ.get("MV_DUMP"):
         np.save(os.path.join(os.environ["MV_DUMP"], f"trace_{qt}_{rows}x{cols}.npy"), t)
