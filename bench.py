@@ -50,7 +50,7 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--model-dir", default=os.environ.get("LLMI_BENCH_DIR", "/tmp/llmi_bench"))
     ap.add_argument("--profile-steps", type=int, default=20)
-    ap.add_argument("--cpu-sample-tokens", type=int, default=6)
+    ap.add_argument("--cpu-sample-tokens", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--batch-seqs", default="2,4,8",
                     help="continuous-batching leg: sequence counts to time (comma list, '' to skip)")
@@ -273,13 +273,15 @@ def log(msg):
 
 
 def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
-    """The reference's CPU path (NGL=0) restated — the oracle, oracle/ — timed on this
-    host: the -O3 -march=x86-64-v3 build (bit-identical to the -O2 parity build), ggml's
-    generic fp32 order (the reference's numerics), one thread per physical core up to the
-    box's CPU share (16).  Workload: the same 128-token prompt (its KV rows filled by the
-    oracle's batched prefill, untimed), then n_tokens timed greedy decode steps at
-    context 128+ — a bounded sample of the GPU run's decode.  Beside it the host DRAM
-    streaming-read rate and the decode roofline it implies (bytes/token / host GB/s)."""
+    """The reference's CPU path (NGL=0: llama.cpp built for the host, Dockerfile.cpu:84-89)
+    restated — oracle/, test infrastructure — timed on this host: the -O3
+    -march=x86-64-v3 build with its AVX2 dot products (the x86 kernels' maddubs/madd
+    structure and 8-lane fp32 block accumulation; or_set_fast_dots), one OpenMP thread per
+    physical core up to the box's CPU share (16).  Workload: the same 128-token prompt (its
+    KV rows filled by decode steps without logits, untimed), then n_tokens timed greedy
+    decode steps at context 128+ — a bounded sample of the GPU run's decode.  Beside it the
+    host DRAM streaming-read rate and the decode roofline it implies, and the scalar
+    generic-order restatement's rate (the parity checker, 2 steps)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
@@ -288,17 +290,28 @@ def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
     po.prefer_simd()
     phys = po.physical_cores()
     threads = max(1, min(phys, 16))
-    om = po.OracleModel(path, n_ctx=len(prompt) + n_tokens + 2, threads=threads)
-    t = time.perf_counter()
-    om.prefill(prompt[:-1])  # the batched path fills the KV rows (untimed)
-    fill_s = time.perf_counter() - t
-    lg = om.decode(prompt[-1], len(prompt) - 1)  # first step (page-in), untimed
-    tok = int(np.argmax(lg))
-    t0 = time.perf_counter()
-    for k in range(n_tokens):
-        lg = om.decode(tok, len(prompt) + k)
+    fast = po.set_fast_dots(True)
+    om = po.OracleModel(path, n_ctx=len(prompt) + n_tokens + 4, threads=threads)
+    try:
+        t = time.perf_counter()
+        for i, tk in enumerate(prompt[:-1]):  # KV rows of the prompt (untimed)
+            om.decode(tk, i, logits=False)
+        fill_s = time.perf_counter() - t
+        lg = om.decode(prompt[-1], len(prompt) - 1)  # first step (page-in), untimed
         tok = int(np.argmax(lg))
-    dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for k in range(n_tokens):
+            lg = om.decode(tok, len(prompt) + k)
+            tok = int(np.argmax(lg))
+        dt = time.perf_counter() - t0
+        # the scalar generic-order restatement (the parity checker) for comparison
+        po.set_fast_dots(False)
+        t1 = time.perf_counter()
+        for k in range(2):
+            om.decode(tok, len(prompt) + n_tokens + k)
+        generic_tok_s = 2 / (time.perf_counter() - t1)
+    finally:
+        po.set_fast_dots(False)
     bpt = om.bytes_per_token(len(prompt) + n_tokens // 2)
     om.close()
     host_gbps = po.host_stream_gbps(1 << 30, 3, threads)
@@ -306,13 +319,14 @@ def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
     return {"value": round(tok_s, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
             "physical_cores": phys,
             "achieved_GBps": round(tok_s * bpt / 1e9, 2),
+            "dots": "avx2 (x86 kernel association)" if fast else "generic scalar (no AVX2 in this build)",
+            "generic_order_tok_s": round(generic_tok_s, 3),
             "host_dram_roofline": {"stream_read_GBps": round(host_gbps, 1),
                                    "decode_tok_s_at_roofline": round(host_gbps * 1e9 / bpt, 2)},
             "sample": f"{n_tokens} greedy decode steps at ctx {len(prompt)}..{len(prompt) + n_tokens - 1} after the "
-                      f"same {len(prompt)}-token prompt (KV filled by the oracle's batched prefill in "
-                      f"{fill_s:.1f}s, untimed) on {os.path.basename(path)}; oracle/ggml_oracle.c "
-                      f"-O3 -march=x86-64-v3, ggml generic fp32 order, OpenMP {threads} threads "
-                      f"({phys} physical cores on the host; 16 = the box's CPU share per GPU)"}
+                      f"same {len(prompt)}-token prompt (KV rows filled by decode steps in {fill_s:.1f}s, untimed) "
+                      f"on {os.path.basename(path)}; oracle/ggml_oracle.c -O3 -march=x86-64-v3 with AVX2 dots, "
+                      f"OpenMP {threads} threads ({phys} physical cores on the host; 16 = the box's CPU share per GPU)"}
 
 
 def env_knobs() -> dict:

@@ -244,7 +244,21 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
     float* F = (float*)(smem + fold_off(ACT, A.cols, kMVWaves)) + wave * kFoldFloats;
     unsigned long long best;
     if constexpr (T2 == T) {
-        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, gridDim.x * kMVWaves, 0, A.ntasks);
+        // single type: optionally two task ranges, the larger one for the first dispatch
+        // round of workgroups (mv_launch: the older of two co-resident workgroups wins
+        // VALU arbitration and runs ~20 % faster per sub-item); one call site either way
+        int t0 = blockIdx.x * kMVWaves + wave, G = gridDim.x * kMVWaves, tb = 0, te = A.ntasks;
+        if (A.split_wgs > 0) {
+            if ((int)blockIdx.x < A.split_wgs) {
+                G = A.split_wgs * kMVWaves;
+                te = A.split_tasks;
+            } else {
+                t0 = A.split_tasks + (blockIdx.x - A.split_wgs) * kMVWaves + wave;
+                G = (gridDim.x - A.split_wgs) * kMVWaves;
+                tb = A.split_tasks;
+            }
+        }
+        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, t0, G, tb, te);
     } else {
         if ((int)blockIdx.x < A.split_wgs)
             best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
@@ -1183,10 +1197,39 @@ static dim3 resident_grid(K kernel, dim3 grid, size_t lds, int threads = kMVThre
     return grid;
 }
 
+// Share of a long single-type launch's tasks given to the first dispatch round of
+// workgroups when two workgroups share each CU (profiles/r03/matvec/old_young_workgroups.json:
+// the older workgroup of a CU retires a sub-item in 3.91 us where the younger takes 4.90
+// on the output head, 2.87 vs 3.40 on gate+up): the first round gets share / (1 + share)
+// of the tasks.  LLMI_MV_OLD_SHARE (A/B; 1 = equal ranges, 0 = off) — which wave reduces
+// a task never changes a result.
+static double old_share() {
+    static const double v = [] {
+        const char* e = getenv("LLMI_MV_OLD_SHARE");
+        return e ? atof(e) : 1.25;
+    }();
+    return v;
+}
 template <int ACT, bool NORM, int T, int EPI, int NP>
-static hipError_t mv_launch(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds, hipStream_t s) {
     auto k = k_matvec<ACT, NORM, EPI, T, NP>;
-    launch_k(k, resident_grid(k, grid, lds), dim3(kMVThreads), lds, s, true, true, a);
+    const dim3 g = resident_grid(k, grid, lds);
+    MVArgs a = a0;
+    a.split_wgs = 0;
+    const double sh = old_share();
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+        return n;
+    }();
+    // long launches only (>= 4 tasks per wave), and only when the grid is exactly two
+    // dispatch rounds of one workgroup per CU
+    if (sh > 0 && cus > 0 && (int)g.x == 2 * cus && a.ntasks >= 4 * (int)g.x * kMVWaves) {
+        a.split_wgs = cus;
+        a.split_tasks = (int)(a.ntasks * (sh / (1.0 + sh)) + 0.5);
+    }
+    launch_k(k, g, dim3(kMVThreads), lds, s, true, true, a);
     return hipGetLastError();
 }
 

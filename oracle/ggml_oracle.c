@@ -428,7 +428,133 @@ static float vd_generic_unpacked(int wtype, int n, const RowConst* rcs, const ui
     return sumf;
 }
 
+/* ---------------- CPU baseline only: AVX2 dot products ----------------
+ * TIMING PATH, NOT THE CHECKER.  The reference's CPU image builds llama.cpp for the host
+ * (Dockerfile.cpu:84-89), whose x86 kernels (ggml-cpu arch/x86 quants.c, upstream, not
+ * vendored) vectorise these dots with AVX2 maddubs/madd and accumulate the per-block
+ * integer sums in 8 fp32 lanes — a different fp32 association from the generic order the
+ * parity checks use.  These are written here in that style (unsigned-weights x signed-q8
+ * maddubs, 16-bit scale madd, one fp32 FMA per block) so bench.py's cpu_baseline times a
+ * vectorised CPU path instead of the scalar restatement.  Results agree with the generic
+ * order to float rounding (tests/test_oracle_fast.py), never bit for bit; or_set_fast_dots
+ * is off by default and no parity test turns it on. */
+static int g_fast = 0;
+#if defined(__AVX2__) && defined(__FMA__)
+#include <immintrin.h>
+static inline float hsum8(__m256 v) {
+    __m128 a = _mm_add_ps(_mm256_castps256_ps128(v), _mm256_extractf128_ps(v, 1));
+    a = _mm_add_ps(a, _mm_movehl_ps(a, a));
+    a = _mm_add_ss(a, _mm_movehdup_ps(a));
+    return _mm_cvtss_f32(a);
+}
+static inline int kq_mins_dot(const int16_t* bsums, const uint8_t* mn) {
+    int s = 0;
+    for (int j = 0; j < 16; ++j) s += bsums[j] * mn[j / 2];
+    return s;
+}
+static float fd_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
+    const __m256i m4 = _mm256_set1_epi8(0x0F);
+    __m256 acc = _mm256_setzero_ps();
+    float accm = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        uint8_t sc[8], mn[8];
+        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
+        __m256i sumi = _mm256_setzero_si256();
+        for (int j = 0; j < 4; ++j) {
+            const __m256i qb = _mm256_loadu_si256((const __m256i*)(x[i].qs + 32 * j));
+            const __m256i lo = _mm256_and_si256(qb, m4), hi = _mm256_and_si256(_mm256_srli_epi16(qb, 4), m4);
+            const __m256i yl = _mm256_loadu_si256((const __m256i*)(y[i].qs + 64 * j));
+            const __m256i yh = _mm256_loadu_si256((const __m256i*)(y[i].qs + 64 * j + 32));
+            const __m256i pl = _mm256_madd_epi16(_mm256_maddubs_epi16(lo, yl), _mm256_set1_epi16(sc[2 * j]));
+            const __m256i ph = _mm256_madd_epi16(_mm256_maddubs_epi16(hi, yh), _mm256_set1_epi16(sc[2 * j + 1]));
+            sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
+        }
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[i].d) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
+        accm += llmi_h2f(x[i].dmin) * y[i].d * (float)kq_mins_dot(y[i].bsums, mn);
+    }
+    return hsum8(acc) - accm;
+}
+static float fd_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
+    const __m256i m4 = _mm256_set1_epi8(0x0F), b16 = _mm256_set1_epi8(0x10);
+    __m256 acc = _mm256_setzero_ps();
+    float accm = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        uint8_t sc[8], mn[8];
+        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
+        const __m256i hb = _mm256_loadu_si256((const __m256i*)x[i].qh);
+        __m256i sumi = _mm256_setzero_si256();
+        for (int j = 0; j < 4; ++j) {
+            const __m256i qb = _mm256_loadu_si256((const __m256i*)(x[i].qs + 32 * j));
+            const __m256i ml = _mm256_set1_epi8((char)(1 << (2 * j))), mh = _mm256_set1_epi8((char)(1 << (2 * j + 1)));
+            const __m256i lo = _mm256_or_si256(_mm256_and_si256(qb, m4),
+                                               _mm256_and_si256(_mm256_cmpeq_epi8(_mm256_and_si256(hb, ml), ml), b16));
+            const __m256i hi = _mm256_or_si256(_mm256_and_si256(_mm256_srli_epi16(qb, 4), m4),
+                                               _mm256_and_si256(_mm256_cmpeq_epi8(_mm256_and_si256(hb, mh), mh), b16));
+            const __m256i yl = _mm256_loadu_si256((const __m256i*)(y[i].qs + 64 * j));
+            const __m256i yh = _mm256_loadu_si256((const __m256i*)(y[i].qs + 64 * j + 32));
+            const __m256i pl = _mm256_madd_epi16(_mm256_maddubs_epi16(lo, yl), _mm256_set1_epi16(sc[2 * j]));
+            const __m256i ph = _mm256_madd_epi16(_mm256_maddubs_epi16(hi, yh), _mm256_set1_epi16(sc[2 * j + 1]));
+            sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
+        }
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[i].d) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
+        accm += llmi_h2f(x[i].dmin) * y[i].d * (float)kq_mins_dot(y[i].bsums, mn);
+    }
+    return hsum8(acc) - accm;
+}
+static float fd_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
+    const __m256i m4 = _mm256_set1_epi8(0x0F), m2 = _mm256_set1_epi8(0x30), k32 = _mm256_set1_epi8(32);
+    __m256 acc = _mm256_setzero_ps();
+    for (int i = 0; i < n / QK_K; ++i) {
+        __m256i sumi = _mm256_setzero_si256();
+        for (int h = 0; h < 2; ++h) {
+            const __m256i l0 = _mm256_loadu_si256((const __m256i*)(x[i].ql + 64 * h));
+            const __m256i l1 = _mm256_loadu_si256((const __m256i*)(x[i].ql + 64 * h + 32));
+            const __m256i qh = _mm256_loadu_si256((const __m256i*)(x[i].qh + 32 * h));
+            __m256i q[4];  /* elements 128h + 32k + l, unsigned 6-bit */
+            q[0] = _mm256_or_si256(_mm256_and_si256(l0, m4), _mm256_and_si256(_mm256_slli_epi16(qh, 4), m2));
+            q[1] = _mm256_or_si256(_mm256_and_si256(l1, m4), _mm256_and_si256(_mm256_slli_epi16(qh, 2), m2));
+            q[2] = _mm256_or_si256(_mm256_and_si256(_mm256_srli_epi16(l0, 4), m4), _mm256_and_si256(qh, m2));
+            q[3] = _mm256_or_si256(_mm256_and_si256(_mm256_srli_epi16(l1, 4), m4), _mm256_and_si256(_mm256_srli_epi16(qh, 2), m2));
+            for (int k = 0; k < 4; ++k) {
+                const int e0 = 128 * h + 32 * k;
+                const __m256i yv = _mm256_loadu_si256((const __m256i*)(y[i].qs + e0));
+                /* (q - 32) * y = q * y - 32 * y: both maddubs in range */
+                const __m256i p = _mm256_sub_epi16(_mm256_maddubs_epi16(q[k], yv), _mm256_maddubs_epi16(k32, yv));
+                const __m256i s = _mm256_set_m128i(_mm_set1_epi16(x[i].scales[e0 / 16 + 1]), _mm_set1_epi16(x[i].scales[e0 / 16]));
+                sumi = _mm256_add_epi32(sumi, _mm256_madd_epi16(p, s));
+            }
+        }
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[i].d) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
+    }
+    return hsum8(acc);
+}
+static float fd_q8_0(int n, const block_q8_0* x, const block_q8_0* y) {
+    __m256 acc = _mm256_setzero_ps();
+    const __m256i ones = _mm256_set1_epi16(1);
+    for (int ib = 0; ib < n / QK8_0; ++ib) {
+        const __m256i a = _mm256_loadu_si256((const __m256i*)x[ib].qs), b = _mm256_loadu_si256((const __m256i*)y[ib].qs);
+        const __m256i p = _mm256_madd_epi16(_mm256_maddubs_epi16(_mm256_sign_epi8(a, a), _mm256_sign_epi8(b, a)), ones);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[ib].d) * llmi_h2f(y[ib].d)), _mm256_cvtepi32_ps(p), acc);
+    }
+    return hsum8(acc);
+}
+int or_set_fast_dots(int on) { g_fast = on ? 1 : 0; return 1; }
+#else
+int or_set_fast_dots(int on) { g_fast = 0; (void)on; return 0; }  /* no AVX2 in this build */
+#endif
+
 float or_vec_dot(int wtype, int n, const void* w, const void* a) {
+#if defined(__AVX2__) && defined(__FMA__)
+    if (g_fast) {
+        switch (wtype) {
+            case OR_Q4_K: return fd_q4_K(n, w, a);
+            case OR_Q5_K: return fd_q5_K(n, w, a);
+            case OR_Q6_K: return fd_q6_K(n, w, a);
+            case OR_Q8_0: return fd_q8_0(n, w, a);
+            default: break;
+        }
+    }
+#endif
     switch (wtype) {
         case OR_Q4_K: return vd_q4_K(n, w, a);
         case OR_Q5_K: return vd_q5_K(n, w, a);

@@ -43,6 +43,9 @@ void or_quantize_row_q8_K(const float* x, void* y, int64_t n);
 void or_quantize_row_q8_0(const float* x, void* y, int64_t n);
 /* ggml_vec_dot_<wtype>_<vec_dot_type>_generic: one weight row against one quantized activation */
 float or_vec_dot(int wtype, int n, const void* wrow, const void* act);
+/* CPU baseline timing only: AVX2 dots in the x86 kernels' association (not the
+ * generic order; never used by a parity check).  Returns 0 if this build has no AVX2. */
+int or_set_fast_dots(int on);
 /* y[r] = vec_dot(W[r], quantize(x)) for r < rows (x is f32[cols]); OpenMP over rows */
 int or_matvec(int wtype, const void* W, int64_t rows, int64_t cols, const float* x, float* y, int nthreads);
 

@@ -38,6 +38,12 @@ def build() -> str:
     return LIB
 
 
+def set_fast_dots(on: bool) -> bool:
+    """CPU-baseline timing only: AVX2 dots in the x86 kernels' association (not the
+    generic order the parity checks use).  False if the loaded build has no AVX2."""
+    return bool(lib().or_set_fast_dots(1 if on else 0))
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
@@ -69,6 +75,7 @@ def lib() -> C.CDLL:
         "or_host_stream_gbps": (C.c_double, [C.c_size_t, C.c_int, C.c_int]),
         "or_tap": (C.c_int, [P, C.c_int, P]),
         "or_bytes_per_token": (C.c_double, [P, C.c_int]),
+        "or_set_fast_dots": (C.c_int, [C.c_int]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)

@@ -1,0 +1,44 @@
+"""The CPU baseline's AVX2 dot products (oracle/ggml_oracle.c or_set_fast_dots — bench.py
+cpu_baseline timing only, never a parity reference) compute the same dot products as the
+generic-order restatement up to fp32 association: relative agreement ~1e-5, not bit
+equality.  Also: the switch is off by default and a no-AVX2 build reports it."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from helpers import Q4_K, Q5_K, Q6_K, Q8_0, random_blocks
+
+
+@pytest.fixture(scope="module")
+def simd():
+    po.prefer_simd()
+    assert po.set_fast_dots(False) in (True, False)
+    yield po.lib()
+    po.set_fast_dots(False)
+
+
+@pytest.mark.parametrize("qt", [Q4_K, Q5_K, Q6_K, Q8_0])
+def test_fast_dots_match_generic(simd, qt):
+    if not po.set_fast_dots(True):
+        pytest.skip("oracle build without AVX2")
+    po.set_fast_dots(False)
+    rng = np.random.default_rng(qt)
+    rows, cols = 64, 4096
+    w = random_blocks(qt, rows, cols, rng)
+    x = rng.standard_normal(cols).astype(np.float32)
+    y0 = np.empty(rows, np.float32)
+    y1 = np.empty(rows, np.float32)
+    P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+    assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y0), 4) == 0
+    assert po.set_fast_dots(True)
+    try:
+        assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y1), 4) == 0
+    finally:
+        po.set_fast_dots(False)
+    scale = np.abs(y0).max()
+    assert np.abs(y1 - y0).max() <= 1e-5 * scale + 1e-6, (np.abs(y1 - y0).max(), scale)
+    # off again: bit-identical to the generic order
+    assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y1), 4) == 0
+    assert np.array_equal(y0, y1)
