@@ -352,7 +352,22 @@ def committed_profile(profile_dir: str, preset: str) -> dict:
     return d if d.get("preset") == preset else {}
 
 
+def dump_maps(tag: str) -> None:
+    """LLMI_DUMP_MAPS=<dir>: this process's address map at a named point (profiler-crash
+    forensics: resolving unsymbolised frames and fault addresses against the mapped
+    objects)."""
+    d = os.environ.get("LLMI_DUMP_MAPS")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    with open("/proc/self/maps") as f, open(os.path.join(d, f"maps_{os.getpid()}_{tag}.txt"), "w") as g:
+        g.write(f.read())
+
+
 def main(argv=None):
+    if os.environ.get("LLMI_DUMP_MAPS"):
+        import faulthandler
+        faulthandler.enable(all_threads=True)
     args = parse(argv)
     knobs = env_knobs()
     dist = Dist(os.environ.get("LLMI_DIST_BACKEND", "nccl"))
@@ -362,7 +377,9 @@ def main(argv=None):
     eng = LlmiEngine(args, dist)
     log(f"rank {dist.rank}: {eng.model.desc} load {eng.load_s:.1f}s fanout {eng.fanout_s:.2f}s prefill "
         f"{args.prompt} tok {eng.prefill_s:.2f}s")
+    dump_maps("before_timed")
     dt, dt_max = timed_decode(eng, dist, args.steps, args.warmup)
+    dump_maps("after_timed")
     tok_s = n * args.steps / dt_max
     # end-to-end roofline: algorithmic bytes of the timed tokens / time (this rank)
     e2e_gbps = eng.bytes / (eng.us * 1e-6) / 1e9 if eng.us > 0 else 0.0

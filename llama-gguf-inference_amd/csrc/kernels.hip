@@ -79,9 +79,6 @@ size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + 
 #define MV_STAMP(I, V)
 #endif
 
-#ifndef LLMI_MV_DIST2
-#define LLMI_MV_DIST2 0
-#endif
 template <int ACT, bool NORM, int EPI, int T, int NP>
 __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
                                                       int tend) {
@@ -120,60 +117,6 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     __syncthreads();
     MV_STAMP(1, MV_NOW)
 
-#if LLMI_MV_DIST2
-    // Ping-pong: two register buffers alternate through a 2x unrolled loop, so a unit's
-    // registers are never copied (the `cur = nxt` copy of the plain loop waits for the
-    // prefetch, vmcnt(0), before the next one is issued).  Sub-item descriptors are
-    // slim (segment by index); an invalid one (past the wave's last pipelined sub-item)
-    // keeps a valid address (loads stay unconditional) and the next task index.
-    struct SubRef {
-        int task, s, valid;
-        Sub b;
-        LaneUnit lu;
-    };
-    auto make = [&](int tk, int sj, bool v) {
-        SubRef c;
-        c.task = tk;
-        c.s = sj;
-        c.valid = v;
-        c.b = sub_of<EPI>(A, g, tk < tend ? tk : tend - 1, v ? sj : 0);
-        c.lu = lane_unit(g, c.b, pick(A, c.b.si), r, ul);
-        return c;
-    };
-    auto advance = [&](const SubRef& c) {
-        if (!c.valid) return c;
-        if (c.s + 1 < S) return make(c.task, c.s + 1, true);
-        const int tn = c.task + G;
-        if (tn < tend && task_is<EPI, T>(A, g, tn)) return make(tn, 0, true);
-        SubRef x = c;
-        x.task = tn;
-        x.valid = 0;
-        return x;
-    };
-    auto issue = [&](const SubRef& c) { return load_unit<T>(pick(A, c.b.si), c.lu.row, c.lu.u, g.U); };
-    if (pipe) {
-        float acc = 0.f, vg = 0.f;
-        auto process = [&](const UnitW<T>& w, const SubRef& c) {
-            float tm[9];
-            unit_terms<T>(w, L.act + (size_t)c.lu.u * kRec, tm);
-            sub_finish<ACT, EPI>(A, F, g, c.s, c.b, pick(A, c.b.si), tm, c.lu, r, ul, acc, vg, pos, best);
-        };
-        SubRef d0 = make(task, 0, true);
-        SubRef d1 = advance(d0);
-        UnitW<T> w0 = cur;
-        UnitW<T> w1 = issue(d1);
-        for (;;) {
-            process(w0, d0);
-            if (!d1.valid) { task = d1.task; break; }
-            d0 = advance(d1);
-            w0 = issue(d0);
-            process(w1, d1);
-            if (!d0.valid) { task = d0.task; break; }
-            d1 = advance(d0);
-            w1 = issue(d1);
-        }
-    }
-#else
     if (pipe) {
         int s = 0;
         float acc = 0.f, vg = 0.f;
@@ -224,7 +167,6 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             lu = lun;
         }
     }
-#endif
     // remaining tasks of other types (or all tasks if the first was not of type T)
     for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
     MV_STAMP(3, MV_NOW)
