@@ -25,14 +25,15 @@ import llmi  # noqa: E402
 from llmi._lib import lib  # noqa: E402
 
 preset = sys.argv[1] if len(sys.argv) > 1 else "llama3-8b-q4km"
-lens = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "128,512,2048").split(",")]
+lens = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "128,512,2048").split(",") if x.strip()]
+GEMM_T = [int(x) for x in os.environ.get("PF_GEMM_T", "128,512").split(",")]
 path = f"/tmp/llmi_bench/{preset}-s3.gguf"
 if not os.path.exists(path):
     os.makedirs(os.path.dirname(path), exist_ok=True)
     llmi.write_synthetic_gguf(path + ".tmp", preset, seed=3)
     os.replace(path + ".tmp", path)
 m = llmi.Model(path)
-n_ctx = (max(lens) + 2 + 255) // 256 * 256
+n_ctx = (max(lens + [1]) + 2 + 255) // 256 * 256
 c = llmi.Context(m, n_ctx=n_ctx)
 rng = np.random.default_rng(4)
 out = {"preset": preset, "prefill_supported": m.prefill_supported, "prompts": {}}
@@ -72,7 +73,7 @@ for (qt, rows, cols) in ((Q4_K, 14336, 4096), (Q4_K, 4096, 14336), (Q6_K, 4096, 
     torch.cuda.synchronize()
     assert L.llmi_repack(qt, C.c_void_p(rd.data_ptr()), C.c_void_p(wd.data_ptr()), rows, cols) == 0
     del rd
-    for T in (128, 512):
+    for T in GEMM_T:
         x = to_dev(r.standard_normal((T, cols)).astype(np.float32))
         y = torch.empty((T, rows), dtype=torch.float32, device="cuda")
         us = C.c_double()
