@@ -13,17 +13,25 @@ from helpers import Q4_K, Q5_K, Q6_K, Q8_0, random_blocks
 
 @pytest.fixture(scope="module")
 def simd():
-    po.prefer_simd()
-    assert po.set_fast_dots(False) in (True, False)
-    yield po.lib()
-    po.set_fast_dots(False)
+    """The AVX2 build loaded on its own (other tests may already hold the generic build
+    as pyoracle's library): or_matvec + or_set_fast_dots of libggml_oracle_simd.so."""
+    import os
+    if not os.path.exists(po.LIB_SIMD):
+        po.build()
+    L = C.CDLL(po.LIB_SIMD)
+    L.or_matvec.restype = C.c_int
+    L.or_matvec.argtypes = [C.c_int, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int]
+    L.or_set_fast_dots.restype = C.c_int
+    L.or_set_fast_dots.argtypes = [C.c_int]
+    yield L
+    L.or_set_fast_dots(0)
 
 
 @pytest.mark.parametrize("qt", [Q4_K, Q5_K, Q6_K, Q8_0])
 def test_fast_dots_match_generic(simd, qt):
-    if not po.set_fast_dots(True):
+    if not simd.or_set_fast_dots(1):
         pytest.skip("oracle build without AVX2")
-    po.set_fast_dots(False)
+    simd.or_set_fast_dots(0)
     rng = np.random.default_rng(qt)
     rows, cols = 64, 4096
     w = random_blocks(qt, rows, cols, rng)
@@ -32,11 +40,11 @@ def test_fast_dots_match_generic(simd, qt):
     y1 = np.empty(rows, np.float32)
     P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
     assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y0), 4) == 0
-    assert po.set_fast_dots(True)
+    assert simd.or_set_fast_dots(1)
     try:
         assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y1), 4) == 0
     finally:
-        po.set_fast_dots(False)
+        simd.or_set_fast_dots(0)
     scale = np.abs(y0).max()
     assert np.abs(y1 - y0).max() <= 1e-5 * scale + 1e-6, (np.abs(y1 - y0).max(), scale)
     # off again: bit-identical to the generic order
