@@ -110,10 +110,9 @@ __device__ __forceinline__ void bprologue(const MVArgs& A, uint8_t* smem, size_t
 }
 
 // the per-token view of the launch's descriptor for the epilogue
-__device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t) {
+__device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t, int seq) {
     MVArgs B = A;
     B.y = A.y + (size_t)t * A.y_stride;
-    const int seq = A.tseq ? A.tseq[t] : 0;
     B.kc = A.kc ? A.kc + (size_t)seq * A.kv_stride : nullptr;
     B.vc = A.vc ? A.vc + (size_t)seq * A.kv_stride : nullptr;
     return B;
@@ -138,6 +137,14 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     for (int t = 0; t < NT; ++t) best[t] = 0;
     bprologue<ACT, NORM, NT>(A, smem, img, red);
 
+    // the tokens' positions and sequences, read once: a global load inside the loop would
+    // wait (in-order vmcnt) behind the weight prefetch every sub-item
+    int tpos[NT], tseq[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        tpos[t] = A.tpos ? A.tpos[t] : 0;
+        tseq[t] = A.tseq ? A.tseq[t] : 0;
+    }
     int task = blockIdx.x * kBW + wave;
     if (task < A.ntasks) {
         int s = 0;
@@ -167,9 +174,8 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
             for (int t = 0; t < NT; ++t) {
                 float tm[9];
                 unit_terms<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, tm);
-                const MVArgs B = token_view(A, t);
-                const int pos = A.tpos ? A.tpos[t] : 0;
-                sub_finish<ACT, EPI>(B, F, g, s, b, sg, tm, lu, r, ul, acc[t], vg[t], pos, best[t]);
+                const MVArgs B = token_view(A, t, tseq[t]);
+                sub_finish<ACT, EPI>(B, F, g, s, b, sg, tm, lu, r, ul, acc[t], vg[t], tpos[t], best[t]);
             }
             if (!has_next) break;
             cur = nxt;
