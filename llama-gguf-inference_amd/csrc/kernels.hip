@@ -26,6 +26,7 @@
 //   k_repack_* one-time load-time layout transforms (common.h).
 #include "kernels.h"
 #include "mv_device.h"
+#include "pf_device.h"
 
 #include <algorithm>
 #include <cstdlib>
