@@ -13,6 +13,7 @@
 // over the batch slots, each slot reading its own sequence's KV cache.
 #include "kernels.h"
 #include "mv_device.h"
+#include "pf_device.h"
 
 #include <cstdlib>
 #include <map>
@@ -252,6 +253,248 @@ __global__ __launch_bounds__(512) void k_battn_pv16(BAttnArgs b, int kvb) {
     attn_pv16_body<D, G>(a, kvb);
 }
 
+
+// ---- the batched matvec on the matrix cores ---------------------------------------------
+// k_bmm: workgroup = one ROW TILE of 16 rows (SWIGLU: 16 gate rows and the same 16 up
+// rows) for all nt <= 8 tokens, kBmW waves; the S unit stages of K are dealt round-robin
+// over the waves (wave w: stages w, w + kBmW, ...).  Per stage a wave forms the exact
+// integer sums of the prefill GEMM (pf_device.h; one v_mfma_f32_16x16x32_f16 per residue
+// l, A = the tokens' q8 fragments from k_pf_quant, B = q * scale) and from them the fp32
+// terms of ggml's generic order, (d_w d_a) aux32[l] and -((dmin_w d_a) sumi), for its
+// (row, token) pairs (C layout: lane = row lane & 15, tokens 4 (lane >> 4) + i; lanes 32..63
+// hold the padding tokens 8..15 and are dropped).  After each round of kBmW stages the
+// terms go through LDS to the fold threads, one per (matrix, chain, lane quad), which add
+// them stage after stage onto their chains — every chain sees the blocks in order, so a
+// token's results equal its single-sequence decode (k_matvec) and the oracle bit for bit.
+// The padded token rows of the MFMA read token 0's fragments (finite, discarded).
+constexpr int kBmW = 8, kBmT = kBmW * 64;
+
+template <int T, int NW>
+struct BmStage {
+    PfW<T> w[NW];
+    h8 a[8];
+    float da[4];
+    u32x4 bp[4];
+};
+
+template <int T, int NW>
+__device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[NW], const uint8_t* aq,
+                                        const int16_t* abs, const float* ad, int s, int S, int nt) {
+    const int lane = threadIdx.x & 63, n = lane & 15, grp = lane >> 4;
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) st.w[wi] = pf_w_load<T>(rp[wi], s, S);
+    const int tok = n < nt ? n : 0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) st.a[l] = *(const h8*)(aq + pf_aq_off(tok, s, 4 * l + grp, S));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int t = 4 * grp + i, tc = t < nt ? t : 0;
+        st.da[i] = ad[(size_t)tc * S + s];
+        if constexpr (T != T_Q6_K) st.bp[i] = *(const u32x4*)(abs + ((size_t)tc * S + s) * 8);
+    }
+}
+
+// the stage's terms tm[wi][chain][i] (token 4 grp + i, row lane & 15)
+template <int T, int NW>
+__device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[NW][9][4]) {
+    const int lane = threadIdx.x & 63, grp = lane >> 4;
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) {
+        const PfW<T>& w = st.w[wi];
+        h2 slo{}, shi{}, slo_o{}, shi_o{};
+        h2 s6[8], s6o[8];
+        float dw, dmw = 0.f;
+        uint32_t mp[4] = {0u, 0u, 0u, 0u};
+        if constexpr (T == T_Q4_K || T == T_Q5_K) {
+            int sc0, m0, sc1, m1;
+            scale_min(2 * grp, w.hdr.y, w.hdr.z, w.hdr.w, sc0, m0);
+            scale_min(2 * grp + 1, w.hdr.y, w.hdr.z, w.hdr.w, sc1, m1);
+            slo = h2{(_Float16)(float)sc0, (_Float16)(float)sc0};
+            shi = h2{(_Float16)(float)sc1, (_Float16)(float)sc1};
+            slo_o = slo * h2{(_Float16)1024.f, (_Float16)1024.f};
+            shi_o = shi * h2{(_Float16)1024.f, (_Float16)1024.f};
+            dw = h2f(w.hdr.x);
+            dmw = h2f(w.hdr.x >> 16);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                int a0, b0, a1, b1;
+                scale_min(2 * j, w.hdr.y, w.hdr.z, w.hdr.w, a0, b0);
+                scale_min(2 * j + 1, w.hdr.y, w.hdr.z, w.hdr.w, a1, b1);
+                mp[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+            }
+        } else {  // Q6_K: sc = 16 sh + sl per sub-block 4 grp + k
+            dw = h2f(w.d);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int sc = (int)(int8_t)(w.sc >> (8 * k));
+                const int sh = sc >> 4, sl = sc & 15;
+                const _Float16 fl = (_Float16)(float)sl, fh = (_Float16)(float)sh;
+                s6[2 * k] = h2{fl, fl};
+                s6[2 * k + 1] = h2{fh, fh};
+                s6o[2 * k] = s6[2 * k] * h2{(_Float16)1056.f, (_Float16)1056.f};
+                s6o[2 * k + 1] = s6[2 * k + 1] * h2{(_Float16)1056.f, (_Float16)1056.f};
+            }
+        }
+        float d[4], dm[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            d[i] = dw * st.da[i];
+            dm[i] = dmw * st.da[i];
+        }
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            h8 bf[2];
+            pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf);
+            f4 acc = mfma16(st.a[l], bf[0], f4{0.f, 0.f, 0.f, 0.f});
+            if constexpr (T == T_Q6_K) {
+                const f4 acc_h = mfma16(st.a[l], bf[1], f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = acc_h[i] * 16.f + acc[i];  // exact (< 2^24)
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tm[wi][l][i] = d[i] * acc[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (T != T_Q6_K) {
+                int si = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) si = __builtin_amdgcn_sdot2(as_h2s(mp[j]), as_h2s(st.bp[i][j]), si, false);
+                tm[wi][8][i] = -(dm[i] * (float)si);
+            } else {
+                tm[wi][8][i] = 0.f;
+            }
+        }
+    }
+}
+
+template <int T, int EPI>
+__global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const int16_t* abs, const float* ad, int nt) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;   // weight matrices (SWIGLU: gate, up)
+    constexpr int NC = T == T_Q6_K ? 8 : 9;         // chains per (row, token)
+    constexpr int kBuf = kBmW * NW * 9 * 32;        // float4 per round buffer
+    float4* TmB = (float4*)smem;
+    const int wave = uniform((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const int S = A.cols >> 8;
+    int si = 0, row0;
+    if constexpr (EPI == EPI_SWIGLU) {
+        row0 = blockIdx.x * 16;
+    } else {
+        const int r0 = uniform(A.seg[0].row0), r1 = uniform(A.seg[1].row0), r2 = uniform(A.seg[2].row0);
+        const int q = r0 + blockIdx.x * 16;
+        if (A.nseg > 1 && q >= r1) si = 1;
+        if (A.nseg > 2 && q >= r2) si = 2;
+        row0 = q - (si == 0 ? r0 : si == 1 ? r1 : r2);
+    }
+    RowPtr rp[NW];
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) rp[wi] = row_ptr<T>(pick(A, EPI == EPI_SWIGLU ? wi : si), row0 + (lane & 15), A.cols);
+
+    // fold items (matrix wi, chain c, lane quad L): threads tid and tid + kBmT
+    constexpr int NI = NW * NC * 32;
+    float4 fs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    const int R = (S + kBmW - 1) / kBmW;
+    BmStage<T, NW> cur;
+    bm_load<T, NW>(cur, rp, aq, abs, ad, wave < S ? wave : S - 1, S, nt);
+    for (int rho = 0; rho < R; ++rho) {
+        const int s = rho * kBmW + wave, sn = s + kBmW;
+        BmStage<T, NW> nxt;
+        bm_load<T, NW>(nxt, rp, aq, abs, ad, sn < S ? sn : S - 1, S, nt);  // unconditional
+        float4* Tm = TmB + (rho & 1) * kBuf;
+        if (s < S) {
+            float tm[NW][9][4];
+            bm_terms<T, NW>(cur, tm);
+            if (lane < 32) {
+#pragma unroll
+                for (int wi = 0; wi < NW; ++wi)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c)
+                        Tm[((wave * NW + wi) * 9 + c) * 32 + lane] =
+                            make_float4(tm[wi][c][0], tm[wi][c][1], tm[wi][c][2], tm[wi][c][3]);
+            }
+        }
+        __syncthreads();
+        const int nv = S - rho * kBmW < kBmW ? S - rho * kBmW : kBmW;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int it = threadIdx.x + k * kBmT;
+            if (it < NI) {
+                const int wi = it / (NC * 32), c = (it / 32) % NC, L = it & 31;
+                float4 a = fs[k];
+                for (int w = 0; w < nv; ++w) {
+                    const float4 v = Tm[((w * NW + wi) * 9 + c) * 32 + L];
+                    a.x += v.x;
+                    a.y += v.y;
+                    a.z += v.z;
+                    a.w += v.w;
+                }
+                fs[k] = a;
+            }
+        }
+        cur = nxt;
+    }
+    // chain results into the buffer the last round did not use (its last reads were
+    // before the last round's barrier), then the row values and the epilogue
+    float4* G = TmB + (R & 1) * kBuf;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int it = threadIdx.x + k * kBmT;
+        if (it < NI) {
+            const int wi = it / (NC * 32), c = (it / 32) % NC, L = it & 31;
+            G[(wi * 9 + c) * 32 + L] = fs[k];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const int t = threadIdx.x >> 3, n0 = 2 * (threadIdx.x & 7);
+    unsigned long long best = 0;
+    int seq = 0, pos = 0;
+    if (t < nt) {
+        seq = A.tseq ? A.tseq[t] : 0;
+        pos = A.tpos ? A.tpos[t] : 0;
+        const float* Gf = (const float*)G;
+        float v[NW][2];
+#pragma unroll
+        for (int wi = 0; wi < NW; ++wi)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int L = n0 + h + 16 * (t >> 2), i = t & 3;
+                float x = NC == 9 ? Gf[((wi * 9 + 8) * 32 + L) * 4 + i] : 0.f;  // sumf, then + sums[0..7]
+#pragma unroll
+                for (int l = 0; l < 8; ++l) x += Gf[((wi * 9 + l) * 32 + L) * 4 + i];
+                v[wi][h] = x;
+            }
+        const MVArgs B = token_view(A, t, seq);
+        PairRef ref;
+        ref.sa = ref.sb = pick(A, si);
+        ref.ra = row0 + n0;
+        ref.rb = ref.ra + 1;
+        ref.vb = 1;
+        ref.type = T;
+        if constexpr (EPI == EPI_SWIGLU) {
+            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
+            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
+        } else {
+            epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
+        }
+    }
+    if constexpr (EPI == EPI_LOGITS) {
+        // per token: the max over its 8 threads (consecutive lanes), one atomic into the
+        // slot of its sequence's StepState; tile 0 advances the sequence's next position
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const unsigned long long b = __shfl_xor(best, o);
+            best = b > best ? b : best;
+        }
+        if ((threadIdx.x & 7) == 0 && t < nt) {
+            StepState* st = A.st + seq;
+            if (best) atomicMax(&st->key[pos & 1][blockIdx.x % kArgSlots], best);
+            if (blockIdx.x == 0) st->pos_next = pos + 1;
+        }
+    }
+}
+
 // ---- launchers -----------------------------------------------------------------------------
 size_t mvn_lds_bytes(int act, int cols, int nt) {
     return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * kFoldFloats * 4;
@@ -355,6 +598,69 @@ hipError_t launch_mvn(const MVArgs& a0, int epi, int nt, int max_blocks, hipStre
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// ---- k_bmm launchers -------------------------------------------------------------------
+static int g_bmm_env = getenv("LLMI_BMM") ? atoi(getenv("LLMI_BMM")) : 1;  // 0: k_mvn everywhere (A/B)
+
+// fewest tokens for which the step takes k_bmm (its cost is nearly flat in nt; k_mvn's
+// grows with nt: 8B bench, 2 / 4 / 8 sequences: k_bmm 6.51 / 6.62 / 6.77 ms per step,
+// k_mvn 2.96 / 4.73 / 8.02 ms); LLMI_BMM_MIN overrides (A/B)
+int bmm_min_tokens() {
+    static const int v = getenv("LLMI_BMM_MIN") ? atoi(getenv("LLMI_BMM_MIN")) : 8;
+    return v;
+}
+
+bool bmm_ok(const MVArgs& a, int epi) {
+    if (!g_bmm_env || a.nseg < 1 || a.cols <= 0 || a.cols % 256) return false;
+    const int t = a.seg[0].type;
+    if (!(t == T_Q4_K || t == T_Q5_K || t == T_Q6_K)) return false;
+    if (epi == EPI_SWIGLU && (a.nseg != 2 || a.seg[0].rows != a.seg[1].rows)) return false;
+    for (int i = 0; i < a.nseg; ++i) {
+        if (a.seg[i].type != t || a.seg[i].rows % 16) return false;
+        if (epi != EPI_SWIGLU && i > 0 && a.seg[i].row0 != a.seg[i - 1].row0 + a.seg[i - 1].rows) return false;
+    }
+    return epi == EPI_STORE || epi == EPI_ADD || epi == EPI_QKV || epi == EPI_SWIGLU || epi == EPI_LOGITS;
+}
+
+template <int T, int EPI>
+static hipError_t bmm_launch(const MVArgs& a, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
+    auto k = k_bmm<T, EPI>;
+    constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
+    const size_t lds = (size_t)2 * kBmW * NW * 9 * 32 * 16;
+    static bool attr = false;  // per instantiation
+    if (!attr) {
+        if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    int rows = 0;
+    if (EPI == EPI_SWIGLU) rows = a.seg[0].rows;
+    else
+        for (int i = 0; i < a.nseg; ++i) rows += a.seg[i].rows;
+    hipLaunchKernelGGL(k, dim3(rows / 16), dim3(kBmT), lds, s, a, (const uint8_t*)aq, abs, ad, nt);
+    return hipGetLastError();
+}
+
+template <int T>
+static hipError_t bmm_epi(const MVArgs& a, int epi, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
+    switch (epi) {
+        case EPI_STORE: return bmm_launch<T, EPI_STORE>(a, aq, abs, ad, nt, s);
+        case EPI_ADD: return bmm_launch<T, EPI_ADD>(a, aq, abs, ad, nt, s);
+        case EPI_QKV: return bmm_launch<T, EPI_QKV>(a, aq, abs, ad, nt, s);
+        case EPI_SWIGLU: return bmm_launch<T, EPI_SWIGLU>(a, aq, abs, ad, nt, s);
+        case EPI_LOGITS: return bmm_launch<T, EPI_LOGITS>(a, aq, abs, ad, nt, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const int16_t* abs, const float* ad, hipStream_t s) {
+    if (nt < 1 || nt > kMaxBatch || !bmm_ok(a, epi)) return hipErrorInvalidValue;
+    switch (a.seg[0].type) {
+        case T_Q4_K: return bmm_epi<T_Q4_K>(a, epi, aq, abs, ad, nt, s);
+        case T_Q5_K: return bmm_epi<T_Q5_K>(a, epi, aq, abs, ad, nt, s);
+        case T_Q6_K: return bmm_epi<T_Q6_K>(a, epi, aq, abs, ad, nt, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s) {

@@ -52,7 +52,7 @@ Context::~Context() {
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
     void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad,
-                    bx, bq, batt, bh, blogits, bscores, btpos, btseq};
+                    bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -659,6 +659,11 @@ static bool balloc(Context& c, std::string& err) {
     HIPC(hipMalloc(&c.bscores, B * attn_scratch_floats(hp.n_head, c.n_ctx) * 4));
     HIPC(hipMalloc(&c.btpos, B * 4));
     HIPC(hipMalloc(&c.btseq, B * 4));
+    const size_t maxc = std::max({(size_t)E, QD, F});
+    HIPC(hipMalloc(&c.baq, 32 * maxc * 2));
+    HIPC(hipMalloc(&c.babs, B * (maxc / 16) * 2));
+    HIPC(hipMalloc(&c.bad, B * (maxc / 32) * 4));
+    HIPC(hipMemsetAsync(c.baq, 0, 32 * maxc * 2, c.stream));
     // padded slots read these rows: finite (zeros); their positions 0.  On the context
     // stream (a null-stream memset is not ordered with it: it could land after the slot
     // map upload that follows and point every slot at sequence 0)
@@ -689,8 +694,22 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     BC(launch_bembed(ea, c.stream));
     MVArgs base;
     base.tpos = c.btpos; base.tseq = c.btseq; base.kv_stride = c.kv_seq_elems; base.st = c.st0;
+    // one matvec of the step: k_bmm (matrix cores) after quantizing the nt inputs, where
+    // its segments qualify, else k_mvn; `quantized` skips the quantization for a launch
+    // that reads the same input as the previous one (QKV type groups)
+    bool qkv_quant = false;
+    auto bmv = [&](const MVArgs& a, int epi, bool& quantized) -> hipError_t {
+        if (nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
+        if (!quantized) {
+            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, c.stream);
+            if (e != hipSuccess) return e;
+            quantized = true;
+        }
+        return launch_bmm(a, epi, nt, c.baq, c.babs, c.bad, c.stream);
+    };
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m.layers[(size_t)l];
+        qkv_quant = false;
         // QKV + RoPE + f16 KV write, one launch per run of same-type segments
         const Seg qkv[3] = {seg_of(m, L.wq, 0), seg_of(m, L.wk, QD), seg_of(m, L.wv, QD + nk)};
         for (int i = 0; i < 3;) {
@@ -702,7 +721,7 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
             a.cols = E; a.x = c.bx; a.x_stride = E; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps;
             a.y = c.bq; a.y_stride = QD; a.kc = c.kc0 + l * kv_layer; a.vc = c.vc0 + l * kv_layer; a.rope = c.rope;
             a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = QD; a.nk = nk; a.npairs = rows / 2;
-            BC(launch_mvn(a, EPI_QKV, nt, c.max_blocks, c.stream));
+            BC(bmv(a, EPI_QKV, qkv_quant));
             i = j;
         }
         BAttnArgs ba;
@@ -719,21 +738,21 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
         MVArgs o = base;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = QD; o.x = c.batt; o.x_stride = QD; o.y = c.bx; o.y_stride = E;
         o.npairs = (E + 1) / 2;
-        BC(launch_mvn(o, EPI_ADD, nt, c.max_blocks, c.stream));
+        { bool q = false; BC(bmv(o, EPI_ADD, q)); }
         MVArgs gu = base;
         gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2; gu.cols = E; gu.x = c.bx; gu.x_stride = E;
         gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps; gu.y = c.bh; gu.y_stride = F; gu.npairs = F;
-        BC(launch_mvn(gu, EPI_SWIGLU, nt, c.max_blocks, c.stream));
+        { bool q = false; BC(bmv(gu, EPI_SWIGLU, q)); }
         MVArgs dn = base;
         dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = F; dn.x = c.bh; dn.x_stride = F; dn.y = c.bx; dn.y_stride = E;
         dn.npairs = (E + 1) / 2;
-        BC(launch_mvn(dn, EPI_ADD, nt, c.max_blocks, c.stream));
+        { bool q = false; BC(bmv(dn, EPI_ADD, q)); }
     }
     MVArgs lo = base;
     lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.bx; lo.x_stride = E;
     lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.blogits; lo.y_stride = V;
     lo.npairs = (V + 1) / 2;
-    BC(launch_mvn(lo, EPI_LOGITS, nt, c.max_blocks, c.stream));
+    { bool q = false; BC(bmv(lo, EPI_LOGITS, q)); }
 #undef BC
     return true;
 }

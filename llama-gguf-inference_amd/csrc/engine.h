@@ -101,6 +101,9 @@ struct Context {
     // batched decode (batch.hip): kMaxBatch rows each, allocated on first use
     float *bx = nullptr, *bq = nullptr, *batt = nullptr, *bh = nullptr, *blogits = nullptr, *bscores = nullptr;
     int *btpos = nullptr, *btseq = nullptr;
+    void* baq = nullptr;           // k_bmm: the step's quantized activations (pf_quant layout, 32 token rows)
+    int16_t* babs = nullptr;
+    float* bad = nullptr;
     std::vector<int> btseq_host;            // the slot -> sequence map btseq holds
     std::map<std::string, hipGraphExec_t> bgraphs;  // by (slots, sequences, KV bucket)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -124,6 +124,12 @@ struct BEmbArgs {
 };
 hipError_t launch_bembed(const BEmbArgs& a, hipStream_t s);
 hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s);
+// batched matvec on the matrix cores (batch.hip k_bmm): K-quant segments whose rows are
+// multiples of 16; the nt tokens' activations quantized by launch_pf_quant into (aq,
+// abs, ad) first.  bmm_ok: whether launch_bmm takes these segments (else launch_mvn).
+bool bmm_ok(const MVArgs& a, int epi);
+int bmm_min_tokens();
+hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const int16_t* abs, const float* ad, hipStream_t s);
 hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
                              hipStream_t s);
 size_t mvn_lds_bytes(int act, int cols, int nt);
