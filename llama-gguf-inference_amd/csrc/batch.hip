@@ -279,18 +279,30 @@ struct BmStage {
 
 template <int T, int NW>
 __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[NW], const uint8_t* aq,
-                                        const int16_t* abs, const float* ad, int s, int S, int nt) {
+                                        const int16_t* abs, const float* ad, int s, int S, int nt, int exp = 0) {
     const int lane = threadIdx.x & 63, n = lane & 15, grp = lane >> 4;
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) st.w[wi] = pf_w_load<T>(rp[wi], s, S);
-    const int tok = n < nt ? n : 0;
+    // only the lanes of real tokens load (the padding rows' loads would repeat token 0's
+    // fragments through the TA); the others keep zeros
+    int ntl = nt;
+#if defined(LLMI_EXPERIMENTS)
+    if (exp & 2) ntl = 0;  // experiment: no activation loads
+#endif
 #pragma unroll
-    for (int l = 0; l < 8; ++l) st.a[l] = *(const h8*)(aq + pf_aq_off(tok, s, 4 * l + grp, S));
+    for (int l = 0; l < 8; ++l) {
+        st.a[l] = h8{};
+        if (n < ntl) st.a[l] = *(const h8*)(aq + pf_aq_off(n, s, 4 * l + grp, S));
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int t = 4 * grp + i, tc = t < nt ? t : 0;
-        st.da[i] = ad[(size_t)tc * S + s];
-        if constexpr (T != T_Q6_K) st.bp[i] = *(const u32x4*)(abs + ((size_t)tc * S + s) * 8);
+        const int t = 4 * grp + i;
+        st.da[i] = 0.f;
+        if constexpr (T != T_Q6_K) st.bp[i] = u32x4{0u, 0u, 0u, 0u};
+        if (t < ntl) {
+            st.da[i] = ad[(size_t)t * S + s];
+            if constexpr (T != T_Q6_K) st.bp[i] = *(const u32x4*)(abs + ((size_t)t * S + s) * 8);
+        }
     }
 }
 
@@ -368,42 +380,85 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
     }
 }
 
+// the tile's segment, segment-local row 0 and its lanes' row views (tile = 16 rows of the
+// launch's concatenated segments; SWIGLU: 16 gate rows, the same up rows)
+template <int T, int EPI, int NW>
+__device__ __forceinline__ void bm_tile(const MVArgs& A, int tile, int& si, int& row0, RowPtr (&rp)[NW]) {
+    si = 0;
+    if constexpr (EPI == EPI_SWIGLU) {
+        row0 = tile * 16;
+    } else {
+        const int r0 = uniform(A.seg[0].row0), r1 = uniform(A.seg[1].row0), r2 = uniform(A.seg[2].row0);
+        const int q = r0 + tile * 16;
+        if (A.nseg > 1 && q >= r1) si = 1;
+        if (A.nseg > 2 && q >= r2) si = 2;
+        row0 = q - (si == 0 ? r0 : si == 1 ? r1 : r2);
+    }
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi)
+        rp[wi] = row_ptr<T>(pick(A, EPI == EPI_SWIGLU ? wi : si), row0 + (int)(threadIdx.x & 15), A.cols);
+#if defined(LLMI_EXPERIMENTS)
+    if (A.prio_alt & 1)  // experiment: every lane reads row 0 of the tile (coalesced, L2 hits)
+#pragma unroll
+        for (int wi = 0; wi < NW; ++wi) rp[wi] = row_ptr<T>(pick(A, EPI == EPI_SWIGLU ? wi : si), row0, A.cols);
+#endif
+}
+
+// Persistent: workgroup b runs tiles b, b + grid, ...; one ITERATION = one round of kBmW
+// stages of one tile, the next iteration's loads (next round, or the next tile's first
+// round) issued before this one's terms, so the next tile's weights are in flight during
+// this tile's last fold and epilogue.  LDS: two round buffers of terms (parity of the
+// iteration) and the chain results G of the tile just finished.
 template <int T, int EPI>
-__global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const int16_t* abs, const float* ad, int nt) {
+__global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const int16_t* abs, const float* ad, int nt,
+                                              int ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;   // weight matrices (SWIGLU: gate, up)
     constexpr int NC = T == T_Q6_K ? 8 : 9;         // chains per (row, token)
     constexpr int kBuf = kBmW * NW * 9 * 32;        // float4 per round buffer
     float4* TmB = (float4*)smem;
+    float4* G = TmB + 2 * kBuf;
     const int wave = uniform((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-    const int S = A.cols >> 8;
-    int si = 0, row0;
-    if constexpr (EPI == EPI_SWIGLU) {
-        row0 = blockIdx.x * 16;
-    } else {
-        const int r0 = uniform(A.seg[0].row0), r1 = uniform(A.seg[1].row0), r2 = uniform(A.seg[2].row0);
-        const int q = r0 + blockIdx.x * 16;
-        if (A.nseg > 1 && q >= r1) si = 1;
-        if (A.nseg > 2 && q >= r2) si = 2;
-        row0 = q - (si == 0 ? r0 : si == 1 ? r1 : r2);
-    }
+    const int S = A.cols >> 8, R = (S + kBmW - 1) / kBmW;
+    int tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    int si, row0;
     RowPtr rp[NW];
-#pragma unroll
-    for (int wi = 0; wi < NW; ++wi) rp[wi] = row_ptr<T>(pick(A, EPI == EPI_SWIGLU ? wi : si), row0 + (lane & 15), A.cols);
+    bm_tile<T, EPI, NW>(A, tile, si, row0, rp);
 
     // fold items (matrix wi, chain c, lane quad L): threads tid and tid + kBmT
     constexpr int NI = NW * NC * 32;
     float4 fs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-    const int R = (S + kBmW - 1) / kBmW;
     BmStage<T, NW> cur;
-    bm_load<T, NW>(cur, rp, aq, abs, ad, wave < S ? wave : S - 1, S, nt);
-    for (int rho = 0; rho < R; ++rho) {
-        const int s = rho * kBmW + wave, sn = s + kBmW;
+    bm_load<T, NW>(cur, rp, aq, abs, ad, wave < S ? wave : S - 1, S, nt, A.prio_alt);
+    int rho = 0, it = 0;
+    for (;;) {
+        // the next iteration: (tile, rho + 1) or (tile + grid, 0); its loads now
+        int tn = tile, rn = rho + 1;
+        if (rn == R) {
+            rn = 0;
+            tn = tile + gridDim.x;
+        }
+        const bool has_next = tn < ntiles;
+        int sin, row0n;
+        RowPtr rpn[NW];
+        bm_tile<T, EPI, NW>(A, has_next ? tn : tile, sin, row0n, rpn);  // unconditional (no scratch copies)
+        const int s = rho * kBmW + wave, sn = rn * kBmW + wave;
         BmStage<T, NW> nxt;
-        bm_load<T, NW>(nxt, rp, aq, abs, ad, sn < S ? sn : S - 1, S, nt);  // unconditional
-        float4* Tm = TmB + (rho & 1) * kBuf;
+        bm_load<T, NW>(nxt, rpn, aq, abs, ad, sn < S ? sn : S - 1, S, nt, A.prio_alt);
+        float4* Tm = TmB + (it & 1) * kBuf;
         if (s < S) {
             float tm[NW][9][4];
+#if defined(LLMI_EXPERIMENTS)
+            if (A.prio_alt & 4) {  // experiment: no terms (zeros)
+#pragma unroll
+                for (int wi = 0; wi < NW; ++wi)
+#pragma unroll
+                    for (int c = 0; c < 9; ++c)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) tm[wi][c][i] = cur.da[i] + (float)cur.w[wi].q0[i & 3];
+            } else
+#endif
             bm_terms<T, NW>(cur, tm);
             if (lane < 32) {
 #pragma unroll
@@ -416,11 +471,12 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
         }
         __syncthreads();
         const int nv = S - rho * kBmW < kBmW ? S - rho * kBmW : kBmW;
+        const bool last = rho == R - 1;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            const int it = threadIdx.x + k * kBmT;
-            if (it < NI) {
-                const int wi = it / (NC * 32), c = (it / 32) % NC, L = it & 31;
+            const int f = threadIdx.x + k * kBmT;
+            if (f < NI) {
+                const int wi = f / (NC * 32), c = (f / 32) % NC, L = f & 31;
                 float4 a = fs[k];
                 for (int w = 0; w < nv; ++w) {
                     const float4 v = Tm[((w * NW + wi) * 9 + c) * 32 + L];
@@ -429,69 +485,73 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
                     a.z += v.z;
                     a.w += v.w;
                 }
+                if (last) {  // the tile's chain results; the chains restart for the next tile
+                    G[(wi * 9 + c) * 32 + L] = a;
+                    a = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
                 fs[k] = a;
             }
         }
-        cur = nxt;
-    }
-    // chain results into the buffer the last round did not use (its last reads were
-    // before the last round's barrier), then the row values and the epilogue
-    float4* G = TmB + (R & 1) * kBuf;
+        if (last) {
+            __syncthreads();
+            if (threadIdx.x < 64) {  // wave 0: the row values and the epilogue of the tile
+                const int t = threadIdx.x >> 3, n0 = 2 * (threadIdx.x & 7);
+                unsigned long long best = 0;
+                int seq = 0, pos = 0;
+                if (t < nt) {
+                    seq = A.tseq ? A.tseq[t] : 0;
+                    pos = A.tpos ? A.tpos[t] : 0;
+                    const float* Gf = (const float*)G;
+                    float v[NW][2];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int it = threadIdx.x + k * kBmT;
-        if (it < NI) {
-            const int wi = it / (NC * 32), c = (it / 32) % NC, L = it & 31;
-            G[(wi * 9 + c) * 32 + L] = fs[k];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x >= 64) return;
-    const int t = threadIdx.x >> 3, n0 = 2 * (threadIdx.x & 7);
-    unsigned long long best = 0;
-    int seq = 0, pos = 0;
-    if (t < nt) {
-        seq = A.tseq ? A.tseq[t] : 0;
-        pos = A.tpos ? A.tpos[t] : 0;
-        const float* Gf = (const float*)G;
-        float v[NW][2];
+                    for (int wi = 0; wi < NW; ++wi)
 #pragma unroll
-        for (int wi = 0; wi < NW; ++wi)
+                        for (int h = 0; h < 2; ++h) {
+                            const int L = n0 + h + 16 * (t >> 2), i = t & 3;
+                            float x = NC == 9 ? Gf[((wi * 9 + 8) * 32 + L) * 4 + i] : 0.f;  // sumf, then + sums[0..7]
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int L = n0 + h + 16 * (t >> 2), i = t & 3;
-                float x = NC == 9 ? Gf[((wi * 9 + 8) * 32 + L) * 4 + i] : 0.f;  // sumf, then + sums[0..7]
+                            for (int l = 0; l < 8; ++l) x += Gf[((wi * 9 + l) * 32 + L) * 4 + i];
+                            v[wi][h] = x;
+                        }
+                    const MVArgs B = token_view(A, t, seq);
+                    PairRef ref;
+                    ref.sa = ref.sb = pick(A, si);
+                    ref.ra = row0 + n0;
+                    ref.rb = ref.ra + 1;
+                    ref.vb = 1;
+                    ref.type = T;
+                    if constexpr (EPI == EPI_SWIGLU) {
+                        epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
+                        epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
+                    } else {
+                        epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
+                    }
+                }
+                if constexpr (EPI == EPI_LOGITS) {
+                    // per token: the max over its 8 threads (consecutive lanes), one atomic
+                    // into the slot of its sequence's StepState; tile 0 advances the position
 #pragma unroll
-                for (int l = 0; l < 8; ++l) x += Gf[((wi * 9 + l) * 32 + L) * 4 + i];
-                v[wi][h] = x;
+                    for (int o = 1; o < 8; o <<= 1) {
+                        const unsigned long long bo = __shfl_xor(best, o);
+                        best = bo > best ? bo : best;
+                    }
+                    if ((threadIdx.x & 7) == 0 && t < nt) {
+                        StepState* st = A.st + seq;
+                        if (best) atomicMax(&st->key[pos & 1][tile % kArgSlots], best);
+                        if (tile == 0) st->pos_next = pos + 1;
+                    }
+                }
             }
-        const MVArgs B = token_view(A, t, seq);
-        PairRef ref;
-        ref.sa = ref.sb = pick(A, si);
-        ref.ra = row0 + n0;
-        ref.rb = ref.ra + 1;
-        ref.vb = 1;
-        ref.type = T;
-        if constexpr (EPI == EPI_SWIGLU) {
-            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
-            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
-        } else {
-            epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
         }
-    }
-    if constexpr (EPI == EPI_LOGITS) {
-        // per token: the max over its 8 threads (consecutive lanes), one atomic into the
-        // slot of its sequence's StepState; tile 0 advances the sequence's next position
+        if (!has_next) break;
+        cur = nxt;
+        tile = tn;
+        rho = rn;
+        si = sin;
+        row0 = row0n;
 #pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            const unsigned long long b = __shfl_xor(best, o);
-            best = b > best ? b : best;
-        }
-        if ((threadIdx.x & 7) == 0 && t < nt) {
-            StepState* st = A.st + seq;
-            if (best) atomicMax(&st->key[pos & 1][blockIdx.x % kArgSlots], best);
-            if (blockIdx.x == 0) st->pos_next = pos + 1;
-        }
+        for (int wi = 0; wi < NW; ++wi) rp[wi] = rpn[wi];
+        ++it;
     }
 }
 
@@ -607,8 +667,8 @@ static int g_bmm_env = getenv("LLMI_BMM") ? atoi(getenv("LLMI_BMM")) : 1;  // 0:
 // grows with nt: 8B bench, 2 / 4 / 8 sequences: k_bmm 6.51 / 6.62 / 6.77 ms per step,
 // k_mvn 2.96 / 4.73 / 8.02 ms); LLMI_BMM_MIN overrides (A/B)
 int bmm_min_tokens() {
-    static const int v = getenv("LLMI_BMM_MIN") ? atoi(getenv("LLMI_BMM_MIN")) : 8;
-    return v;
+    const char* e = getenv("LLMI_BMM_MIN");  // read per call (step capture): tests switch it
+    return e ? atoi(e) : 8;
 }
 
 bool bmm_ok(const MVArgs& a, int epi) {
@@ -627,17 +687,29 @@ template <int T, int EPI>
 static hipError_t bmm_launch(const MVArgs& a, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
     auto k = k_bmm<T, EPI>;
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
-    const size_t lds = (size_t)2 * kBmW * NW * 9 * 32 * 16;
-    static bool attr = false;  // per instantiation
-    if (!attr) {
+    const size_t lds = (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
+    static int cap = 0;  // per instantiation: resident workgroups on the device
+    if (!cap) {
         if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+        int occ = 0, cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBmT, lds) != hipSuccess || occ <= 0) occ = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
+        cap = occ * cus;
     }
     int rows = 0;
     if (EPI == EPI_SWIGLU) rows = a.seg[0].rows;
     else
         for (int i = 0; i < a.nseg; ++i) rows += a.seg[i].rows;
-    hipLaunchKernelGGL(k, dim3(rows / 16), dim3(kBmT), lds, s, a, (const uint8_t*)aq, abs, ad, nt);
+    const int ntiles = rows / 16;
+    const int grid = ntiles < cap ? ntiles : cap;
+#if defined(LLMI_EXPERIMENTS)
+    MVArgs ax = a;
+    ax.prio_alt = getenv("LLMI_BMM_EXP") ? atoi(getenv("LLMI_BMM_EXP")) : 0;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, ax, (const uint8_t*)aq, abs, ad, nt, ntiles);
+#else
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, a, (const uint8_t*)aq, abs, ad, nt, ntiles);
+#endif
     return hipGetLastError();
 }
 

@@ -178,6 +178,24 @@ def test_batched_real_widths(gpu, synth_dir, preset, n_vocab):
         assert got[s] == want[s], f"seq {s}"
 
 
+@pytest.mark.parametrize("preset,k", [("llama3-8b-q4km", 2), ("llama3-8b-q4km", 5), ("mistral7b-q5km", 3),
+                                       ("mistral7b-q6k", 8)])
+def test_bmm_any_batch_size(gpu, synth_dir, monkeypatch, preset, k):
+    """The matrix-core batched matvec (batch.hip k_bmm) forced for every batch size
+    (LLMI_BMM_MIN=1; by default it takes 8-token steps): each sequence's tokens and
+    logits equal its single-sequence decode at real widths, Q4_K / Q5_K / Q6_K."""
+    monkeypatch.setenv("LLMI_BMM_MIN", "1")
+    path = str(synth_dir / f"{preset}-batch-L2.gguf")
+    llmi.write_synthetic_gguf(path, preset, seed=11, n_layer=2)
+    rng = np.random.default_rng(5 + k)
+    prompts = _prompts(rng, k, hi=30000, max_len=24)
+    want, want_lg = _single_reference(path, prompts, 10, 256)
+    got, got_lg, _ = _batched(path, prompts, 10, 256, n_seq=k)
+    for s in range(k):
+        assert np.array_equal(got_lg[s], want_lg[s]), f"seq {s}: prompt logits differ"
+        assert got[s] == want[s], f"seq {s}"
+
+
 def test_batched_long_context_gqa8(gpu, synth_dir):
     """TinyLlama shapes (GQA 8) with one sequence past 4096 positions: the batched step's
     attention used to hold 8 heads x kv_bound scores in LDS and refused such batches; it
