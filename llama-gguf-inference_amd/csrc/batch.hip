@@ -310,6 +310,7 @@ __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[N
 template <int T, int NW>
 __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[NW][9][4]) {
     const int lane = threadIdx.x & 63, grp = lane >> 4;
+    const PfK K = pf_consts();
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) {
         const PfW<T>& w = st.w[wi];
@@ -356,7 +357,7 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
             h8 bf[2];
-            pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf);
+            pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf, K);
             f4 acc = mfma16(st.a[l], bf[0], f4{0.f, 0.f, 0.f, 0.f});
             if constexpr (T == T_Q6_K) {
                 const f4 acc_h = mfma16(st.a[l], bf[1], f4{0.f, 0.f, 0.f, 0.f});
