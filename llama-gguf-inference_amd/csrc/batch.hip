@@ -310,7 +310,6 @@ __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[N
 template <int T, int NW>
 __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[NW][9][4]) {
     const int lane = threadIdx.x & 63, grp = lane >> 4;
-    const PfK K = pf_consts();
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) {
         const PfW<T>& w = st.w[wi];
@@ -357,7 +356,7 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
             h8 bf[2];
-            pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf, K);
+            pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf);
             f4 acc = mfma16(st.a[l], bf[0], f4{0.f, 0.f, 0.f, 0.f});
             if constexpr (T == T_Q6_K) {
                 const f4 acc_h = mfma16(st.a[l], bf[1], f4{0.f, 0.f, 0.f, 0.f});
@@ -665,11 +664,12 @@ hipError_t launch_mvn(const MVArgs& a0, int epi, int nt, int max_blocks, hipStre
 static int g_bmm_env = getenv("LLMI_BMM") ? atoi(getenv("LLMI_BMM")) : 1;  // 0: k_mvn everywhere (A/B)
 
 // fewest tokens for which the step takes k_bmm (its cost is nearly flat in nt; k_mvn's
-// grows with nt: 8B bench, 2 / 4 / 8 sequences: k_bmm 6.51 / 6.62 / 6.77 ms per step,
-// k_mvn 2.96 / 4.73 / 8.02 ms); LLMI_BMM_MIN overrides (A/B)
+// grows with nt and pads 5..7 tokens to 8: 8B bench, 2 / 4 / 8 sequences: k_bmm (first
+// form) 6.51 / 6.62 / 6.77 ms per step, persistent 6.27 at 8; k_mvn 2.96 / 4.73 / 8.02
+// ms); LLMI_BMM_MIN overrides (A/B)
 int bmm_min_tokens() {
     const char* e = getenv("LLMI_BMM_MIN");  // read per call (step capture): tests switch it
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 5;
 }
 
 bool bmm_ok(const MVArgs& a, int epi) {

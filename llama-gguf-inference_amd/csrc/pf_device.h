@@ -94,25 +94,9 @@ struct PfB {
     h8 b[NP];  // Q6_K: b[0] = (q-32)*sl, b[1] = (q-32)*sh
 };
 // B fragments of residue l (K-quants) or 32-block l (Q8_0) for this lane
-// a constant held in a VGPR the compiler cannot see through: gfx9 VOP3 takes no literal,
-// so (x & M) | MAGIC with both in registers becomes one v_and_or_b32 instead of two ops
-__device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-struct PfK {
-    uint32_t m4 = 0x000F000Fu, magic = 0x64006400u;  // nibble mask of two halves; f16 1024
-};
-__device__ __forceinline__ PfK pf_consts() {
-    PfK k;
-    k.m4 = opaque_u32(0x000F000Fu);
-    k.magic = opaque_u32(0x64006400u);
-    return k;
-}
-
 template <int T>
 __device__ __forceinline__ void pf_build_b(const PfW<T>& w, int l, h2 slo, h2 shi, h2 slo_o, h2 shi_o, const h2* s6,
-                                           const h2* s6o, h8* out, const PfK& K = PfK{}) {
+                                           const h2* s6o, h8* out) {
     if constexpr (T == T_Q8_0) {
         const uint32_t lo = w.q8[l].x, hi = w.q8[l].y;
         uint32_t v[4];
@@ -168,20 +152,8 @@ __device__ __forceinline__ void pf_build_b(const PfW<T>& w, int l, h2 slo, h2 sh
             return;
         }
         // j = 0..3: low nibbles i = 0..3 (x01: i = 0, 1 in its halves; x23: i = 2, 3)
-        uint32_t m01, m23, n01, n23;
-        if constexpr (T == T_Q4_K) {  // (x & M) | MAGIC: one v_and_or_b32 each
-            m01 = (x01 & K.m4) | K.magic;
-            m23 = (x23 & K.m4) | K.magic;
-            n01 = ((x01 >> 4) & K.m4) | K.magic;
-            n23 = ((x23 >> 4) & K.m4) | K.magic;
-        } else {
-            m01 = pf_magic(lo01);
-            m23 = pf_magic(lo23);
-            n01 = pf_magic(hi01);
-            n23 = pf_magic(hi23);
-        }
-        const h2 a = as_h2(pf_scale(m01, slo, slo_o)), b = as_h2(pf_scale(m23, slo, slo_o));
-        const h2 c = as_h2(pf_scale(n01, shi, shi_o)), e = as_h2(pf_scale(n23, shi, shi_o));
+        const h2 a = as_h2(pf_scale(pf_magic(lo01), slo, slo_o)), b = as_h2(pf_scale(pf_magic(lo23), slo, slo_o));
+        const h2 c = as_h2(pf_scale(pf_magic(hi01), shi, shi_o)), e = as_h2(pf_scale(pf_magic(hi23), shi, shi_o));
         out[0] = h8{a[0], a[1], b[0], b[1], c[0], c[1], e[0], e[1]};
     }
 }
