@@ -451,7 +451,10 @@ def main(argv=None):
             "continuous_batching": {"sequences": batched,
                                     "note": "k sequences per replica in batched steps (one weight stream per step), "
                                             f"{args.prompt}-token prompts, {args.batch_steps} timed steps; "
-                                            "aggregate tokens/s of this rank; not the metric's value"}
+                                            "aggregate tokens/s of this rank; not the metric's value",
+                                    "matvec": "k_bmm (f16 MFMA, batch.hip) from "
+                                              f"{os.environ.get('LLMI_BMM_MIN', '5')} sequences on K-quant "
+                                              "segments, else k_mvn (VALU)"}
             if batched else None,
             "cpu_baseline": cpu,
             "env": knobs,
