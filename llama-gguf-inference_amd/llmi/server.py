@@ -11,6 +11,8 @@ module answers that contract:
   GET  /v1/models              OpenAI model list
   POST /v1/completions         prompt: str | [token ids]; non-stream or SSE
   POST /v1/chat/completions    messages -> chat template -> tokens; non-stream or SSE
+  POST /v1/embeddings          501 not_supported_error (the reference starts llama-server
+                               without embedding support)
   Authorization: Bearer <key> required on every route but /health when a key is
   configured (401 otherwise; llama-server's public endpoints are /health and /v1/health)
 
@@ -523,6 +525,12 @@ class Handler(BaseHTTPRequestHandler):
         route = self.path.split("?")[0]
         if not self._authorized(route):
             return self._send_json(401, _error(401, "Invalid API Key", "authentication_error"))
+        if route in ("/v1/embeddings", "/embeddings", "/embedding"):
+            # the reference launches llama-server without embedding support (start.sh
+            # passes no --embeddings; docs/API_REFERENCE.md:537-540 "only available if ...
+            # started with embedding support"): upstream then answers 501 not_supported_error
+            return self._send_json(501, _error(
+                501, "This server does not support embeddings. Start it with `--embeddings`", "not_supported_error"))
         if route not in ("/v1/completions", "/v1/chat/completions", "/completion"):
             return self._send_json(404, _error(404, "File Not Found", "not_found_error"))
         if not eng.ready:

@@ -117,6 +117,21 @@ def test_decode_failure_is_json_500(server):
     assert r.status == 200 and json.loads(events[-1][6:])["error"]["code"] == 500
 
 
+def test_embeddings_not_supported(server):
+    """/v1/embeddings (docs/API_REFERENCE.md:537-590) exists only when llama-server runs
+    with embedding support, which the reference's start.sh does not pass: the answer is
+    upstream's 501 not_supported_error, behind the same auth as every /v1 route."""
+    eng, port = server
+    eng.ready = True
+    r, raw = req(port, "POST", "/v1/embeddings", {"model": "any", "input": "Hello world"}, auth=False)
+    assert r.status == 401
+    for path in ("/v1/embeddings", "/embeddings"):
+        r, raw = req(port, "POST", path, {"model": "any", "input": ["a", "b"]})
+        err = json.loads(raw)["error"]
+        assert r.status == 501 and err["code"] == 501 and err["type"] == "not_supported_error"
+        assert "--embeddings" in err["message"]
+
+
 def test_models(server):
     eng, port = server
     eng.ready = True
