@@ -182,6 +182,11 @@ __host__ __device__ inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
 // be cut into tasks (a QKV segment boundary that is not on an even row)
 bool mv_geometry(MVArgs& a, int epi);
 size_t mv_lds_bytes(int act, int cols);
+// per-type matvec launchers (mv_kernels.h; instantiated in mv_q4k/q5k/q6k/q80.hip)
+template <int ACT, bool NORM, int T>
+hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s);
+template <bool NORM, int T, int T2>
+hipError_t mv_qkv2_launch(const MVArgs& a, int split_tasks, dim3 grid, size_t lds, hipStream_t s);
 
 // All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).
 hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t stream);

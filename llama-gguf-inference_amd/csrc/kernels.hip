@@ -27,6 +27,7 @@
 #include "kernels.h"
 #include "mv_device.h"
 #include "pf_device.h"
+#include "launch_util.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -47,186 +48,12 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop) {
     t_ev_start = start;
     t_ev_stop = stop;
 }
-template <typename K, typename... Args>
-static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool first, bool last, Args... args) {
-    hipEvent_t e0 = first ? t_ev_start : nullptr, e1 = last ? t_ev_stop : nullptr;
-    if (e0 || e1) hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, e0, e1, 0, args...);
-    else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
-}
-
-
-static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_SPLIT_BY_PAIRS")) : 0;  // A/B only
+hipEvent_t launch_event(bool stop) { return stop ? t_ev_stop : t_ev_start; }
 
 // LDS of a matvec workgroup: the activation image, the prologue's reduction slots, then
 // one fold buffer (mv_device.h kFoldFloats) per wave
-__host__ __device__ inline size_t fold_off(int act, int cols, int waves) {
-    return a16(lds_red_off(act, cols) + (size_t)waves * sizeof(double));
-}
 size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + (size_t)kMVWaves * kFoldFloats * 4; }
 
-// The matvec of the task range [tbeg, tend) by waves starting at task t0 with stride G
-// (one type group of a launch); returns the wave's LOGITS argmax key.  Per sub-item:
-// every lane's unit terms into the wave's fold buffer F, the fold lanes add them onto
-// their chains; after a row set's last sub-item the row sums (ggml's generic order,
-// mv_device.h) go to the epilogue.  The next sub-item's units are in flight meanwhile.
-#if defined(LLMI_EXP_TRACE)
-// per-wave stamps (tools/mvtrace.py): [block][wave][16] = {entry, prologue done, first
-// sub-item done, exit, -, XCC << 32 | sub-items, x arrived, -, end of sub-items 2..9}
-#define MV_STAMP(I, V)                                                                                    \
-    if (A.trace && (threadIdx.x & 63) == 0)                                                               \
-        A.trace[((size_t)blockIdx.x * kMVWaves + (threadIdx.x >> 6)) * 16 + (I)] = (V);
-#define MV_NOW __builtin_amdgcn_s_memrealtime()
-#else
-#define MV_STAMP(I, V)
-#endif
-
-template <int ACT, bool NORM, int EPI, int T, int NP>
-__device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
-                                                      int tend) {
-    int pos = 0;
-    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
-    unsigned long long best = 0;
-    const int lane = threadIdx.x & 63;
-    const TaskGeo g = task_geo(A);
-    const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
-    const int r = lane / g.lr, ul = lane - r * g.lr;
-
-    int task = t0;
-    MV_STAMP(0, MV_NOW)
-    [[maybe_unused]] int nsub_done = 0, nsub_alt = 0;
-    ProRegs<NORM, NP> R;
-    ImgRegs<2 * NP + 1> RI;
-    const bool img = A.xq != nullptr;
-    if (img) mv_img_issue<2 * NP + 1>(A, RI);  // activation loads first ...
-    else mv_prologue_issue<NORM, NP>(A, R);
-    // Single-round launches (every wave owns at most one task: QKV, attn_output) issue
-    // their weights only once the activation has arrived: the activation loads then do
-    // not queue behind the chip-wide weight burst, and the weight latency overlaps the
-    // quantization instead.  Multi-round launches keep the weights in flight from the start.
-    if (tend - tbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const bool pipe = task < tend && task_is<EPI, T>(A, g, task);
-    Sub b = sub_of<EPI>(A, g, task < tend ? task : tend - 1, 0);
-    Seg sg = pick(A, b.si);
-    LaneUnit lu = lane_unit(g, b, sg, r, ul);
-    // ... then the first units, in flight during the prologue (issued on every path: an
-    // idle wave re-reads row 0, so the prologue's first wait counts only the activation)
-    // (prefetch distance 2 -- three rotating register buffers in a 3x unrolled loop --
-    // measured slower on every shape: gate+up 16.9 -> 21.2 us, 516 -> 433 tok/s)
-    UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
-    if (img) mv_img_finish<2 * NP + 1>(A, L, RI);
-    else mv_prologue_finish<ACT, NORM, NP>(A, L, R);
-    __syncthreads();
-    MV_STAMP(1, MV_NOW)
-
-    if (pipe) {
-        int s = 0;
-        float acc = 0.f, vg = 0.f;
-        for (;;) {
-            // next sub-item: (task, s+1) or (task+G, 0); uniform control flow
-            int tn = task, sn = s + 1;
-            Sub bn = b;
-            Seg sgn = sg;
-            bool has_next = true;
-            if (sn == S) {
-                sn = 0;
-                tn = task + G;
-                has_next = tn < tend && task_is<EPI, T>(A, g, tn);
-            }
-            if (has_next) {
-                bn = sub_of<EPI>(A, g, tn, sn);
-                sgn = pick(A, bn.si);
-            }
-            const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
-            // always issue the prefetch (a valid re-load of the current unit if none)
-            const UnitW<T> nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
-#if defined(LLMI_EXPERIMENTS)
-            // experiment: alternate the wave priority per sub-item, opposite phases for the
-            // first and second dispatch round of workgroups (co-resident pairs), so that
-            // neither workgroup of a CU loses every VALU arbitration to the older one
-            if (A.prio_alt) {
-                if (((nsub_alt++) + ((int)blockIdx.x >= A.prio_alt ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-#endif
-            float tm[9];
-            unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
-            sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
-#if defined(LLMI_EXP_TRACE)
-            ++nsub_done;
-            if (nsub_done == 1) { MV_STAMP(2, MV_NOW) }
-            else if (nsub_done <= 9) { MV_STAMP(6 + nsub_done, MV_NOW) }
-#endif
-            if (!has_next) {
-                task = tn;
-                break;
-            }
-            cur = nxt;
-            task = tn;
-            s = sn;
-            b = bn;
-            sg = sgn;
-            lu = lun;
-        }
-    }
-    // remaining tasks of other types (or all tasks if the first was not of type T)
-    for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
-    MV_STAMP(3, MV_NOW)
-    MV_STAMP(5, ((unsigned long long)(__builtin_amdgcn_s_getreg(6164) & 15) << 32) | (unsigned)nsub_done)
-    return best;
-}
-
-// A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
-// split by workgroup: workgroups [0, split_wgs) run the tasks of type T, the rest the
-// tasks of type T2, each group pipelined in its own type (no divergence in a workgroup).
-template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T>
-__global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Lds L = carve(smem, ACT, A.cols);
-    const int wave = uniform((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    float* F = (float*)(smem + fold_off(ACT, A.cols, kMVWaves)) + wave * kFoldFloats;
-    unsigned long long best;
-    if constexpr (T2 == T) {
-        // single type: optionally two task ranges, the larger one for the first dispatch
-        // round of workgroups (mv_launch: the older of two co-resident workgroups wins
-        // VALU arbitration and runs ~20 % faster per sub-item); one call site either way
-        int t0 = blockIdx.x * kMVWaves + wave, G = gridDim.x * kMVWaves, tb = 0, te = A.ntasks;
-        if (A.split_wgs > 0) {
-            if ((int)blockIdx.x < A.split_wgs) {
-                G = A.split_wgs * kMVWaves;
-                te = A.split_tasks;
-            } else {
-                t0 = A.split_tasks + (blockIdx.x - A.split_wgs) * kMVWaves + wave;
-                G = (gridDim.x - A.split_wgs) * kMVWaves;
-                tb = A.split_tasks;
-            }
-        }
-        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, t0, G, tb, te);
-    } else {
-        if ((int)blockIdx.x < A.split_wgs)
-            best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
-                                                  A.split_tasks);
-        else
-            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, F, A.split_tasks + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
-                                                   (gridDim.x - A.split_wgs) * kMVWaves, A.split_tasks, A.ntasks);
-    }
-    if constexpr (EPI == EPI_LOGITS) {
-        // workgroup max of the lanes' keys, then one atomic into this workgroup's slot
-        const int cur_pos = A.st->pos;
-        unsigned long long* red = (unsigned long long*)L.red;
-        best = wave_max_u64(best);
-        __syncthreads();
-        if (lane == 0) red[wave] = best;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long b = red[0];
-#pragma unroll
-            for (int w = 1; w < kMVWaves; ++w) b = red[w] > b ? red[w] : b;
-            if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
-            if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
-        }
-    }
-}
 
 // The prologue's quantized activation written out in ggml block form (test hook).
 template <int ACT>
@@ -1111,139 +938,6 @@ hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int bl
 // ----------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------
-// Grid of a matvec launch: never more workgroups than can be resident at once (the
-// kernel is grid-strided over row pairs; a second dispatch round would be a tail of
-// idle CUs).  Residency per CU comes from the occupancy query for the instantiation
-// and its LDS, cached per (kernel, LDS bytes, device).
-template <typename K>
-static dim3 resident_grid(K kernel, dim3 grid, size_t lds, int threads = kMVThreads) {
-    static std::mutex mu;
-    static std::map<std::tuple<const void*, size_t, int>, int> cache;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const auto key = std::make_tuple((const void*)kernel, lds, dev * 4096 + threads);
-    int cap = 0;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = cache.find(key);
-        if (it != cache.end()) {
-            cap = it->second;
-        } else {
-            int occ = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, lds) != hipSuccess || occ <= 0) occ = 1;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
-            cap = occ * cus;
-            cache.emplace(key, cap);
-        }
-    }
-    if ((int)grid.x > cap) grid.x = cap;
-    return grid;
-}
-
-// Share of a long single-type launch's tasks given to the first dispatch round of
-// workgroups when two workgroups share each CU (profiles/r03/matvec/old_young_workgroups.json:
-// the older workgroup of a CU retires a sub-item in 3.91 us where the younger takes 4.90
-// on the output head, 2.87 vs 3.40 on gate+up): the first round gets share / (1 + share)
-// of the tasks.  LLMI_MV_OLD_SHARE (A/B; 1 = equal ranges, 0 = off) — which wave reduces
-// a task never changes a result.
-static double old_share() {
-    static const double v = [] {
-        const char* e = getenv("LLMI_MV_OLD_SHARE");
-        return e ? atof(e) : 1.25;
-    }();
-    return v;
-}
-template <int ACT, bool NORM, int T, int EPI, int NP>
-static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds, hipStream_t s) {
-    auto k = k_matvec<ACT, NORM, EPI, T, NP>;
-    const dim3 g = resident_grid(k, grid, lds);
-    MVArgs a = a0;
-    a.split_wgs = 0;
-    const double sh = old_share();
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
-        return n;
-    }();
-    // long launches only (>= 4 tasks per wave), and only when the grid is exactly two
-    // dispatch rounds of one workgroup per CU
-    if (sh > 0 && cus > 0 && (int)g.x == 2 * cus && a.ntasks >= 4 * (int)g.x * kMVWaves) {
-        a.split_wgs = cus;
-        a.split_tasks = (int)(a.ntasks * (sh / (1.0 + sh)) + 0.5);
-    }
-    launch_k(k, g, dim3(kMVThreads), lds, s, true, true, a);
-    return hipGetLastError();
-}
-
-// Two type groups (tasks [0, split) of type T, [split, ntasks) of type T2): the
-// resident grid is dealt to the groups so that the largest per-wave byte count (tasks per
-// wave rounded up x bytes per task) is smallest, >= 1 workgroup each.  Which wave reduces
-// a task never changes a result.
-static int split_groups(int wgs, int p1, int p2, double b1, double b2) {
-    int best = 1;
-    double best_cost = 1e300;
-    for (int w1 = 1; w1 < wgs; ++w1) {
-        const int n1 = w1 * kMVWaves, n2 = (wgs - w1) * kMVWaves;
-        const double c = std::max((double)((p1 + n1 - 1) / n1) * b1, (double)((p2 + n2 - 1) / n2) * b2);
-        if (c < best_cost) { best_cost = c; best = w1; }
-    }
-    return best;
-}
-template <int ACT, bool NORM, int T, int T2, int EPI, int NP>
-static hipError_t mv_launch2(const MVArgs& a0, int split_tasks, dim3 grid, size_t lds, hipStream_t s) {
-    auto k = k_matvec<ACT, NORM, EPI, T, NP, T2>;
-    const dim3 g = resident_grid(k, grid, lds);
-    MVArgs a = a0;
-    a.split_tasks = split_tasks;
-    int w1;
-    if (g_split_by_pairs) {  // A/B: deal by task count
-        w1 = (int)(((long long)g.x * split_tasks + a.ntasks / 2) / a.ntasks);
-        w1 = w1 < 1 ? 1 : w1 > (int)g.x - 1 ? (int)g.x - 1 : w1;
-    } else {
-        w1 = split_groups((int)g.x, split_tasks, a.ntasks - split_tasks, (double)tensor_bytes(T, a.rpt, a.cols),
-                          (double)tensor_bytes(T2, a.rpt, a.cols));
-    }
-    a.split_wgs = w1;
-    launch_k(k, g, dim3(kMVThreads), lds, s, true, true, a);
-    return hipGetLastError();
-}
-
-// prologue sub-blocks per thread held in registers: 1, 2 or 4
-static int prologue_np(int cols) {
-    const int per = (cols / 16 + kMVThreads - 1) / kMVThreads;
-    return per <= 1 ? 1 : per <= 2 ? 2 : 4;
-}
-
-template <int ACT, bool NORM, int T, int EPI>
-static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    switch (prologue_np(a.cols)) {
-        case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
-        case 2: return mv_launch<ACT, NORM, T, EPI, 2>(a, grid, lds, s);
-        default: return mv_launch<ACT, NORM, T, EPI, 4>(a, grid, lds, s);
-    }
-}
-
-// Instantiated (ACT, NORM, EPI) combinations: STORE and ADD with or without the fused
-// RMSNorm; QKV, SWIGLU and LOGITS always take a normalised input.
-template <int ACT, bool NORM, int T>
-static hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
-    switch (epi) {
-        case EPI_STORE: return mv_launch_np<ACT, NORM, T, EPI_STORE>(a, grid, lds, s);
-        case EPI_ADD: return mv_launch_np<ACT, NORM, T, EPI_ADD>(a, grid, lds, s);
-        default: break;
-    }
-    if constexpr (NORM) {
-        switch (epi) {
-            case EPI_QKV: return mv_launch_np<ACT, NORM, T, EPI_QKV>(a, grid, lds, s);
-            case EPI_SWIGLU: return mv_launch_np<ACT, NORM, T, EPI_SWIGLU>(a, grid, lds, s);
-            case EPI_LOGITS: return mv_launch_np<ACT, NORM, T, EPI_LOGITS>(a, grid, lds, s);
-            default: break;
-        }
-    }
-    return hipErrorInvalidValue;
-}
-
 // QKV whose segments form two contiguous type groups split at a task boundary: both groups
 // pipelined (k_matvec's T2 path).  Returns hipErrorNotSupported when not applicable.
 template <bool NORM>
@@ -1256,10 +950,10 @@ static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipSt
         t2 = a.seg[i].type;
         split_row = a.seg[i].row0 - a.seg[0].row0;
     }
-    if (t2 < 0 || split_row % a.rpt || prologue_np(a.cols) != 1) return hipErrorNotSupported;
+    if (t2 < 0 || split_row % a.rpt || a.cols > 16 * kMVThreads) return hipErrorNotSupported;
     const int sp = split_row / a.rpt;
 #define LLMI_QKV2(A_, B_)                                                                            \
-    if (t1 == A_ && t2 == B_) return mv_launch2<0, NORM, A_, B_, EPI_QKV, 1>(a, sp, grid, lds, s);
+    if (t1 == A_ && t2 == B_) return mv_qkv2_launch<NORM, A_, B_>(a, sp, grid, lds, s);
     if constexpr (NORM) {
         LLMI_QKV2(T_Q4_K, T_Q6_K) LLMI_QKV2(T_Q4_K, T_Q5_K) LLMI_QKV2(T_Q5_K, T_Q6_K)
     }
@@ -1577,7 +1271,5 @@ hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint
     return hipGetLastError();
 }
 
-// batched prefill (MFMA): same translation unit, shares the device helpers above
-#include "prefill.hip.inc"
 
 }  // namespace llmi

@@ -141,7 +141,11 @@ struct Lds {
 };
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ inline size_t lds_red_off(int act, int cols) { return (size_t)(cols >> 8) * kRec; }
-// (mv_lds_bytes: defined in kernels.hip)
+// offset of the per-wave fold buffers in a matvec workgroup's LDS (after the activation
+// image and the prologue's reduction slots); mv_lds_bytes: kernels.hip
+__host__ __device__ inline size_t fold_off(int act, int cols, int waves) {
+    return a16(lds_red_off(act, cols) + (size_t)waves * sizeof(double));
+}
 
 __device__ __forceinline__ Lds carve(uint8_t* smem, int act, int cols) {
     Lds l;

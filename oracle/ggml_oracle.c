@@ -543,7 +543,174 @@ int or_set_fast_dots(int on) { g_fast = on ? 1 : 0; return 1; }
 int or_set_fast_dots(int on) { g_fast = 0; (void)on; return 0; }  /* no AVX2 in this build */
 #endif
 
+/* ---------------- x86 association mode (parity measurement) ----------------
+ * MEASUREMENT PATH, NOT THE CHECKER.  The GPU is bit-identical to the generic order above.
+ * The reference's CPU path (Dockerfile.cpu:11 `llama.cpp:server`, NGL=0 at :84-89) runs
+ * llama.cpp's x86 build instead, whose kernels associate the same operations differently
+ * [upstream ggml-cpu arch/x86/quants.c, vec.h/vec.cpp, simd-mappings.h, ops.cpp; recalled,
+ * not vendored; modelled on the AVX2+FMA ("haswell") variant].  or_set_x86_mode() switches
+ * the oracle onto that association, so that generic-vs-x86 over a trajectory measures the
+ * GPU's distance from the NGL=0 numerics (tools/parity_x86.py, profiles/r04/parity_x86.jsonl).
+ * Lanes are emulated in scalar C with fmaf() where upstream uses _mm256_fmadd_ps:
+ *   OR_X86_DOTS   ggml_vec_dot_q{4,5,6}_K_q8_K / q8_0_q8_0 AVX2: per 256-block the integer
+ *                 sums in 8 int32 lanes (lane k = bytes 4k..4k+3 of every 32-byte vector,
+ *                 maddubs + madd), acc[k] = fma(d, (float)sumi[k], acc[k]) with
+ *                 d = y.d * fp16(x.d); Q4_K's min terms in 4 lanes acc_m[k] = fma(dmin,
+ *                 (float)prod[k], acc_m[k]) with dmin = -y.d * fp16(x.dmin), prod[k] =
+ *                 m[2k](bs[4k]+bs[4k+1]) + m[2k+1](bs[4k+2]+bs[4k+3]) (hadd + madd),
+ *                 reduced (a0+a2)+(a1+a3); Q5_K's one scalar summs += dmin*(float)sum(prod)
+ *                 (FMA-contracted, gnu11 default); result hsum_float_8(acc) [+ mins]
+ *   OR_X86_Q80    quantize_row_q8_0 AVX2: id = 127/amax, q = round-half-even(x*id)
+ *   OR_X86_F16DOT ggml_vec_dot_f16 AVX2+F16C (KQ over head dims, PV over positions):
+ *                 4 x 8 fp32 FMA accumulators (element i -> acc[(i%32)/8][i%8]), reduced
+ *                 acc0+acc2, acc1+acc3, then those two, then lo4+hi4 and two hadds
+ *   OR_X86_VEXP   ggml_v_expf / ggml_v_silu (AVX2 polynomial exp) in soft_max and SwiGLU,
+ *                 and ggml_vec_soft_max_f32's sum: per 8 positions an fp32 hsum, added in double
+ *   OR_X86_LIBM   libm expf in soft_max and SiLU (scalar sums) instead of llmi_expf
+ *   OR_X86_NOFMA  Q5_K's scalar min term without FMA contraction (-ffp-contract=off build) */
+enum { OR_X86_DOTS = 1, OR_X86_Q80 = 2, OR_X86_F16DOT = 4, OR_X86_VEXP = 8, OR_X86_LIBM = 16, OR_X86_NOFMA = 32 };
+static int g_x86 = 0;
+int or_set_x86_mode(int flags) { g_x86 = flags; return g_x86; }
+int or_get_x86_mode(void) { return g_x86; }
+
+/* hsum_float_8: (lo4 + hi4), then movehl + add, then movehdup + add_ss */
+static inline float x86_hsum8(const float* a) {
+    const float t0 = a[4] + a[0], t1 = a[5] + a[1], t2 = a[6] + a[2], t3 = a[7] + a[3];
+    return (t0 + t2) + (t1 + t3);
+}
+static float x86_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
+    float acc[8] = {0}, accm[4] = {0};
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = y[i].d * llmi_h2f(x[i].d);
+        const float dmin = -y[i].d * llmi_h2f(x[i].dmin);
+        uint8_t sc[8], mn[8];
+        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
+        int32_t sumi[8] = {0};
+        for (int j = 0; j < 4; ++j)
+            for (int b = 0; b < 32; ++b) {
+                const int q = x[i].qs[32 * j + b];
+                sumi[b >> 2] += sc[2 * j] * ((q & 0xF) * y[i].qs[64 * j + b]) + sc[2 * j + 1] * ((q >> 4) * y[i].qs[64 * j + 32 + b]);
+            }
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(d, (float)sumi[k], acc[k]);
+        const int16_t* bs = y[i].bsums;
+        for (int k = 0; k < 4; ++k) {
+            const int prod = mn[2 * k] * (bs[4 * k] + bs[4 * k + 1]) + mn[2 * k + 1] * (bs[4 * k + 2] + bs[4 * k + 3]);
+            accm[k] = fmaf(dmin, (float)prod, accm[k]);
+        }
+    }
+    const float m = (accm[0] + accm[2]) + (accm[1] + accm[3]);
+    return x86_hsum8(acc) + m;
+}
+static float x86_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
+    float acc[8] = {0}, summs = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = y[i].d * llmi_h2f(x[i].d);
+        const float dmin = -y[i].d * llmi_h2f(x[i].dmin);
+        uint8_t sc[8], mn[8];
+        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
+        int32_t sumi[8] = {0};
+        for (int j = 0; j < 4; ++j)
+            for (int b = 0; b < 32; ++b) {
+                const int q = x[i].qs[32 * j + b], h = x[i].qh[b];
+                const int lo = (q & 0xF) + (((h >> (2 * j)) & 1) << 4), hi = (q >> 4) + (((h >> (2 * j + 1)) & 1) << 4);
+                sumi[b >> 2] += sc[2 * j] * (lo * y[i].qs[64 * j + b]) + sc[2 * j + 1] * (hi * y[i].qs[64 * j + 32 + b]);
+            }
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(d, (float)sumi[k], acc[k]);
+        int sm = 0;
+        for (int j = 0; j < 16; ++j) sm += mn[j / 2] * y[i].bsums[j];
+        summs = (g_x86 & OR_X86_NOFMA) ? summs + dmin * (float)sm : fmaf(dmin, (float)sm, summs);
+    }
+    return x86_hsum8(acc) + summs;
+}
+static float x86_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
+    float acc[8] = {0};
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = y[i].d * llmi_h2f(x[i].d);
+        int32_t sumi[8] = {0};
+        for (int h = 0; h < 2; ++h)
+            for (int v = 0; v < 4; ++v)
+                for (int b = 0; b < 32; ++b) {
+                    const int e = 128 * h + 32 * v + b;
+                    const uint8_t lq = x[i].ql[64 * h + 32 * (v & 1) + b], hq = x[i].qh[32 * h + b];
+                    const int q = ((v < 2 ? lq & 0xF : lq >> 4) | (((hq >> (2 * v)) & 3) << 4)) - 32;
+                    sumi[b >> 2] += x[i].scales[e / 16] * (q * y[i].qs[e]);
+                }
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(d, (float)sumi[k], acc[k]);
+    }
+    return x86_hsum8(acc);
+}
+static float x86_q8_0(int n, const block_q8_0* x, const block_q8_0* y) {
+    float acc[8] = {0};
+    for (int ib = 0; ib < n / QK8_0; ++ib) {
+        const float d = llmi_h2f(x[ib].d) * llmi_h2f(y[ib].d);
+        int32_t sumi[8] = {0};
+        for (int b = 0; b < 32; ++b) sumi[b >> 2] += x[ib].qs[b] * y[ib].qs[b];
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(d, (float)sumi[k], acc[k]);
+    }
+    return x86_hsum8(acc);
+}
+/* quantize_row_q8_0 (x86 AVX2 path) */
+static void x86_quantize_row_q8_0(const float* x, void* vy, int64_t k) {
+    block_q8_0* y = vy;
+    for (int64_t i = 0; i < k / QK8_0; i++) {
+        float amax = 0.0f;
+        for (int j = 0; j < QK8_0; j++) amax = fmaxf(amax, fabsf(x[i * QK8_0 + j]));
+        const float d = amax / 127.f;
+        y[i].d = llmi_f2h(d);
+        const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+        for (int j = 0; j < QK8_0; ++j) y[i].qs[j] = (int8_t)(int)rintf(x[i * QK8_0 + j] * id);
+    }
+}
+/* ggml_vec_dot_f16 (AVX2 + F16C): n a multiple of 32 (head dims; padded KV rows) */
+static float x86_dot_f16f(int n, const float* a, const float* b) {
+    float acc[4][8];
+    memset(acc, 0, sizeof acc);
+    const int np = n & ~31;
+    for (int i = 0; i < np; ++i) acc[(i & 31) >> 3][i & 7] = fmaf(a[i], b[i], acc[(i & 31) >> 3][i & 7]);
+    for (int l = 0; l < 8; ++l) { acc[0][l] = acc[0][l] + acc[2][l]; acc[1][l] = acc[1][l] + acc[3][l]; }
+    for (int l = 0; l < 8; ++l) acc[0][l] = acc[0][l] + acc[1][l];
+    const float t0 = acc[0][0] + acc[0][4], t1 = acc[0][1] + acc[0][5], t2 = acc[0][2] + acc[0][6], t3 = acc[0][3] + acc[0][7];
+    double sumf = (double)((t0 + t1) + (t2 + t3));  /* _mm_hadd_ps twice: lane 0 */
+    for (int i = np; i < n; ++i) sumf += (double)(a[i] * b[i]);
+    return (float)sumf;
+}
+/* ggml_v_expf (AVX2 form; the ARM optimized-routines expf polynomial) */
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static float x86_v_expf(float x) {
+    const float r = 0x1.8p23f;
+    const float z = fmaf(x, 0x1.715476p+0f, r);
+    const float n = z - r;
+    const float b = fmaf(-n, 0x1.7f7d1cp-20f, fmaf(-n, 0x1.62e4p-1f, x));
+    const uint32_t e = f2u(z) << 23;
+    const float k = u2f(e + f2u(1.0f));
+    const float u = b * b;
+    const float j = fmaf(fmaf(fmaf(0x1.0e4020p-7f, b, 0x1.573e2ep-5f), u, fmaf(0x1.555e66p-3f, b, 0x1.fffdb6p-2f)), u,
+                         0x1.ffffecp-1f * b);
+    if (!(fabsf(n) > 126.f)) return fmaf(j, k, k);
+    const uint32_t g = n <= 0.f ? 0x82000000u : 0u;
+    const float s1 = u2f(g + 0x7f000000u), s2 = u2f(e - g);
+    if (fabsf(n) > 192.f) return s1 * s1;
+    return fmaf(s2, j, s2) * s1;
+}
+/* SiLU and exp under the mode's exp (ggml_v_silu: x / (1 + v_expf(-x))) */
+static inline float mode_expf(float x) {
+    if (g_x86 & OR_X86_VEXP) return x86_v_expf(x);
+    if (g_x86 & OR_X86_LIBM) return expf(x);
+    return llmi_expf(x);
+}
+static inline float mode_silu(float x) { return x / (1.0f + mode_expf(-x)); }
+
 float or_vec_dot(int wtype, int n, const void* w, const void* a) {
+    if (g_x86 & OR_X86_DOTS) {
+        switch (wtype) {
+            case OR_Q4_K: return x86_q4_K(n, w, a);
+            case OR_Q5_K: return x86_q5_K(n, w, a);
+            case OR_Q6_K: return x86_q6_K(n, w, a);
+            case OR_Q8_0: return x86_q8_0(n, w, a);
+            default: break;
+        }
+    }
 #if defined(__AVX2__) && defined(__FMA__)
     if (g_fast) {
         switch (wtype) {
@@ -573,7 +740,7 @@ static size_t act_bytes(int wtype, int64_t cols) {
 static void quantize_act(int wtype, const float* x, void* act, int64_t cols) {
     int vt = or_vec_dot_type(wtype);
     if (vt == OR_Q8_K) or_quantize_row_q8_K(x, act, cols);
-    else if (vt == OR_Q8_0) or_quantize_row_q8_0(x, act, cols);
+    else if (vt == OR_Q8_0) { if (g_x86 & OR_X86_Q80) x86_quantize_row_q8_0(x, act, cols); else or_quantize_row_q8_0(x, act, cols); }
     else if (vt == OR_F16) for (int64_t i = 0; i < cols; ++i) ((uint16_t*)act)[i] = llmi_f2h(x[i]);
     else memcpy(act, x, (size_t)cols * 4);
 }
@@ -864,17 +1031,51 @@ static void attn_head(const or_model* m, int l, const float* q, int h, int n_kv,
     float qf[512];
     for (int d = 0; d < D; ++d) qf[d] = llmi_h2f(llmi_f2h(q[d]));
     float mx = -INFINITY;
+    const int f16x = (g_x86 & OR_X86_F16DOT) != 0;
     for (int t = 0; t < n_kv; ++t) {
         const uint16_t* kr = kl + (size_t)t * kvd + (size_t)g * D;
-        double sumf = 0.0;  /* ggml_vec_dot_f16 (generic): double accumulation */
-        for (int d = 0; d < D; ++d) sumf += (double)(llmi_h2f(kr[d]) * qf[d]);
-        w[t] = (float)sumf * kq_scale;
+        if (f16x) {
+            float kf[512];
+            for (int d = 0; d < D; ++d) kf[d] = llmi_h2f(kr[d]);
+            w[t] = x86_dot_f16f(D, kf, qf) * kq_scale;
+        } else {
+            double sumf = 0.0;  /* ggml_vec_dot_f16 (generic): double accumulation */
+            for (int d = 0; d < D; ++d) sumf += (double)(llmi_h2f(kr[d]) * qf[d]);
+            w[t] = (float)sumf * kq_scale;
+        }
         mx = fmaxf(mx, w[t]);
     }
     double sum = 0.0;
-    for (int t = 0; t < n_kv; ++t) { float e = llmi_expf(w[t] - mx); sum += (double)e; w[t] = e; }
+    if (g_x86 & OR_X86_VEXP) {  /* ggml_vec_soft_max_f32, AVX2: per 8 positions an fp32 hsum */
+        int t = 0;
+        for (; t + 7 < n_kv; t += 8) {
+            float e8[8];
+            for (int l = 0; l < 8; ++l) { e8[l] = x86_v_expf(w[t + l] - mx); w[t + l] = e8[l]; }
+            sum += (double)x86_hsum8(e8);
+        }
+        if (t < n_kv) {  /* the row is padded to 32 with masked (-inf -> 0) positions */
+            float e8[8] = {0};
+            for (int l = 0; t + l < n_kv; ++l) { e8[l] = x86_v_expf(w[t + l] - mx); w[t + l] = e8[l]; }
+            sum += (double)x86_hsum8(e8);
+        }
+    } else {
+        for (int t = 0; t < n_kv; ++t) { float e = mode_expf(w[t] - mx); sum += (double)e; w[t] = e; }
+    }
     const float inv = (float)(1.0 / sum);
     for (int t = 0; t < n_kv; ++t) w[t] = llmi_h2f(llmi_f2h(w[t] * inv));  /* p rounded to f16 */
+    if (f16x) {  /* mul_mat(V^T, p): one f16 dot over the positions (padded to 32 with p = 0) per dim */
+        const int np = (n_kv + 31) & ~31;
+        float vf[8192], pf[8192];
+        if (np > 8192) return;
+        for (int t = n_kv; t < np; ++t) pf[t] = 0.f;
+        for (int t = 0; t < n_kv; ++t) pf[t] = w[t];
+        for (int d = 0; d < D; ++d) {
+            for (int t = 0; t < n_kv; ++t) vf[t] = llmi_h2f(vl[(size_t)t * kvd + (size_t)g * D + d]);
+            for (int t = n_kv; t < np; ++t) vf[t] = 0.f;
+            out[d] = x86_dot_f16f(np, vf, pf);
+        }
+        return;
+    }
     double acc[512];
     for (int d = 0; d < D; ++d) acc[d] = 0.0;
     for (int t = 0; t < n_kv; ++t) {  /* per d the same sequential double sum over t */
@@ -917,7 +1118,7 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
         or_rms_norm_mul(m->x, (const float*)m->L[l].fn->data, m->xb, E, m->eps);
         matvec_t(m->L[l].wg, m->xb, m->hb, nth);
         matvec_t(m->L[l].wu, m->xb, m->hb2, nth);
-        for (int i = 0; i < F; ++i) m->hb[i] = llmi_silu(m->hb[i]) * m->hb2[i];
+        for (int i = 0; i < F; ++i) m->hb[i] = mode_silu(m->hb[i]) * m->hb2[i];
         matvec_t(m->L[l].wd, m->hb, m->tmp, nth);
         for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
     }
@@ -942,7 +1143,7 @@ static void matmul_t(const or_tensor* W, const float* X, int T, float* Y, int nt
     uint8_t* acts = malloc(ab * (size_t)T);
     for (int t = 0; t < T; ++t) quantize_act(wtype, X + (size_t)t * cols, acts + ab * t, cols);
     const size_t row_bytes = (size_t)(cols / or_block_size(wtype)) * or_type_size(wtype);
-    const int kq = wtype == OR_Q4_K || wtype == OR_Q5_K || wtype == OR_Q6_K;
+    const int kq = (wtype == OR_Q4_K || wtype == OR_Q5_K || wtype == OR_Q6_K) && !(g_x86 & OR_X86_DOTS);
 #pragma omp parallel num_threads(nth > 0 ? nth : 1)
     {
         uint8_t* u = malloc((size_t)cols);
@@ -1008,7 +1209,7 @@ int or_prefill(or_model* m, const int32_t* tokens, int T, int pos0, int nth) {
         for (int t = 0; t < T; ++t) or_rms_norm_mul(X + (size_t)t * E, (const float*)m->L[l].fn->data, XB + (size_t)t * E, E, m->eps);
         matmul_t(m->L[l].wg, XB, T, HB, nth);
         matmul_t(m->L[l].wu, XB, T, HB2, nth);
-        for (size_t i = 0; i < (size_t)T * F; ++i) HB[i] = llmi_silu(HB[i]) * HB2[i];
+        for (size_t i = 0; i < (size_t)T * F; ++i) HB[i] = mode_silu(HB[i]) * HB2[i];
         matmul_t(m->L[l].wd, HB, T, TMP, nth);
         for (size_t i = 0; i < (size_t)T * E; ++i) X[i] = TMP[i] + X[i];
         if (l == m->n_layer - 1) {  /* the last token's taps, as or_decode leaves them */

@@ -46,6 +46,11 @@ float or_vec_dot(int wtype, int n, const void* wrow, const void* act);
 /* CPU baseline timing only: AVX2 dots in the x86 kernels' association (not the
  * generic order; never used by a parity check).  Returns 0 if this build has no AVX2. */
 int or_set_fast_dots(int on);
+/* Parity measurement only (never a check): switch the dots, q8_0 quantization, f16 attention
+ * dots and exp onto upstream's x86 AVX2 association (flags in ggml_oracle.c: 1 dots, 2 q8_0,
+ * 4 f16 dots, 8 ggml_v_expf, 16 libm expf, 32 no FMA contraction).  0 = generic (default). */
+int or_set_x86_mode(int flags);
+int or_get_x86_mode(void);
 /* y[r] = vec_dot(W[r], quantize(x)) for r < rows (x is f32[cols]); OpenMP over rows */
 int or_matvec(int wtype, const void* W, int64_t rows, int64_t cols, const float* x, float* y, int nthreads);
 

@@ -44,6 +44,16 @@ def set_fast_dots(on: bool) -> bool:
     return bool(lib().or_set_fast_dots(1 if on else 0))
 
 
+# x86 association flags (ggml_oracle.c "x86 association mode"): parity MEASUREMENT only
+X86_DOTS, X86_Q80, X86_F16DOT, X86_VEXP, X86_LIBM, X86_NOFMA = 1, 2, 4, 8, 16, 32
+X86_ALL = X86_DOTS | X86_Q80 | X86_F16DOT | X86_VEXP  # upstream's AVX2 build as restated
+
+
+def set_x86_mode(flags: int) -> None:
+    """Switch the oracle (process-global) onto upstream's x86 association; 0 = generic."""
+    lib().or_set_x86_mode(int(flags))
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
@@ -76,6 +86,8 @@ def lib() -> C.CDLL:
         "or_tap": (C.c_int, [P, C.c_int, P]),
         "or_bytes_per_token": (C.c_double, [P, C.c_int]),
         "or_set_fast_dots": (C.c_int, [C.c_int]),
+        "or_set_x86_mode": (C.c_int, [C.c_int]),
+        "or_get_x86_mode": (C.c_int, []),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -164,8 +176,11 @@ def expf(x: float) -> float:
 class OracleModel:
     """Whole-model decode (llm_build_llama order) on the CPU, f16 KV cache."""
 
-    def __init__(self, path: str, n_ctx: int = 512, threads: int = 0):
+    def __init__(self, path: str, n_ctx: int = 512, threads: int = 0, x86: int = 0):
+        """x86: association flags applied around this model's calls (0 = the generic order
+        the parity checks use; nonzero only for the x86 distance measurement)."""
         L = lib()
+        self.x86 = int(x86)
         self._h = L.or_model_load(path.encode(), n_ctx)
         if not self._h:
             raise RuntimeError("oracle load failed: " + L.or_last_error().decode())
@@ -178,6 +193,7 @@ class OracleModel:
     def decode(self, token: int, pos: int, logits: bool = True) -> np.ndarray | None:
         """One decode step; logits=False skips the output head (prompt tokens)."""
         out = np.empty(self.n_vocab, dtype=np.float32) if logits else None
+        lib().or_set_x86_mode(self.x86)
         rc = lib().or_decode(self._h, int(token), int(pos), _p(out) if logits else None, self.threads)
         if rc != 0:
             raise RuntimeError(f"or_decode rc={rc}: " + lib().or_last_error().decode())
@@ -187,13 +203,25 @@ class OracleModel:
         """T decode steps at pos0.. with no logits (or_prefill: the same operations per
         token, loops reordered so each weight row is unpacked once)."""
         toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
+        lib().or_set_x86_mode(self.x86)
         rc = lib().or_prefill(self._h, _p(toks), int(toks.size), int(pos0), self.threads)
         if rc != 0:
             raise RuntimeError(f"or_prefill rc={rc}: " + lib().or_last_error().decode())
 
     def tap(self, which: int) -> np.ndarray:
-        out = np.empty(self.n_embd, dtype=np.float32)
-        lib().or_tap(self._h, which, _p(out))
+        """or_tap: 0 embedding row, 1 final hidden (pre-norm), 2 roped q, 3 attention
+        output, 4 SwiGLU output, 5 roped k, 6 v (last layer of the last step); 7 / 8 the
+        last layer's raw f16 K / V cache [n_ctx][n_head_kv * head_dim]."""
+        kvd = self.n_head_kv * self.head_dim
+        n = {0: self.n_embd, 1: self.n_embd, 2: self.n_head * self.head_dim, 3: self.n_head * self.head_dim,
+             4: self.n_ff, 5: kvd, 6: kvd}.get(which)
+        if which in (7, 8):
+            out = np.empty(self.n_ctx * kvd, dtype=np.uint16)
+        elif n is None:
+            raise ValueError(f"tap {which}")
+        else:
+            out = np.empty(n, dtype=np.float32)
+        assert lib().or_tap(self._h, which, _p(out)) == 0
         return out
 
     def kv_clear(self) -> None:
