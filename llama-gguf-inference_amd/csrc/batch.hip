@@ -266,7 +266,7 @@ __global__ __launch_bounds__(512) void k_battn_pv16(BAttnArgs b, int kvb) {
 // terms go through LDS to the fold threads, one per (matrix, chain, lane quad), which add
 // them stage after stage onto their chains — every chain sees the blocks in order, so a
 // token's results equal its single-sequence decode (k_matvec) and the oracle bit for bit.
-// The padded token rows of the MFMA read token 0's fragments (finite, discarded).
+// The padded token rows of the MFMA are zero fragments (bm_load zeroes them; discarded).
 constexpr int kBmW = 8, kBmT = kBmW * 64;
 
 template <int T, int NW>
@@ -684,20 +684,33 @@ bool bmm_ok(const MVArgs& a, int epi) {
     return epi == EPI_STORE || epi == EPI_ADD || epi == EPI_QKV || epi == EPI_SWIGLU || epi == EPI_LOGITS;
 }
 
+// Resident k_bmm workgroups on the CURRENT device, per (kernel, LDS bytes, device), with
+// the dynamic-LDS attribute set once per device: in-process replicas run one scheduler
+// thread per GPU, so the cache is keyed by device and guarded (as mvn_grid's).
+static int bmm_cap(const void* k, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, size_t, int>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(k, lds, dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int occ = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBmT, lds) != hipSuccess || occ <= 0) occ = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
+    const int cap = occ * cus;
+    cache.emplace(key, cap);
+    return cap;
+}
+
 template <int T, int EPI>
 static hipError_t bmm_launch(const MVArgs& a, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
     auto k = k_bmm<T, EPI>;
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
     const size_t lds = (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
-    static int cap = 0;  // per instantiation: resident workgroups on the device
-    if (!cap) {
-        if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        int occ = 0, cus = 0, dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBmT, lds) != hipSuccess || occ <= 0) occ = 1;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
-        cap = occ * cus;
-    }
+    const int cap = bmm_cap((const void*)k, lds);
     int rows = 0;
     if (EPI == EPI_SWIGLU) rows = a.seg[0].rows;
     else

@@ -796,6 +796,7 @@ int32_t llama_tokenize(const struct llama_vocab* v, const char* text, int32_t te
 int32_t llama_token_to_piece(const struct llama_vocab* v, llama_token token, char* buf, int32_t length, int32_t lstrip,
                              bool special) {
     if (!v) return 0;
+    API_TRY
     std::string p = v->tok->piece(token, special);
     size_t k = 0;
     while (lstrip > 0 && k < p.size() && p[k] == ' ') {
@@ -806,26 +807,31 @@ int32_t llama_token_to_piece(const struct llama_vocab* v, llama_token token, cha
     if (n > length) return -n;
     if (n > 0) memcpy(buf, p.data() + k, (size_t)n);
     return n;
+    API_CATCH(INT32_MIN)
 }
 
 // upstream llama_detokenize: the pieces concatenated; remove_special drops a leading BOS
-// (when the vocabulary adds one) and a trailing EOS; unparse_special renders CONTROL text.
+// (when the vocabulary adds one) and a trailing EOS (when it adds one: add_eos_token);
+// unparse_special renders CONTROL text.
 // Bytes written, or -(bytes needed).
 int32_t llama_detokenize(const struct llama_vocab* v, const llama_token* tokens, int32_t n_tokens, char* text,
                          int32_t text_len_max, bool remove_special, bool unparse_special) {
     if (!v || n_tokens < 0 || (!tokens && n_tokens > 0)) return INT32_MIN;
+    API_TRY
     int32_t b = 0, e = n_tokens;
     if (remove_special && e > b && v->tok->add_bos && tokens[b] == v->tok->bos) ++b;
-    if (remove_special && e > b && tokens[e - 1] == v->tok->eos) --e;
+    if (remove_special && e > b && v->tok->add_eos && tokens[e - 1] == v->tok->eos) --e;
     std::string out;
     for (int32_t i = b; i < e; ++i) out += v->tok->piece(tokens[i], unparse_special);
     if ((int64_t)out.size() > (int64_t)text_len_max) return -(int32_t)out.size();
     if (!out.empty()) memcpy(text, out.data(), out.size());
     return (int32_t)out.size();
+    API_CATCH(INT32_MIN)
 }
 
 // a tokenizer-only handle from a GGUF's metadata (no tensors needed)
 struct llama_vocab* llmi_vocab_load_from_file(const char* path) {
+    API_TRY
     GgufFile f;
     std::string err;
     if (!path || !f.open(path, err)) {
@@ -838,6 +844,7 @@ struct llama_vocab* llmi_vocab_load_from_file(const char* path) {
     v->owned = Tokenizer::from_gguf(f, te ? (int)te->ne[1] : 0);
     v->tok = v->owned.get();
     return v.release();
+    API_CATCH(nullptr)
 }
 void llmi_vocab_free(struct llama_vocab* v) {
     if (v && v->owned) delete v;
@@ -990,7 +997,10 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     const int mb = std::max(64, prop.multiProcessorCount * wg_per_cu());
     float* nw = nullptr;
     StepState* st = nullptr;
-    const bool norm = mode & 1, logits = mode & 2, img = mode & 8;
+    // mode bit 5: gate+up SwiGLU launch (rows = both halves; RMSNorm on), bit 6: residual-add
+    // epilogue (ffn_down / attn_output)
+    const bool swiglu = mode & 32, add = mode & 64;
+    const bool norm = (mode & 1) || swiglu, logits = mode & 2, img = mode & 8;
     if (norm) {
         std::vector<float> ones((size_t)cols, 1.0f);
         if (hipMalloc(&nw, (size_t)cols * 4) != hipSuccess) { set_err("out of device memory"); return -1.0; }
@@ -1011,7 +1021,8 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
         (void)hipMemset(xq, 0, (size_t)(cols / 256) * 304);
         a.xq = xq;
     }
-    const int epi = logits ? EPI_LOGITS : EPI_STORE;
+    const int epi = logits ? EPI_LOGITS : swiglu ? EPI_SWIGLU : add ? EPI_ADD : EPI_STORE;
+    const size_t half = swiglu ? (size_t)llmi_device_layout_bytes(type, rows / 2, cols) : 0;
     // one graph of n_mats launches (one per weight copy), replayed: no host launch cost
     hipStream_t s = nullptr;
     (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
@@ -1019,7 +1030,13 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     hipGraphExec_t ex = nullptr;
     bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
     for (int k = 0; ok && k < n_mats; ++k) {
-        a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows, cols);
+        if (swiglu) {
+            a.nseg = 2;
+            a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows / 2, cols);
+            a.seg[1] = seg_at(type, (const uint8_t*)w + stride * k + half, rows / 2, cols);
+        } else {
+            a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows, cols);
+        }
         ok = launch_matvec(a, epi, mb, s) == hipSuccess;
     }
     ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;

@@ -62,7 +62,8 @@ __device__ __forceinline__ int dot4(uint32_t a, int b, int c) {
 // row_mirror partner (lane 7-i / 15-i) is used, which equals lane L^4 / L^8 whenever
 // the value is already uniform over aligned 4- / 8-lane groups, i.e. inside a
 // butterfly after the xor-1/xor-2 (and xor-4) steps.  Every butterfly below runs the
-// steps in the order 1, 2, 4, 8, 16, 32; the oracle's device order models exactly that.
+// steps in the order 1, 2, 4, 8, 16, 32 (used only where the result is exact in any order:
+// integer sums, max / min keys, double sums that absorb the reordering -- DESIGN.md §5).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);

@@ -1,4 +1,4 @@
-// mv_kernels.h — the single-token quantized matvec kernels (k_matvec, k_matvec_burst)
+// mv_kernels.h — the single-token quantized matvec kernel (k_matvec, 4- or 8-wave workgroups)
 // and their launchers, compiled once per weight type in mv_q4k.hip / mv_q5k.hip /
 // mv_q6k.hip / mv_q80.hip (explicit instantiations of mv_dispatch_epi and mv_qkv2_launch,
 // declared in kernels.h).  Split by type so the instantiations build in parallel.
@@ -28,13 +28,13 @@ static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_
 // sub-item done, exit, -, XCC << 32 | sub-items, x arrived, -, end of sub-items 2..9}
 #define MV_STAMP(I, V)                                                                                    \
     if (A.trace && (threadIdx.x & 63) == 0)                                                               \
-        A.trace[((size_t)blockIdx.x * kMVWaves + (threadIdx.x >> 6)) * 16 + (I)] = (V);
+        A.trace[((size_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * 16 + (I)] = (V);
 #define MV_NOW __builtin_amdgcn_s_memrealtime()
 #else
 #define MV_STAMP(I, V)
 #endif
 
-template <int ACT, bool NORM, int EPI, int T, int NP>
+template <int ACT, bool NORM, int EPI, int T, int NP, int NT = kMVThreads>
 __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
                                                       int tend) {
     int pos = 0;
@@ -51,8 +51,8 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     ProRegs<NORM, NP> R;
     ImgRegs<2 * NP + 1> RI;
     const bool img = A.xq != nullptr;
-    if (img) mv_img_issue<2 * NP + 1>(A, RI);  // activation loads first ...
-    else mv_prologue_issue<NORM, NP>(A, R);
+    if (img) mv_img_issue<2 * NP + 1, NT>(A, RI);  // activation loads first ...
+    else mv_prologue_issue<NORM, NP, NT>(A, R);
     // Single-round launches (every wave owns at most one task: QKV, attn_output) issue
     // their weights only once the activation has arrived: the activation loads then do
     // not queue behind the chip-wide weight burst, and the weight latency overlaps the
@@ -67,8 +67,8 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     // (prefetch distance 2 -- three rotating register buffers in a 3x unrolled loop --
     // measured slower on every shape: gate+up 16.9 -> 21.2 us, 516 -> 433 tok/s)
     UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
-    if (img) mv_img_finish<2 * NP + 1>(A, L, RI);
-    else mv_prologue_finish<ACT, NORM, NP>(A, L, R);
+    if (img) mv_img_finish<2 * NP + 1, NT>(A, L, RI);
+    else mv_prologue_finish<ACT, NORM, NP, NT>(A, L, R);
     __syncthreads();
     MV_STAMP(1, MV_NOW)
 
@@ -132,37 +132,37 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
 // A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
 // split by workgroup: workgroups [0, split_wgs) run the tasks of type T, the rest the
 // tasks of type T2, each group pipelined in its own type (no divergence in a workgroup).
-template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T>
-__global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
+template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T, int NT = kMVThreads>
+__global__ __launch_bounds__(NT) void k_matvec(MVArgs A) {
+    constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Lds L = carve(smem, ACT, A.cols);
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
-    float* F = (float*)(smem + fold_off(ACT, A.cols, kMVWaves)) + wave * kFoldFloats;
+    float* F = (float*)(smem + fold_off(ACT, A.cols, NW)) + wave * kFoldFloats;
     unsigned long long best;
     if constexpr (T2 == T) {
         // single type: optionally two task ranges, the larger one for the first dispatch
         // round of workgroups (mv_launch: the older of two co-resident workgroups wins
         // VALU arbitration and runs ~20 % faster per sub-item); one call site either way
-        int t0 = blockIdx.x * kMVWaves + wave, G = gridDim.x * kMVWaves, tb = 0, te = A.ntasks;
+        int t0 = blockIdx.x * NW + wave, G = gridDim.x * NW, tb = 0, te = A.ntasks;
         if (A.split_wgs > 0) {
             if ((int)blockIdx.x < A.split_wgs) {
-                G = A.split_wgs * kMVWaves;
+                G = A.split_wgs * NW;
                 te = A.split_tasks;
             } else {
-                t0 = A.split_tasks + (blockIdx.x - A.split_wgs) * kMVWaves + wave;
-                G = (gridDim.x - A.split_wgs) * kMVWaves;
+                t0 = A.split_tasks + (blockIdx.x - A.split_wgs) * NW + wave;
+                G = (gridDim.x - A.split_wgs) * NW;
                 tb = A.split_tasks;
             }
         }
-        best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, t0, G, tb, te);
+        best = mv_body<ACT, NORM, EPI, T, NP, NT>(A, L, F, t0, G, tb, te);
     } else {
         if ((int)blockIdx.x < A.split_wgs)
-            best = mv_body<ACT, NORM, EPI, T, NP>(A, L, F, blockIdx.x * kMVWaves + wave, A.split_wgs * kMVWaves, 0,
-                                                  A.split_tasks);
+            best = mv_body<ACT, NORM, EPI, T, NP, NT>(A, L, F, blockIdx.x * NW + wave, A.split_wgs * NW, 0, A.split_tasks);
         else
-            best = mv_body<ACT, NORM, EPI, T2, NP>(A, L, F, A.split_tasks + (blockIdx.x - A.split_wgs) * kMVWaves + wave,
-                                                   (gridDim.x - A.split_wgs) * kMVWaves, A.split_tasks, A.ntasks);
+            best = mv_body<ACT, NORM, EPI, T2, NP, NT>(A, L, F, A.split_tasks + (blockIdx.x - A.split_wgs) * NW + wave,
+                                                       (gridDim.x - A.split_wgs) * NW, A.split_tasks, A.ntasks);
     }
     if constexpr (EPI == EPI_LOGITS) {
         // workgroup max of the lanes' keys, then one atomic into this workgroup's slot
@@ -175,84 +175,10 @@ __global__ __launch_bounds__(kMVThreads) void k_matvec(MVArgs A) {
         if (threadIdx.x == 0) {
             unsigned long long b = red[0];
 #pragma unroll
-            for (int w = 1; w < kMVWaves; ++w) b = red[w] > b ? red[w] : b;
+            for (int w = 1; w < NW; ++w) b = red[w] > b ? red[w] : b;
             if (b) atomicMax(&A.argmax[(cur_pos & 1) * kArgSlots + blockIdx.x % kArgSlots], b);
             if (blockIdx.x == 0) A.st->pos_next = cur_pos + 1;
         }
-    }
-}
-
-// ----------------------------------------------------------------------------------
-// Burst matvec: short single-type launches (every wave owns at most 4 sub-items: the 8B
-// ffn_down, gate+up, O and single-type QKV).  The pipelined body above keeps ONE sub-item
-// in flight, so a wave with 2-4 sub-items pays the HBM latency of every sub-item after
-// the prologue (ffn_down: 14.8 us where a streaming read of its 33 MB takes 6.1,
-// profiles/r03/matvec).  Here a wave issues the loads of ALL its sub-items before the
-// activation prologue, so the launch's whole matrix is requested at t = 0 and the waves
-// compute as it lands.  N sub-items are held in registers (straight-line code, a compile-
-// time N per wave: the compiler counts vmcnt exactly and sub-item k waits only for its
-// own loads).  Tasks are dealt in contiguous runs (Bresenham: the waves of a workgroup
-// together own an equal share +-1).  Arithmetic and fold are mv_body's: bit-identical.
-// ----------------------------------------------------------------------------------
-template <int ACT, bool NORM, int EPI, int T, int NP, int N>
-__device__ __forceinline__ unsigned long long mv_burst_n(const MVArgs& A, const Lds& L, float* F, int tb) {
-    int pos = 0;
-    if constexpr (EPI == EPI_QKV) pos = A.st->pos;
-    unsigned long long best = 0;
-    const int lane = threadIdx.x & 63;
-    const TaskGeo g = task_geo(A);
-    const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
-    const int r = lane / g.lr, ul = lane - r * g.lr;
-    ProRegs<NORM, NP> R;
-    ImgRegs<2 * NP + 1> RI;
-    const bool img = A.xq != nullptr;
-    if (img) mv_img_issue<2 * NP + 1>(A, RI);
-    else mv_prologue_issue<NORM, NP>(A, R);
-    if (A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    UnitW<T> buf[N > 0 ? N : 1];
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const Sub b = sub_of<EPI>(A, g, tb + k / S, k % S);
-        const Seg sg = pick(A, b.si);
-        const LaneUnit lu = lane_unit(g, b, sg, r, ul);
-        buf[k] = load_unit<T>(sg, lu.row, lu.u, g.U);
-    }
-    if (img) mv_img_finish<2 * NP + 1>(A, L, RI);
-    else mv_prologue_finish<ACT, NORM, NP>(A, L, R);
-    __syncthreads();
-    float acc = 0.f, vg = 0.f;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const int s = k % S;
-        const Sub b = sub_of<EPI>(A, g, tb + k / S, s);
-        const Seg sg = pick(A, b.si);
-        const LaneUnit lu = lane_unit(g, b, sg, r, ul);
-        float tm[9];
-        unit_terms<T>(buf[k], L.act + (size_t)lu.u * kRec, tm);
-        sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
-    }
-    return best;
-}
-
-template <int ACT, bool NORM, int EPI, int T, int NP, int NMAX>
-__global__ __launch_bounds__(kMVThreads, 2) void k_matvec_burst(MVArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Lds L = carve(smem, ACT, A.cols);
-    const int wave = uniform((int)(threadIdx.x >> 6));
-    float* F = (float*)(smem + fold_off(ACT, A.cols, kMVWaves)) + wave * kFoldFloats;
-    const TaskGeo g = task_geo(A);
-    const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
-    const long long W = (long long)gridDim.x * kMVWaves, wv = (long long)blockIdx.x * kMVWaves + wave;
-    const int tb = (int)(wv * A.ntasks / W), te = (int)((wv + 1) * A.ntasks / W);
-    const int n = uniform((te - tb) * S);
-    // (a wave with no task still joins the prologue's workgroup barriers)
-    switch (n) {
-        case 0: mv_burst_n<ACT, NORM, EPI, T, NP, 0>(A, L, F, tb); break;
-        case 1: mv_burst_n<ACT, NORM, EPI, T, NP, 1>(A, L, F, tb); break;
-        case 2: if constexpr (NMAX >= 2) mv_burst_n<ACT, NORM, EPI, T, NP, 2>(A, L, F, tb); break;
-        case 3: if constexpr (NMAX >= 3) mv_burst_n<ACT, NORM, EPI, T, NP, 3>(A, L, F, tb); break;
-        case 4: if constexpr (NMAX >= 4) mv_burst_n<ACT, NORM, EPI, T, NP, 4>(A, L, F, tb); break;
-        default: break;
     }
 }
 
@@ -298,50 +224,57 @@ static inline double old_share() {
     }();
     return v;
 }
-// Burst launches (k_matvec_burst): on unless LLMI_MV_BURST=0 (A/B: results are identical).
-static inline int burst_max() {
+// Wide launches: ONE workgroup of 8 waves per CU instead of two of 4.  Every workgroup
+// re-derives the activation image from the f32 input (the prologue), so the chip reads
+// the activation once per workgroup: 512 x 57 KB = 29 MB beside ffn_down's 33 MB of
+// weights at 14336 columns (profiles/r03/matvec trace: the first sub-item's weights land
+// only ~6 us into the launch).  One workgroup per CU halves that traffic and shares the
+// quantization over 512 threads.  LLMI_MV_WIDE = the fewest columns that go wide
+// (0 = never); which wave reduces a row never changes a result.
+static inline int wide_cols() {
     static const int v = [] {
-        const char* e = getenv("LLMI_MV_BURST");
-        return e ? atoi(e) : 4;
+        const char* e = getenv("LLMI_MV_WIDE");
+        return e ? atoi(e) : 0;
     }();
     return v;
 }
+static inline int cu_count() {
+    static const int n = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 0;
+        return c;
+    }();
+    return n;
+}
+constexpr int kMVWide = 512;
 template <int ACT, bool NORM, int T, int EPI, int NP>
-static bool mv_try_burst(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if constexpr (EPI == EPI_LOGITS) {
-        return false;
-    } else {
-        const int bm = burst_max();
-        if (bm <= 0) return false;
+static hipError_t mv_launch_wide(const MVArgs& a, hipStream_t s) {
+    constexpr int NW = kMVWide / 64;
+    const size_t lds = fold_off(ACT, a.cols, NW) + (size_t)NW * kFoldFloats * 4;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int blocks = std::max(1, std::min(cu_count(), (a.ntasks + NW - 1) / NW));
+    launch_k(k_matvec<ACT, NORM, EPI, T, NP, T, kMVWide>, dim3(blocks), dim3(kMVWide), lds, s, true, true, a);
+    return hipGetLastError();
+}
+template <int ACT, bool NORM, int T, int EPI>
+static bool mv_try_wide(const MVArgs& a, hipStream_t s, hipError_t& e) {
+    if constexpr (EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV) {
+        const int wc = wide_cols();
+        if (wc <= 0 || a.cols < wc || cu_count() <= 0) return false;
         for (int i = 0; i < a.nseg; ++i)
-            if (a.seg[i].type != T) return false;
-        const TaskGeo tg = task_geo(a);
-        const int S = EPI == EPI_SWIGLU ? 2 * tg.nj : tg.nj;
-        auto nmax = [&](dim3 g) {
-            const long long W = (long long)g.x * kMVWaves;
-            return (int)((a.ntasks + W - 1) / W) * S;
-        };
-        auto k2 = k_matvec_burst<ACT, NORM, EPI, T, NP, 2>;
-        const dim3 g2 = resident_grid(k2, grid, lds);
-        if (nmax(g2) <= std::min(bm, 2)) {
-            launch_k(k2, g2, dim3(kMVThreads), lds, s, true, true, a);
-            return true;
-        }
-        // four sub-items per wave only where they fit in registers without scratch
-        // (gate+up of the 4096-column models: Q4_K / Q5_K, one prologue sub-block per thread)
-        if constexpr (EPI == EPI_SWIGLU && NP == 1 && (T == T_Q4_K || T == T_Q5_K)) {
-            auto k4 = k_matvec_burst<ACT, NORM, EPI, T, NP, 4>;
-            const dim3 g4 = resident_grid(k4, grid, lds);
-            if (nmax(g4) > std::min(bm, 4)) return false;
-            launch_k(k4, g4, dim3(kMVThreads), lds, s, true, true, a);
-            return true;
-        }
+            if (a.seg[i].type != T) return false;  // single-type launches only
+        const int per = (a.cols / 16 + kMVWide - 1) / kMVWide;
+        e = per <= 1 ? mv_launch_wide<ACT, NORM, T, EPI, 1>(a, s)
+            : per <= 2 ? mv_launch_wide<ACT, NORM, T, EPI, 2>(a, s) : mv_launch_wide<ACT, NORM, T, EPI, 4>(a, s);
+        return true;
+    } else {
+        (void)a; (void)s; (void)e;
         return false;
     }
 }
 template <int ACT, bool NORM, int T, int EPI, int NP>
 static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds, hipStream_t s) {
-    if (mv_try_burst<ACT, NORM, T, EPI, NP>(a0, grid, lds, s)) return hipGetLastError();
     auto k = k_matvec<ACT, NORM, EPI, T, NP>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
@@ -404,6 +337,8 @@ static inline int prologue_np(int cols) {
 
 template <int ACT, bool NORM, int T, int EPI>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (mv_try_wide<ACT, NORM, T, EPI>(a, s, e)) return e;
     switch (prologue_np(a.cols)) {
         case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
         case 2: return mv_launch<ACT, NORM, T, EPI, 2>(a, grid, lds, s);

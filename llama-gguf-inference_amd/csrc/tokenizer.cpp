@@ -316,10 +316,12 @@ std::unique_ptr<Tokenizer> Tokenizer::from_gguf(const GgufFile& f, int n_vocab_f
         for (double d : kv->arr_num) types.push_back((int)d);
     std::vector<std::string> merges;
     if (const GgufKV* kv = f.kv("tokenizer.ggml.merges")) merges = kv->arr_str;
-    return build(f.str("tokenizer.ggml.model", "llama"), f.str("tokenizer.ggml.pre", "default"), std::move(tokens),
-                 std::move(scores), std::move(types), merges, (int)f.num("tokenizer.ggml.bos_token_id", -1),
-                 (int)f.num("tokenizer.ggml.eos_token_id", -1), f.num("tokenizer.ggml.add_bos_token", 1) != 0,
-                 f.num("tokenizer.ggml.add_space_prefix", 1) != 0);
+    auto tk = build(f.str("tokenizer.ggml.model", "llama"), f.str("tokenizer.ggml.pre", "default"), std::move(tokens),
+                    std::move(scores), std::move(types), merges, (int)f.num("tokenizer.ggml.bos_token_id", -1),
+                    (int)f.num("tokenizer.ggml.eos_token_id", -1), f.num("tokenizer.ggml.add_bos_token", 1) != 0,
+                    f.num("tokenizer.ggml.add_space_prefix", 1) != 0);
+    tk->add_eos = f.num("tokenizer.ggml.add_eos_token", 0) != 0;
+    return tk;
 }
 
 // Tokenizer.tokenize: special-token partition, then each text fragment encoded

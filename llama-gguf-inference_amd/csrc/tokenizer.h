@@ -43,6 +43,7 @@ public:
     std::vector<int> types;
     int bos = -1, eos = -1;
     bool add_bos = true;
+    bool add_eos = false;  // tokenizer.ggml.add_eos_token (llama_detokenize's remove_special)
 
 private:
     void init_common();

@@ -307,13 +307,22 @@ class Replica:
                 break
         r.emit(emit)
         self.tokens += len(emit)
-        if r.stop and self.detok is not None and find_stop(self.detok(r.out), r.stop) is not None:
+        if r.stop and self.detok is not None and emit and self._stop_seen(r, len(emit)):
             r.done("stop")
             return True
         if len(r.out) >= r.max_tokens:
             r.done("length")
             return True
         return False
+
+    def _stop_seen(self, r: Request, n_new: int) -> bool:
+        """Did the n_new tokens just emitted complete a stop string?  Earlier text was
+        checked when it was new, so only a window is detokenized: the new tokens plus
+        enough older ones to hold a stop string that starts before them (every token is at
+        least one byte, so max(len(stop)) + 4 tokens cover any stop string plus a split
+        UTF-8 sequence) -- O(1) per call instead of the whole output."""
+        tail = max(len(x.encode("utf-8")) for x in r.stop) + 4
+        return find_stop(self.detok(r.out[-(n_new + tail):]), r.stop) is not None
 
     def _step(self) -> None:
         batch = self.active[:8]
@@ -322,28 +331,36 @@ class Replica:
             k = min(k, 4)  # stop strings are checked between decode calls
         c = self.ctx
         t0 = time.perf_counter()
-        if any(r.sampler is not None for r in batch):
-            # one token per call: every slot's logits (llama_decode with one token per
-            # sequence = one batched step), sampled on the host or argmax on the device
-            k = 1
-            rc = c.decode([r.last for r in batch], pos=[r.pos for r in batch], seq=[r.seq for r in batch],
-                          logits_all=True)
-            if rc != 0:
-                raise RuntimeError(f"llama_decode returned {rc}")
-            outs = [[c.greedy(i) if r.sampler is None else r.sampler.sample(c.logits(i), r.prompt + r.out)]
-                    for i, r in enumerate(batch)]
-        else:
+        greedy = [r for r in batch if r.sampler is None]
+        sampled = [r for r in batch if r.sampler is not None]
+        outs: dict[int, list[int]] = {}
+        if greedy:
+            # greedy slots decode k tokens per call with the argmax fed back on the device,
+            # whether or not sampled requests share the replica
             try:
-                outs = c.generate_greedy_batch([r.seq for r in batch], [r.last for r in batch], [r.pos for r in batch], k)
+                got = c.generate_greedy_batch([r.seq for r in greedy], [r.last for r in greedy],
+                                              [r.pos for r in greedy], k)
             except Exception:
                 # not batchable here (e.g. a context past the batched attention's bound):
                 # one sequence at a time, same results
-                outs = [c.generate_greedy_batch([r.seq], [r.last], [r.pos], k)[0] for r in batch]
+                got = [c.generate_greedy_batch([r.seq], [r.last], [r.pos], k)[0] for r in greedy]
+            for r, toks in zip(greedy, got):
+                outs[id(r)] = toks
+        if sampled:
+            # one token per call: every sampled slot's logits (llama_decode with one token
+            # per sequence = one batched step), sampled on the host
+            rc = c.decode([r.last for r in sampled], pos=[r.pos for r in sampled], seq=[r.seq for r in sampled],
+                          logits_all=True)
+            if rc != 0:
+                raise RuntimeError(f"llama_decode returned {rc}")
+            for i, r in enumerate(sampled):
+                outs[id(r)] = [r.sampler.sample(c.logits(i), r.prompt + r.out)]
         self.busy_s += time.perf_counter() - t0
         self._stats()
         done = []
-        for r, toks in zip(batch, outs):
-            r.pos += k
+        for r in batch:
+            toks = outs[id(r)]
+            r.pos += len(toks)
             r.last = toks[-1]
             if self._take(r, toks):
                 done.append(r)

@@ -53,7 +53,9 @@ const char* or_last_error(void) { return g_err; }
 
 float or_fp16_to_fp32(uint16_t h) { return llmi_h2f(h); }
 uint16_t or_fp32_to_fp16(float f) { return llmi_f2h(f); }
-float or_expf(float x) { return llmi_expf(x); }
+static inline float mode_expf(float x);
+/* exp as the softmax / SiLU use it: llmi_expf (generic), ggml_v_expf or libm expf (x86 mode) */
+float or_expf(float x) { return mode_expf(x); }
 
 size_t or_type_size(int t) {
     switch (t) {
@@ -434,10 +436,12 @@ static float vd_generic_unpacked(int wtype, int n, const RowConst* rcs, const ui
  * vendored) vectorise these dots with AVX2 maddubs/madd and accumulate the per-block
  * integer sums in 8 fp32 lanes — a different fp32 association from the generic order the
  * parity checks use.  These are written here in that style (unsigned-weights x signed-q8
- * maddubs, 16-bit scale madd, one fp32 FMA per block) so bench.py's cpu_baseline times a
- * vectorised CPU path instead of the scalar restatement.  Results agree with the generic
- * order to float rounding (tests/test_oracle_fast.py), never bit for bit; or_set_fast_dots
- * is off by default and no parity test turns it on. */
+ * maddubs, 16-bit scale madd, one fp32 FMA per block, Q4_K's 4-lane min accumulator) so
+ * bench.py's cpu_baseline times a vectorised CPU path instead of the scalar restatement;
+ * they compute exactly the x86 association mode's dots below (bit-identical,
+ * tests/test_parity_x86.py).  Results agree with the generic order to float rounding
+ * (tests/test_oracle_fast.py), never bit for bit; or_set_fast_dots is off by default and
+ * no parity test turns it on. */
 static int g_fast = 0;
 #if defined(__AVX2__) && defined(__FMA__)
 #include <immintrin.h>
@@ -455,7 +459,7 @@ static inline int kq_mins_dot(const int16_t* bsums, const uint8_t* mn) {
 static float fd_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
     const __m256i m4 = _mm256_set1_epi8(0x0F);
     __m256 acc = _mm256_setzero_ps();
-    float accm = 0.f;
+    __m128 accm4 = _mm_setzero_ps();
     for (int i = 0; i < n / QK_K; ++i) {
         uint8_t sc[8], mn[8];
         for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
@@ -469,15 +473,22 @@ static float fd_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
             const __m256i ph = _mm256_madd_epi16(_mm256_maddubs_epi16(hi, yh), _mm256_set1_epi16(sc[2 * j + 1]));
             sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
         }
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[i].d) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
-        accm += llmi_h2f(x[i].dmin) * y[i].d * (float)kq_mins_dot(y[i].bsums, mn);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * llmi_h2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
+        /* upstream's min terms: 4 lanes prod[k] = madd(mins, hadd(bsums)), FMA-accumulated */
+        const __m256i q8sums = _mm256_loadu_si256((const __m256i*)y[i].bsums);
+        const __m128i q8s = _mm_hadd_epi16(_mm256_castsi256_si128(q8sums), _mm256_extracti128_si256(q8sums, 1));
+        const __m128i mins = _mm_cvtepu8_epi16(_mm_loadl_epi64((const __m128i*)mn));
+        const __m128i prod = _mm_madd_epi16(mins, q8s);
+        accm4 = _mm_fmadd_ps(_mm_set1_ps(-y[i].d * llmi_h2f(x[i].dmin)), _mm_cvtepi32_ps(prod), accm4);
     }
-    return hsum8(acc) - accm;
+    accm4 = _mm_add_ps(accm4, _mm_movehl_ps(accm4, accm4));
+    accm4 = _mm_add_ss(accm4, _mm_movehdup_ps(accm4));
+    return hsum8(acc) + _mm_cvtss_f32(accm4);
 }
 static float fd_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
     const __m256i m4 = _mm256_set1_epi8(0x0F), b16 = _mm256_set1_epi8(0x10);
     __m256 acc = _mm256_setzero_ps();
-    float accm = 0.f;
+    float summs = 0.f;
     for (int i = 0; i < n / QK_K; ++i) {
         uint8_t sc[8], mn[8];
         for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
@@ -496,10 +507,11 @@ static float fd_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
             const __m256i ph = _mm256_madd_epi16(_mm256_maddubs_epi16(hi, yh), _mm256_set1_epi16(sc[2 * j + 1]));
             sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
         }
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[i].d) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
-        accm += llmi_h2f(x[i].dmin) * y[i].d * (float)kq_mins_dot(y[i].bsums, mn);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * llmi_h2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
+        /* upstream: one scalar summs += dmin * sum(prod), FMA-contracted (gnu11 build) */
+        summs = fmaf(-y[i].d * llmi_h2f(x[i].dmin), (float)kq_mins_dot(y[i].bsums, mn), summs);
     }
-    return hsum8(acc) - accm;
+    return hsum8(acc) + summs;
 }
 static float fd_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
     const __m256i m4 = _mm256_set1_epi8(0x0F), m2 = _mm256_set1_epi8(0x30), k32 = _mm256_set1_epi8(32);
@@ -524,7 +536,7 @@ static float fd_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
                 sumi = _mm256_add_epi32(sumi, _mm256_madd_epi16(p, s));
             }
         }
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[i].d) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * llmi_h2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
     }
     return hsum8(acc);
 }

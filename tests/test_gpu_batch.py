@@ -2,7 +2,7 @@
 context advance together, each batched step streaming every weight byte once for all
 of them.  The bar is the same as for single-sequence decode: every sequence's logits and
 greedy tokens are BIT-IDENTICAL to decoding that sequence alone (which in turn is
-bit-identical to the device-order oracle, tests/test_gpu_decode.py) — the batched
+bit-identical to the generic-order oracle, tests/test_gpu_decode.py) — the batched
 matvec forms each token's integer dots and fp32 reductions in the single-token order.
 
 Covered: slot counts 1..8 (3, 5, 6, 7 run padded to 4 / 8 with a dummy sequence),
@@ -182,7 +182,7 @@ def test_batched_real_widths(gpu, synth_dir, preset, n_vocab):
                                        ("mistral7b-q6k", 8)])
 def test_bmm_any_batch_size(gpu, synth_dir, monkeypatch, preset, k):
     """The matrix-core batched matvec (batch.hip k_bmm) forced for every batch size
-    (LLMI_BMM_MIN=1; by default it takes 8-token steps): each sequence's tokens and
+    (LLMI_BMM_MIN=1; by default it takes steps of 5 or more tokens): each sequence's tokens and
     logits equal its single-sequence decode at real widths, Q4_K / Q5_K / Q6_K."""
     monkeypatch.setenv("LLMI_BMM_MIN", "1")
     path = str(synth_dir / f"{preset}-batch-L2.gguf")

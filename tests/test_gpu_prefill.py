@@ -1,11 +1,11 @@
 """Batched MFMA prefill (prefill.hip.inc) through the C ABI.
 
 The prompt's leading tokens run through every layer as one launch per op over all of
-them: q8 activations x quantized weights on v_mfma_i32_32x32x16_i8 (exact int32 sub-block
-sums), combined in fp32 exactly as the matvec does and accumulated in the matvec's
-device order.  The bar is therefore BIT-IDENTITY with T decode steps, which are
-themselves bit-identical to the oracle's device order (test_gpu_decode.py):
-- last-token logits of a batched prompt == the oracle's (device order), bit for bit;
+them: q8 activations x quantized weights on v_mfma_f32_16x16x32_f16 (exact integer sums
+per residue class), combined in fp32 exactly as the matvec does, in ggml's generic
+order.  The bar is therefore BIT-IDENTITY with T decode steps, which are
+themselves bit-identical to the oracle's generic order (test_gpu_decode.py):
+- last-token logits of a batched prompt == the oracle's (generic order), bit for bit;
 - the KV cache the prefill wrote: greedy continuation identical, logits bit-identical;
 - prefill vs decode-step prompt processing (LLMI_NO_PREFILL=1) bit-identical at the
   real widths (8B / TinyLlama / Mistral / 70B, 2 layers), across the 512-token ubatch
@@ -135,7 +135,7 @@ def test_prefill_ubatch_boundary(gpu, tiny_models, monkeypatch):
 @pytest.mark.parametrize("no_prefill", [False, True])
 def test_long_context_vs_oracle(gpu, tiny_models, monkeypatch, preset, n_prompt, no_prefill):
     """Hundreds of positions: the prompt (batched prefill, or one decode step per token)
-    and 4 continuation steps bit-identical to the oracle (device order)."""
+    and 4 continuation steps bit-identical to the oracle (generic order)."""
     path = tiny_models[preset]
     rng = np.random.default_rng(5 + n_prompt)
     prompt = [1] + [int(t) for t in rng.integers(3, 700, n_prompt - 1)]
