@@ -14,8 +14,9 @@ fresh 128-token prompt.
 
 Multi-GPU (`torch.distributed.run --nproc-per-node N`): replicas only — each rank
 decodes its own stream (prompt seed 4+rank) with no data-path collective; rank 0's
-weights are fanned out to the other ranks by one RCCL broadcast over xGMI
-(llmi_model_fanout), outside the timed region.  value = N*K / max-over-ranks time.
+weights are fanned out to the other ranks by RCCL broadcasts over xGMI
+(llmi_model_load_fanout: 256 MB pieces pipelined behind rank 0's upload), outside the
+timed region.  value = N*K / max-over-ranks time.
 
 Synthetic data: a GGUF with the exact Llama-3-8B Q4_K_M shapes and type table,
 random-init blocks (llmi_synth.h); there is no network for real checkpoints.
@@ -140,16 +141,19 @@ def timed_decode(engine, dist: Dist, steps: int, warmup: int) -> tuple[float, fl
     return dt, dist.max(dt)
 
 
-def replica_fanout(model, dist: Dist, rccl_unique_id) -> float:
-    """Rank 0's weight arena to every rank's replica: rank 0 makes the
-    RCCL unique id, the torch.distributed group broadcasts it, and every rank joins the
-    one RCCL broadcast over xGMI (llmi_model_fanout).  Returns this rank's seconds."""
+def load_replica(path: str, dist: Dist, rccl_unique_id, load_fanout, load_plain):
+    """This rank's replica of the model.  One rank: load_plain(path, gpu).
+    Several: rank 0 makes the RCCL unique id, the torch.distributed group broadcasts it,
+    and every rank calls load_fanout(path, gpu, uid, nranks, rank) (llmi_model_load_fanout):
+    rank 0 uploads the GGUF and the arena reaches the other ranks over xGMI in 256 MB
+    pieces pipelined behind that upload.  Returns (model, fan-out seconds of this rank,
+    0.0 on one rank)."""
     if dist.world <= 1:
-        return 0.0
+        return load_plain(path, dist.local_rank), 0.0
     uid = dist.bcast_bytes(rccl_unique_id() if dist.rank == 0 else None)
     t = time.perf_counter()
-    model.fanout(uid, dist.world, dist.rank)
-    return time.perf_counter() - t
+    m = load_fanout(path, dist.local_rank, uid, dist.world, dist.rank)
+    return m, time.perf_counter() - t
 
 
 class LlmiEngine:
@@ -175,9 +179,9 @@ class LlmiEngine:
         self.path = path
         self.gate_type = GATE_TYPE.get(args.preset, "?")
         t = time.perf_counter()
-        self.model = llmi.Model(path, main_gpu=dist.local_rank, no_upload=dist.rank != 0)
+        self.model, self.fanout_s = load_replica(path, dist, llmi.rccl_unique_id, llmi.Model.load_fanout,
+                                                 lambda p, g: llmi.Model(p, main_gpu=g))
         self.load_s = time.perf_counter() - t
-        self.fanout_s = replica_fanout(self.model, dist, llmi.rccl_unique_id)
         last = window_start(args.prompt, args.steps, args.warmup) + args.steps
         n_ctx = ((max(last, args.prompt + C2_DECODE) + args.profile_steps + 2 + 255) // 256) * 256
         self.ctx = llmi.Context(self.model, n_ctx=n_ctx, use_graphs=not args.eager)

@@ -221,6 +221,22 @@ int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_
 int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n);
 int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank);
 
+/* Load + fan-out in one call, the broadcast pipelined behind the upload:
+ * the arena goes out in 256 MB pieces, piece k as soon as the upload has completed the
+ * arena prefix covering it.  llmi_model_load_fanout: every rank calls it with the same
+ * RCCL unique id; rank 0 reads and uploads the GGUF, the others only plan the layout and
+ * receive.  llmi_model_load_replicated: one process, the model on params.main_gpu plus a
+ * replica on each of `devices` (out[i]), as llmi_replicate.  NULL on error. */
+struct llama_model* llmi_model_load_fanout(const char* path, struct llama_model_params params, const uint8_t* uid,
+                                           int32_t nranks, int32_t rank);
+struct llama_model* llmi_model_load_replicated(const char* path, struct llama_model_params params,
+                                               const int32_t* devices, int32_t n, struct llama_model** out);
+/* The fan-out schedule (engine.cpp fanout_plan; host only, for tests): pieces of `chunk`
+ * bytes over an arena of arena_bytes; ready[k] = the index of the first upload prefix
+ * (prefix_ends, ascending) that covers piece k.  Returns the number of pieces. */
+int32_t llmi_fanout_plan(uint64_t arena_bytes, uint64_t chunk, const uint64_t* prefix_ends, int32_t n_prefix,
+                         int32_t* ready, int32_t max_pieces);
+
 /* A tokenizer-only vocabulary handle from a GGUF's tokenizer.* metadata (no tensors
  * or device needed); free with llmi_vocab_free (handles from llama_model_get_vocab are
  * owned by their model).  NULL on error. */

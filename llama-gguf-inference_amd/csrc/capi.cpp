@@ -660,66 +660,201 @@ int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64
     return 0;
 }
 
+// ---- replica fan-out ------------------------------------------------
+// The arena goes out in kFanoutChunk (256 MB) pieces on real streams.  When the source is
+// still uploading (llmi_model_load_fanout / llmi_model_load_replicated), piece k is issued
+// as soon as the upload stream has completed the arena prefix that covers it (an event on
+// the upload stream, waited on by the broadcast streams), so the xGMI broadcast runs
+// behind the host-to-device copy instead of after it.  engine.cpp fanout_plan states the
+// schedule; tests/test_fanout_plan.py checks it.
+namespace {
+struct Fanout {
+    // one rank per entry: (device, arena, comm, stream); entry 0 is the root
+    std::vector<int> dev;
+    std::vector<uint8_t*> buf;
+    std::vector<ncclComm_t> comm;
+    std::vector<hipStream_t> st;
+    size_t bytes = 0, next = 0;  // arena bytes; first piece not yet issued
+    std::vector<hipEvent_t> evs;
+    bool ok = true;
+
+    ~Fanout() {
+        for (size_t r = 0; r < st.size(); ++r) {
+            (void)hipSetDevice(dev[r]);
+            if (st[r]) (void)hipStreamSynchronize(st[r]);
+        }
+        for (size_t r = 0; r < comm.size(); ++r)
+            if (comm[r]) ncclCommDestroy(comm[r]);
+        for (size_t r = 0; r < st.size(); ++r) {
+            (void)hipSetDevice(dev[r]);
+            if (st[r]) (void)hipStreamDestroy(st[r]);
+        }
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+    }
+    bool make_streams() {
+        st.assign(dev.size(), nullptr);
+        for (size_t r = 0; r < dev.size(); ++r) {
+            if (hipSetDevice(dev[r]) != hipSuccess) return false;
+            if (hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking) != hipSuccess) return false;
+        }
+        return true;
+    }
+    // issue every piece that ends at or before `prefix` (all of them if prefix >= bytes);
+    // `wait`: an event on the root's upload stream the broadcast streams wait on first
+    bool issue(size_t prefix, hipEvent_t wait) {
+        bool waited = false;
+        while (ok && next * kFanoutChunk < bytes) {
+            const size_t off = next * kFanoutChunk, len = std::min(kFanoutChunk, bytes - off);
+            if (off + len > prefix) break;
+            if (wait && !waited) {
+                for (size_t r = 0; r < dev.size(); ++r) {
+                    (void)hipSetDevice(dev[r]);
+                    if (hipStreamWaitEvent(st[r], wait, 0) != hipSuccess) ok = false;
+                }
+                waited = true;
+            }
+            ncclResult_t nr = dev.size() > 1 ? ncclGroupStart() : ncclSuccess;
+            for (size_t r = 0; r < dev.size() && nr == ncclSuccess; ++r) {
+                (void)hipSetDevice(dev[r]);
+                nr = ncclBroadcast(buf[r] + off, buf[r] + off, len, ncclUint8, 0, comm[r], st[r]);
+            }
+            if (dev.size() > 1) {
+                const ncclResult_t ne = ncclGroupEnd();
+                if (nr == ncclSuccess) nr = ne;
+            }
+            if (nr != ncclSuccess) ok = false;
+            ++next;
+        }
+        return ok;
+    }
+    bool finish() {
+        issue(bytes, nullptr);
+        for (size_t r = 0; r < dev.size(); ++r) {
+            (void)hipSetDevice(dev[r]);
+            if (hipStreamSynchronize(st[r]) != hipSuccess) ok = false;
+        }
+        return ok;
+    }
+    // the model_load hook of the root: record the prefix on the upload stream, issue what it covers
+    UploadHook hook() {
+        return [this](size_t prefix_end, hipStream_t us) -> bool {
+            hipEvent_t e = nullptr;
+            (void)hipSetDevice(dev[0]);
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return ok = false;
+            evs.push_back(e);
+            if (hipEventRecord(e, us) != hipSuccess) return ok = false;
+            const bool r = issue(prefix_end, e);
+            (void)hipSetDevice(dev[0]);
+            return r;
+        };
+    }
+};
+
+bool check_replica_devices(int src, const int32_t* devices, int32_t n, const char* who) {
+    const int nd = llmi_device_count();
+    std::vector<int> seen{src};
+    for (int i = 0; i < n; ++i) {
+        if (devices[i] < 0 || devices[i] >= nd) { set_err(std::string(who) + ": device index out of range"); return false; }
+        if (std::find(seen.begin(), seen.end(), devices[i]) != seen.end()) {
+            set_err(std::string(who) + ": device " + std::to_string(devices[i]) +
+                    " listed twice (or the source model's own device)");
+            return false;
+        }
+        seen.push_back(devices[i]);
+    }
+    return true;
+}
+
+// in-process replicas: layouts on `devices`, one communicator over {src, devices...}
+bool replica_setup(const Model& src, const int32_t* devices, int32_t n, std::vector<llama_model*>& reps, Fanout& F,
+                   std::string& err) {
+    reps.assign((size_t)n, nullptr);
+    for (int i = 0; i < n; ++i) {
+        reps[(size_t)i] = new llama_model();
+        if (!model_clone_layout(src, devices[i], reps[(size_t)i]->m, err)) return false;
+    }
+    F.dev.push_back(src.device);
+    F.buf.push_back(src.arena);
+    for (int i = 0; i < n; ++i) {
+        F.dev.push_back(devices[i]);
+        F.buf.push_back(reps[(size_t)i]->m.arena);
+    }
+    F.bytes = src.arena_bytes;
+    F.comm.assign(F.dev.size(), nullptr);
+    if (ncclCommInitAll(F.comm.data(), (int)F.dev.size(), F.dev.data()) != ncclSuccess) {
+        F.comm.clear();
+        err = "ncclCommInitAll failed";
+        return false;
+    }
+    if (!F.make_streams()) { err = "replica streams"; return false; }
+    return true;
+}
+}  // namespace
+
 int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_t n, struct llama_model** out) {
     API_TRY
     if (!model || !devices || n <= 0 || !out) { set_err("llmi_replicate: bad arguments"); return -1; }
     // one RCCL rank per device: a device listed twice (or the source's own device) would
     // put two ranks of the communicator on one GPU
-    {
-        const int nd = llmi_device_count();
-        std::vector<int> seen{model->m.device};
-        for (int i = 0; i < n; ++i) {
-            if (devices[i] < 0 || devices[i] >= nd) { set_err("llmi_replicate: device index out of range"); return -1; }
-            if (std::find(seen.begin(), seen.end(), devices[i]) != seen.end()) {
-                set_err("llmi_replicate: device " + std::to_string(devices[i]) +
-                        " listed twice (or the source model's own device)");
-                return -1;
-            }
-            seen.push_back(devices[i]);
-        }
-    }
-    std::vector<llama_model*> reps((size_t)n, nullptr);
+    if (!check_replica_devices(model->m.device, devices, n, "llmi_replicate")) return -1;
+    std::vector<llama_model*> reps;
     std::string err;
-    for (int i = 0; i < n; ++i) {
-        reps[(size_t)i] = new llama_model();
-        if (!model_clone_layout(model->m, devices[i], reps[(size_t)i]->m, err)) {
-            set_err("llmi_replicate: " + err);
-            for (auto* r : reps) delete r;
-            return -2;
-        }
+    int rc = 0;
+    {
+        Fanout F;
+        if (!replica_setup(model->m, devices, n, reps, F, err)) rc = -2;
+        else if (!F.finish()) { err = "ncclBroadcast failed"; rc = -4; }
     }
-    // one communicator over {source device, replicas...}; rank 0 broadcasts the arena
-    std::vector<int> devs;
-    devs.push_back(model->m.device);
-    for (int i = 0; i < n; ++i) devs.push_back(devices[i]);
-    std::vector<ncclComm_t> comms(devs.size());
-    if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
-        set_err("ncclCommInitAll failed");
+    if (rc) {
+        set_err("llmi_replicate: " + err);
         for (auto* r : reps) delete r;
-        return -3;
-    }
-    const size_t bytes = model->m.arena_bytes;
-    ncclResult_t nr = ncclGroupStart();
-    for (size_t r = 0; r < devs.size() && nr == ncclSuccess; ++r) {
-        (void)hipSetDevice(devs[r]);
-        void* buf = r == 0 ? (void*)model->m.arena : (void*)reps[r - 1]->m.arena;
-        nr = ncclBroadcast(buf, buf, bytes, ncclUint8, 0, comms[r], nullptr);
-    }
-    if (nr == ncclSuccess) nr = ncclGroupEnd();
-    else (void)ncclGroupEnd();
-    for (size_t r = 0; r < devs.size(); ++r) {
-        (void)hipSetDevice(devs[r]);
-        (void)hipDeviceSynchronize();
-        ncclCommDestroy(comms[r]);
-    }
-    if (nr != ncclSuccess) {
-        set_err("ncclBroadcast failed");
-        for (auto* r : reps) delete r;
-        return -4;
+        return rc;
     }
     for (int i = 0; i < n; ++i) out[i] = reps[(size_t)i];
     return 0;
     API_CATCH(-5)
+}
+
+struct llama_model* llmi_model_load_replicated(const char* path, struct llama_model_params params, const int32_t* devices,
+                                               int32_t n, struct llama_model** out) {
+    API_TRY
+    if (!path || (n > 0 && (!devices || !out)) || n < 0 || params.vocab_only || params.no_upload) {
+        set_err("llmi_model_load_replicated: bad arguments");
+        return nullptr;
+    }
+    const int nd = llmi_device_count();
+    if (nd <= 0) { set_err("no HIP device visible"); return nullptr; }
+    if (params.main_gpu < 0 || params.main_gpu >= nd) { set_err("main_gpu out of range"); return nullptr; }
+    if (!check_replica_devices(params.main_gpu, devices, n, "llmi_model_load_replicated")) return nullptr;
+    auto* m = new llama_model();
+    std::string err;
+    // the layout first (no upload), then the replicas and the communicator, then the
+    // upload with the pieces going out behind it
+    if (!model_load(path, params.main_gpu, false, true, m->m, err)) {
+        set_err(err);
+        delete m;
+        return nullptr;
+    }
+    std::vector<llama_model*> reps;
+    bool ok = true;
+    {
+        Fanout F;
+        if (n > 0) ok = replica_setup(m->m, devices, n, reps, F, err);
+        if (ok) {
+            const UploadHook h = F.hook();
+            ok = model_upload(m->m, err, n > 0 ? &h : nullptr);
+            if (ok && n > 0 && !F.finish()) { err = "ncclBroadcast failed"; ok = false; }
+        }
+    }
+    if (!ok) {
+        set_err("llmi_model_load_replicated: " + err);
+        for (auto* r : reps) delete r;
+        delete m;
+        return nullptr;
+    }
+    for (int i = 0; i < n; ++i) out[i] = reps[(size_t)i];
+    return m;
+    API_CATCH(nullptr)
 }
 
 int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n) {
@@ -730,6 +865,25 @@ int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n) {
     return 0;
 }
 
+namespace {
+bool proc_fanout_init(Fanout& F, const Model& m, const uint8_t* uid, int32_t nranks, int32_t rank) {
+    (void)hipSetDevice(m.device);
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof id);
+    F.dev = {m.device};
+    F.buf = {m.arena};
+    F.bytes = m.arena_bytes;
+    F.comm.assign(1, nullptr);
+    if (ncclCommInitRank(&F.comm[0], nranks, id, rank) != ncclSuccess) {
+        F.comm.clear();
+        set_err("ncclCommInitRank failed");
+        return false;
+    }
+    if (!F.make_streams()) { set_err("fan-out stream"); return false; }
+    return true;
+}
+}  // namespace
+
 int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank) {
     API_TRY
     if (!model || !uid || nranks <= 0 || rank < 0 || rank >= nranks || !model->m.arena) {
@@ -737,19 +891,63 @@ int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t
         return -1;
     }
     if (nranks == 1) return 0;
-    (void)hipSetDevice(model->m.device);
-    ncclUniqueId id;
-    std::memcpy(&id, uid, sizeof id);
-    ncclComm_t comm;
-    if (ncclCommInitRank(&comm, nranks, id, rank) != ncclSuccess) { set_err("ncclCommInitRank failed"); return -2; }
-    hipStream_t s;
-    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    ncclResult_t r = ncclBroadcast(model->m.arena, model->m.arena, model->m.arena_bytes, ncclUint8, 0, comm, s);
-    hipError_t e = hipStreamSynchronize(s);
-    (void)hipStreamDestroy(s);
-    ncclCommDestroy(comm);
-    if (r != ncclSuccess || e != hipSuccess) { set_err("llmi_model_fanout: broadcast failed"); return -3; }
+    Fanout F;
+    if (!proc_fanout_init(F, model->m, uid, nranks, rank)) return -2;
+    if (!F.finish()) { set_err("llmi_model_fanout: broadcast failed"); return -3; }
     return 0;
+    API_CATCH(-5)
+}
+
+struct llama_model* llmi_model_load_fanout(const char* path, struct llama_model_params params, const uint8_t* uid,
+                                           int32_t nranks, int32_t rank) {
+    API_TRY
+    if (!path || !uid || nranks <= 0 || rank < 0 || rank >= nranks || params.vocab_only) {
+        set_err("llmi_model_load_fanout: bad arguments");
+        return nullptr;
+    }
+    const int nd = llmi_device_count();
+    if (nd <= 0) { set_err("no HIP device visible"); return nullptr; }
+    if (params.main_gpu < 0 || params.main_gpu >= nd) { set_err("main_gpu out of range"); return nullptr; }
+    auto* m = new llama_model();
+    std::string err;
+    if (!model_load(path, params.main_gpu, false, true, m->m, err)) {
+        set_err(err);
+        delete m;
+        return nullptr;
+    }
+    bool ok = true;
+    if (nranks > 1) {
+        Fanout F;
+        ok = proc_fanout_init(F, m->m, uid, nranks, rank);
+        if (ok && rank == 0) {
+            const UploadHook h = F.hook();
+            ok = model_upload(m->m, err, &h);
+            if (!ok) set_err(err);
+        }
+        // every piece is issued even after a failed upload: the other ranks are blocked in
+        // their matching broadcasts and would otherwise never return
+        if (!F.comm.empty() && !F.finish() && ok) { set_err("llmi_model_load_fanout: broadcast failed"); ok = false; }
+    } else {
+        ok = model_upload(m->m, err, nullptr);
+        if (!ok) set_err(err);
+    }
+    if (!ok) {
+        delete m;
+        return nullptr;
+    }
+    return m;
+    API_CATCH(nullptr)
+}
+
+int32_t llmi_fanout_plan(uint64_t arena_bytes, uint64_t chunk, const uint64_t* prefix_ends, int32_t n_prefix,
+                         int32_t* ready, int32_t max_pieces) {
+    if (n_prefix < 0 || (n_prefix > 0 && !prefix_ends) || max_pieces < 0 || (max_pieces > 0 && !ready)) return -1;
+    API_TRY
+    std::vector<size_t> pe(prefix_ends, prefix_ends + n_prefix);
+    std::vector<int> rd;
+    const size_t n = fanout_plan((size_t)arena_bytes, (size_t)chunk, pe, rd);
+    for (size_t k = 0; k < n && (int32_t)k < max_pieces; ++k) ready[k] = rd[k];
+    return (int32_t)n;
     API_CATCH(-5)
 }
 

@@ -98,7 +98,31 @@ double bytes_per_token(const Model& m, int n_kv) {
     return b;
 }
 
-bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& M, std::string& err) {
+// end of a matrix's planes in the arena (plan_planes)
+static size_t region_end(const DevMat& m) {
+    const size_t nblk = (size_t)m.rows * (size_t)(m.cols / block_elems(m.type));
+    switch (m.type) {
+        case T_Q4_K: case T_Q5_K: return m.off_s + nblk * 16;
+        case T_Q6_K: case T_Q8_0: return m.off_d + nblk * 2;
+        default: return m.off_a + m.bytes;
+    }
+}
+
+size_t fanout_plan(size_t arena_bytes, size_t chunk, const std::vector<size_t>& prefix_ends, std::vector<int>& ready) {
+    ready.clear();
+    if (chunk == 0 || arena_bytes == 0) return 0;
+    const size_t n = (arena_bytes + chunk - 1) / chunk;
+    size_t e = 0;
+    for (size_t k = 0; k < n; ++k) {
+        const size_t end = std::min((k + 1) * chunk, arena_bytes);
+        while (e < prefix_ends.size() && prefix_ends[e] < end) ++e;
+        ready.push_back(e < prefix_ends.size() ? (int)e : (int)prefix_ends.size() - 1);
+    }
+    return n;
+}
+
+bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& M, std::string& err,
+                const UploadHook* hook) {
     M.path = path;
     M.device = device;
     M.file = std::make_shared<GgufFile>();
@@ -201,6 +225,17 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
     HIPC(hipMalloc(&M.arena, M.arena_bytes));
     M.owns_arena = true;
     if (no_upload) return true;
+    return model_upload(M, err, hook);
+}
+
+// The chunked H2D + on-device repack of every tensor into the planned arena (the model's
+// GGUF stays mapped in M.file).  `hook` (replica fan-out) sees the arena prefix grow.
+bool model_upload(Model& M, std::string& err, const UploadHook* hook) {
+    if (!M.file || !M.arena) { err = "model_upload: no layout"; return false; }
+    GgufFile& f = *M.file;
+    const HParams& hp = M.hp;
+    const bool tied = f.tensor("output.weight") == nullptr;
+    if (hipSetDevice(M.device) != hipSuccess) { err = "hipSetDevice"; return false; }
     (void)hipGetLastError();  // launch_repack reports hipGetLastError: start from a clean slate
     // ---- upload: H2D + on-device repack of the unaligned block types ----
     struct Item { const GgufTensor* t; DevMat* m; };
@@ -306,6 +341,10 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
             }
         }
         if (e != hipSuccess) { err = "upload of " + it.t->name + ": " + hip_err(e); ok = false; break; }
+        if (hook) {
+            const size_t end = &it == &items.back() ? M.arena_bytes : region_end(m);
+            if (!(*hook)(end, us)) { err = "upload: fan-out failed"; ok = false; break; }
+        }
     }
     if (ok) {
         e = hipStreamSynchronize(us);

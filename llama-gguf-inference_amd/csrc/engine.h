@@ -8,6 +8,8 @@
 #include <string>
 #include <vector>
 
+#include <functional>
+
 #include "common.h"
 #include "gguf.h"
 #include "kernels.h"
@@ -122,7 +124,21 @@ struct Context {
 };
 
 // all return false and set err on failure
-bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& m, std::string& err);
+// Upload progress hook (replica fan-out pipelined behind the H2D): called
+// after each tensor's chunks are enqueued on the upload stream `us` with the end of the
+// arena prefix that is complete once `us` reaches that point (tensors are planned in
+// upload order, so the prefix grows monotonically); false aborts the load.
+using UploadHook = std::function<bool(size_t prefix_end, hipStream_t us)>;
+bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& m, std::string& err,
+                const UploadHook* hook = nullptr);
+// the upload half of model_load (after a load with no_upload)
+bool model_upload(Model& m, std::string& err, const UploadHook* hook = nullptr);
+
+// Fan-out pieces of an arena: [k * chunk, min((k + 1) * chunk, arena_bytes)).  Piece k is
+// issued after the first upload event whose prefix covers its end; ready[k] = index of
+// that event in prefix_ends (ascending).  Returns the number of pieces.
+size_t fanout_plan(size_t arena_bytes, size_t chunk, const std::vector<size_t>& prefix_ends, std::vector<int>& ready);
+constexpr size_t kFanoutChunk = 256u << 20;  // 256 MB broadcasts behind the upload
 bool context_init(Model* m, int n_ctx, bool use_graphs, int n_seq, Context& c, std::string& err);
 // point the single-sequence paths (step_run, prefill_enqueue, state) at sequence s
 void context_select_seq(Context& c, int s);

@@ -46,6 +46,19 @@ def device_count() -> int:
     return int(lib().llmi_device_count())
 
 
+def fanout_plan(arena_bytes: int, chunk: int, prefix_ends: Sequence[int]) -> list[int]:
+    """The replica fan-out schedule (engine.cpp fanout_plan): for each chunk-sized piece of
+    the arena, the index of the first upload prefix that covers it.  Host only."""
+    n = len(prefix_ends)
+    pe = (C.c_uint64 * max(1, n))(*prefix_ends)
+    cap = (arena_bytes + chunk - 1) // chunk if chunk else 0
+    rd = (C.c_int32 * max(1, cap))()
+    k = lib().llmi_fanout_plan(int(arena_bytes), int(chunk), pe, n, rd, int(cap))
+    if k < 0:
+        raise LlmiError("llmi_fanout_plan: bad arguments")
+    return [int(rd[i]) for i in range(k)]
+
+
 def write_synthetic_gguf(path: str, preset: str, seed: int = 3, n_layer: int = 0, n_vocab: int = 0,
                          n_threads: int = 0) -> int:
     """Write a synthetic GGUF with the exact shapes/type table of `preset`."""
@@ -156,6 +169,34 @@ class Model:
         buf = C.create_string_buffer(256)
         L.llama_model_desc(self._h, buf, 256)
         self.desc = buf.value.decode()
+
+    @classmethod
+    def load_fanout(cls, path: str, main_gpu: int, uid: bytes, nranks: int, rank: int) -> "Model":
+        """Load with the replica fan-out pipelined behind the upload (llmi_model_load_fanout,
+        SURVEY.md §8e): every rank calls it with the same RCCL unique id; rank 0 uploads the
+        GGUF, the others receive the arena in 256 MB pieces over xGMI."""
+        L = lib()
+        p = L.llama_model_default_params()
+        p.main_gpu = main_gpu
+        h = L.llmi_model_load_fanout(path.encode(), p, uid, int(nranks), int(rank))
+        if not h:
+            raise LlmiError(last_error())
+        return cls._from_handle(h, path, main_gpu)
+
+    @classmethod
+    def load_replicated(cls, path: str, main_gpu: int, devices: Sequence[int]) -> tuple["Model", list["Model"]]:
+        """One process: the model on main_gpu and a replica on each of `devices`, the RCCL
+        broadcast pipelined behind the upload (llmi_model_load_replicated)."""
+        L = lib()
+        p = L.llama_model_default_params()
+        p.main_gpu = main_gpu
+        n = len(devices)
+        devs = (C.c_int32 * max(1, n))(*devices)
+        out = (C.c_void_p * max(1, n))()
+        h = L.llmi_model_load_replicated(path.encode(), p, devs, n, out)
+        if not h:
+            raise LlmiError(last_error())
+        return cls._from_handle(h, path, main_gpu), [cls._from_handle(out[i], path, devices[i]) for i in range(n)]
 
     @classmethod
     def _from_handle(cls, h, path: str, device: int) -> "Model":

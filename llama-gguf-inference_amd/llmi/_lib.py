@@ -111,6 +111,11 @@ SIGNATURES = {
     "llmi_replicate": (C.c_int32, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_void_p)]),
     "llmi_rccl_unique_id": (C.c_int32, [C.c_char_p, C.c_int32]),
     "llmi_model_fanout": (C.c_int32, [_P, C.c_char_p, C.c_int32, C.c_int32]),
+    "llmi_model_load_fanout": (_P, [C.c_char_p, llama_model_params, C.c_char_p, C.c_int32, C.c_int32]),
+    "llmi_model_load_replicated": (_P, [C.c_char_p, llama_model_params, C.POINTER(C.c_int32), C.c_int32,
+                                        C.POINTER(C.c_void_p)]),
+    "llmi_fanout_plan": (C.c_int32, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_int32,
+                                     C.POINTER(C.c_int32), C.c_int32]),
     "llmi_synth_write_gguf": (C.c_int64, [C.c_char_p, C.c_char_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32]),
     "llmi_device_layout_bytes": (C.c_int64, [C.c_int32, C.c_int64, C.c_int64]),
     "llmi_repack": (C.c_int32, [C.c_int32, _P, _P, C.c_int64, C.c_int64]),

@@ -419,8 +419,11 @@ class Engine:
                 import llmi
                 from . import tokenizer as T
 
-                m0 = llmi.Model(self.path, n_gpu_layers=self.ngl, main_gpu=self.devices[0])
-                models = [m0] + (m0.replicate(self.devices[1:]) if len(self.devices) > 1 else [])
+                if len(self.devices) > 1:  # replicas: RCCL pieces pipelined behind the upload
+                    m0, reps = llmi.Model.load_replicated(self.path, self.devices[0], self.devices[1:])
+                else:
+                    m0, reps = llmi.Model(self.path, n_gpu_layers=self.ngl, main_gpu=self.devices[0]), []
+                models = [m0] + reps
                 self._models = models
                 ctxs = [llmi.Context(m, n_ctx=self.n_ctx, n_seq=self.slots) for m in models]
                 self.n_ctx = ctxs[0].n_ctx

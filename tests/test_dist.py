@@ -80,14 +80,19 @@ def test_two_rank_timed_region_gloo():
     assert uid0 == uid1 == b"unique-id-from-rank0"
 
 
-class StubModel:
-    """Records the llmi_model_fanout call a replica makes (no GPU, no RCCL)."""
+class StubLoader:
+    """Records how bench.load_replica loads this rank's replica (no GPU, no RCCL)."""
 
     def __init__(self):
         self.calls = []
 
-    def fanout(self, uid, nranks, rank):
-        self.calls.append((uid, nranks, rank))
+    def fanout(self, path, gpu, uid, nranks, rank):
+        self.calls.append(("fanout", path, gpu, uid, nranks, rank))
+        return "model"
+
+    def plain(self, path, gpu):
+        self.calls.append(("plain", path, gpu))
+        return "model"
 
 
 def _fanout_worker(rank, world, port, q):
@@ -103,17 +108,17 @@ def _fanout_worker(rank, world, port, q):
         made.append(rank)
         return b"rccl-uid-" + bytes([7] * 8)
 
-    m = StubModel()
-    s = bench.replica_fanout(m, d, uid_fn)
-    q.put((rank, made, m.calls, s >= 0))
+    ld = StubLoader()
+    m, s = bench.load_replica("/x.gguf", d, uid_fn, ld.fanout, ld.plain)
+    q.put((rank, made, ld.calls, m == "model" and s >= 0))
     d.close()
 
 
 @pytest.mark.timeout(120)
 def test_replica_fanout_call_sequence_gloo():
     """bench.py's weight fan-out at world size 2: only rank 0 creates the RCCL unique id,
-    both ranks receive the same bytes over the process group and call llmi_model_fanout
-    once with (uid, nranks=2, their rank)."""
+    both ranks receive the same bytes over the process group and load through
+    llmi_model_load_fanout once with (path, their GPU, uid, nranks=2, their rank)."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -127,4 +132,18 @@ def test_replica_fanout_call_sequence_gloo():
     (r0, made0, calls0, ok0), (r1, made1, calls1, ok1) = res
     assert made0 == [0] and made1 == []
     uid = b"rccl-uid-" + bytes([7] * 8)
-    assert calls0 == [(uid, 2, 0)] and calls1 == [(uid, 2, 1)] and ok0 and ok1
+    assert calls0 == [("fanout", "/x.gguf", 0, uid, 2, 0)] and calls1 == [("fanout", "/x.gguf", 1, uid, 2, 1)]
+    assert ok0 and ok1
+
+
+def test_single_rank_loads_plain():
+    """One rank: no RCCL id, no fan-out, a plain load on LOCAL_RANK's GPU."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class D:
+        world, rank, local_rank = 1, 0, 0
+
+    ld = StubLoader()
+    m, s = bench.load_replica("/x.gguf", D(), lambda: pytest.fail("no uid on one rank"), ld.fanout, ld.plain)
+    assert m == "model" and s == 0.0 and ld.calls == [("plain", "/x.gguf", 0)]

@@ -66,3 +66,29 @@ def test_bmm_on_replica_device(synth_dir, monkeypatch):
     m.close()
     for s in range(8):
         assert [firsts[s]] + got[s] == want[s], f"seq {s}"
+
+
+@pytest.mark.gpu
+def test_pipelined_loaders_single_device_equal_plain_load():
+    """llmi_model_load_fanout at one rank and llmi_model_load_replicated with no replica
+    take the same upload path (model_upload) as llama_model_load_from_file: a decode on
+    each gives bit-identical logits and greedy tokens.  (The RCCL pieces themselves need
+    two GPUs: unmeasured on this box.)"""
+    import numpy as np
+    import llmi
+
+    path = os.path.join(ROOT, "tests", "golden", "tiny-mixed.gguf")
+    prompt = [1, 50, 300, 7, 99, 1000, 42]
+    outs = []
+    for load in (lambda: llmi.Model(path), lambda: llmi.Model.load_fanout(path, 0, b"\0" * 128, 1, 0),
+                 lambda: llmi.Model.load_replicated(path, 0, [])[0]):
+        m = load()
+        c = llmi.Context(m, n_ctx=256)
+        assert c.decode(prompt) == 0
+        lg = c.logits(-1)
+        first = c.greedy(-1)
+        outs.append((lg, [first] + c.generate_greedy(first, len(prompt), 8)))
+        c.close()
+        m.close()
+    for lg, toks in outs[1:]:
+        assert np.array_equal(lg, outs[0][0]) and toks == outs[0][1]

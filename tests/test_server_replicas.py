@@ -1,7 +1,7 @@
 """Replica serving without GPUs: the server's least-loaded router
 and per-replica continuous-batching scheduler (llmi/server.py Engine / Replica) over
 stand-in contexts with the llmi.Context decode surface, and the `--replicas N` wiring
-of llmi_replicate checked with a stand-in llmi module.
+of llmi_model_load_replicated checked with a stand-in llmi module.
 
 Each stand-in context computes a deterministic per-sequence recurrence, so every
 request's tokens can be checked against a reference no matter how requests were
@@ -178,8 +178,9 @@ def test_eos_and_health_json_size():
 
 
 def test_replicas_flag_wires_llmi_replicate(tmp_path, monkeypatch):
-    """`--replicas 3` -> llmi.Model on device 0, Model.replicate([1, 2]) (the in-process
-    RCCL broadcast), one Context per replica with the slot count as n_seq."""
+    """`--replicas 3` -> Model.load_replicated(path, 0, [1, 2]) (llmi_model_load_replicated:
+    the in-process RCCL broadcast pipelined behind the upload), one Context per replica
+    with the slot count as n_seq."""
     import llmi as real
 
     path = str(tmp_path / "t.gguf")
@@ -191,9 +192,12 @@ def test_replicas_flag_wires_llmi_replicate(tmp_path, monkeypatch):
             log.append(("model", p, main_gpu))
             self.n_vocab, self.bos, self.eos = 1000, 1, 2
 
-        def replicate(self, devices):
-            log.append(("replicate", list(devices)))
-            return [M.__new__(M) for _ in devices]
+        @classmethod
+        def load_replicated(cls, p, main_gpu, devices):
+            log.append(("load_replicated", p, main_gpu, list(devices)))
+            m = cls.__new__(cls)
+            m.n_vocab, m.bos, m.eos = 1000, 1, 2
+            return m, [cls.__new__(cls) for _ in devices]
 
         def token_text(self, i):
             return f" w{i}"
@@ -209,8 +213,8 @@ def test_replicas_flag_wires_llmi_replicate(tmp_path, monkeypatch):
     eng = Engine(path, 256, 99, [0, 1, 2], slots=3)
     eng.load()
     assert eng.ready, eng.error
-    assert log[0] == ("model", path, 0) and log[1] == ("replicate", [1, 2])
-    assert log[2:] == [("context", 256, 3)] * 3
+    assert log[0] == ("load_replicated", path, 0, [1, 2])
+    assert log[1:] == [("context", 256, 3)] * 3
     assert [r.device for r in eng.replicas] == [0, 1, 2]
     assert eng.vocab.tok.kind == "greedy" and eng.vocab.tokenize(" w5") == [1, 5]
     for r in eng.replicas:
