@@ -250,7 +250,8 @@ void llmi_vocab_free(struct llama_vocab* vocab);
 int64_t llmi_synth_write_gguf(const char* path, const char* preset, uint64_t seed,
                               int32_t n_layer, int32_t n_vocab, int32_t n_threads);
 
-/* Debug taps of the last decode step (host copy, synchronous): 1 residual x after the
+/* Debug taps of the last decode step (host copy, synchronous): 0 the step's embedding
+ * row (get_rows of its token, n_embd), 1 residual x after the
  * last layer (n_embd), 2 roped q (n_head*head_dim), 3 attention output, 4 SwiGLU output
  * (n_ff) — the last layer's.  Mirrors the oracle's or_tap.  7/8: the last layer's raw
  * f16 K/V cache.  11-15: the last batched step's buffers, 8 slot rows each: x, q,
@@ -288,6 +289,13 @@ double llmi_bench_matvec_ex(int32_t type, const void* w_dev, int32_t n_mats, int
 /* streaming-read reference: average microseconds to read `bytes` from each of n_bufs
  * distinct buffers (stride `stride` bytes) with coalesced 16-B/lane loads */
 double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint64_t bytes, int32_t reps, int32_t blocks);
+/* One decode attention (the step's launch_attention, path `mode`: 0 auto as the step
+ * chooses, else LLMI_ATTN_MODE's numbering) of the query q (f32 [n_head*head_dim], roped)
+ * over the first n_kv positions of one layer's f16 caches in the step's layout: K
+ * [n_head_kv][n_ctx][head_dim], V transposed [n_head_kv][head_dim][n_ctx]; out f32
+ * [n_head*head_dim].  n_ctx a multiple of 256.  0 on success. */
+int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t n_ctx, const float* q,
+                       const uint16_t* kc, const uint16_t* vc, float* out, int32_t mode);
 /* Attention microbenchmark: n_kv positions, one launch per layer over >= 512 MB of
  * distinct KV caches, graph-replayed `reps` times; microseconds per launch (< 0 error).
  * mode: 0 auto, 1 fused, 2 split, 3 two-kernel.  trace_dev != NULL (LLMI_EXP_TRACE

@@ -633,6 +633,20 @@ int32_t llmi_debug_tap(struct llama_context* ctx, int32_t which, float* out) {
         if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
         return 0;
     }
+    if (which == 0) {  // the last step's embedding row (get_rows), recomputed by k_embed's dequant
+        float* tmp = nullptr;
+        if (hipMalloc(&tmp, (size_t)hp.n_embd * 4) != hipSuccess) { set_err("out of device memory"); return -2; }
+        EmbArgs ea;
+        ea.w = seg_of(*c.m, c.m->tok_embd, 0);
+        ea.cols = hp.n_embd;
+        ea.vocab = hp.n_vocab;
+        hipError_t e = launch_embed_row(ea, c.st, tmp, c.stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out, tmp, (size_t)hp.n_embd * 4, hipMemcpyDeviceToHost, c.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+        (void)hipFree(tmp);
+        if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
+        return 0;
+    }
     const float* src = which == 1 ? c.x : which == 2 ? c.q : which == 3 ? c.att : which == 4 ? c.h : nullptr;
     const size_t n = which == 1 ? hp.n_embd : which == 4 ? hp.n_ff : (size_t)hp.n_head * hp.head_dim;
     if (!src) { set_err("llmi_debug_tap: unknown tap"); return -1; }
@@ -1296,6 +1310,45 @@ double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint6
 // like a decode step does), one launch per layer captured into a graph, `reps` graph
 // replays timed between two events.  Returns microseconds per launch (incl. the
 // dependent-launch gap), < 0 on error.  mode: attention path (0 auto, 1 fused, 2 split, 3 two-kernel).
+int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t n_ctx, const float* q,
+                       const uint16_t* kc, const uint16_t* vc, float* out, int32_t mode) {
+    if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || (head_dim != 64 && head_dim != 128) || n_kv <= 0 ||
+        n_ctx < n_kv || n_ctx % 256 || !q || !kc || !vc || !out) {
+        set_err("llmi_attention: bad arguments");
+        return -1;
+    }
+    API_TRY
+    float* scores = nullptr;
+    StepState* st = nullptr;
+    if (hipMalloc(&scores, attn_scratch_floats(n_head, n_ctx) * 4) != hipSuccess || hipMalloc(&st, sizeof(StepState)) != hipSuccess) {
+        (void)hipFree(scores);
+        set_err("llmi_attention: out of device memory");
+        return -2;
+    }
+    StepState hs{};
+    hs.pos = n_kv - 1;
+    hs.pos_next = n_kv;
+    hs.seq = 1;
+    (void)hipMemcpy(st, &hs, sizeof(hs), hipMemcpyHostToDevice);
+    (void)hipMemset(scores, 0, attn_scratch_floats(n_head, n_ctx) * 4);
+    AttnArgs a;
+    a.q = q; a.kc = kc; a.vc = vc; a.scores = scores; a.out = out; a.st = st; a.n_ctx = n_ctx;
+    a.scale = 1.0f / sqrtf((float)head_dim);
+    a.tmax = scores + (size_t)n_head * n_ctx;
+    a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
+    a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);
+    set_attn_mode(mode);
+    const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
+    hipError_t e = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    set_attn_mode(0);
+    (void)hipFree(scores);
+    (void)hipFree(st);
+    if (e != hipSuccess) { set_err(std::string("llmi_attention: ") + hip_err(e)); return -3; }
+    return 0;
+    API_CATCH(-5)
+}
+
 double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t mode, int32_t reps,
                             uint64_t* trace_dev) {
     if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || (head_dim != 64 && head_dim != 128) || n_kv <= 0 || reps <= 0) {

@@ -133,6 +133,8 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
                 const UploadHook* hook = nullptr);
 // the upload half of model_load (after a load with no_upload)
 bool model_upload(Model& m, std::string& err, const UploadHook* hook = nullptr);
+// a matrix of the arena as a matvec segment (rows start at row0 of the launch)
+Seg seg_of(const Model& m, const DevMat& d, int row0);
 
 // Fan-out pieces of an arena: [k * chunk, min((k + 1) * chunk, arena_bytes)).  Piece k is
 // issued after the first upload event whose prefix covers its end; ready[k] = index of

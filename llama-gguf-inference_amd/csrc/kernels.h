@@ -200,6 +200,8 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
+// the last step's embedding row again (debug tap 0)
+hipError_t launch_embed_row(const EmbArgs& a, const StepState* st, float* out, hipStream_t stream);
 hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, int64_t cols, int rgs,
                          hipStream_t stream);
 // writes the prologue's quantized activation in ggml block form (test hook)

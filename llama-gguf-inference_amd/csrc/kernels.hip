@@ -823,6 +823,19 @@ __global__ __launch_bounds__(256) void k_embed(EmbArgs a) {
     if (e < a.cols) a.x[e] = dequant_elem(a.w, tok, e, a.cols);
 }
 
+// get_rows of the last step's token (st->token, set by k_embed) with k_embed's dequant:
+// the per-op check of SURVEY.md §8a row a10 (llmi_debug_tap 0)
+__global__ __launch_bounds__(256) void k_embed_row(Seg w, int cols, int vocab, const StepState* st, float* out) {
+    int tok = st->token;
+    if (tok < 0 || tok >= vocab) tok = 0;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e < cols) out[e] = dequant_elem(w, tok, e, cols);
+}
+hipError_t launch_embed_row(const EmbArgs& a, const StepState* st, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_embed_row, dim3((a.cols + 255) / 256), dim3(256), 0, s, a.w, a.cols, a.vocab, st, out);
+    return hipGetLastError();
+}
+
 __global__ void k_state_tick(StepState* st) { st->seq = st->seq + 1u; }
 
 hipError_t launch_state_tick(StepState* st, hipStream_t s) {

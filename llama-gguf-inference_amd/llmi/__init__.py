@@ -323,6 +323,16 @@ class Context:
             raise LlmiError(last_error())
         return np.ctypeslib.as_array(p, shape=(self.model.n_vocab,)).copy()
 
+    def tap(self, which: int, n: int) -> np.ndarray:
+        """llmi_debug_tap of the last decode step (the oracle's or_tap numbering): 0
+        embedding row, 1 residual x after the last layer, 2 roped q, 3 attention output,
+        4 SwiGLU output (the last layer's); 7 / 8 the last layer's raw f16 K / V cache.
+        n = element count (f32; u16 for 7 / 8)."""
+        out = np.empty(n, dtype=np.uint16 if which in (7, 8) else np.float32)
+        if lib().llmi_debug_tap(self._h, int(which), out.ctypes.data_as(C.c_void_p)) != 0:
+            raise LlmiError(last_error())
+        return out
+
     def greedy(self, i: int = -1) -> int:
         t = int(lib().llmi_greedy_ith(self._h, i))
         if t < 0:

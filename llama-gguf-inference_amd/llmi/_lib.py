@@ -108,6 +108,7 @@ SIGNATURES = {
     "llmi_pf_gemm": (C.c_int32, [C.c_int32, _P, C.c_int64, C.c_int64, _P, _P, C.c_float, C.c_int32, _P,
                                  C.POINTER(C.c_double)]),
     "llmi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "llmi_attention": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32]),
     "llmi_replicate": (C.c_int32, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_void_p)]),
     "llmi_rccl_unique_id": (C.c_int32, [C.c_char_p, C.c_int32]),
     "llmi_model_fanout": (C.c_int32, [_P, C.c_char_p, C.c_int32, C.c_int32]),
