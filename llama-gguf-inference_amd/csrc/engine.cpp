@@ -530,8 +530,6 @@ Prof::~Prof() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 }
 
-namespace {
-
 Seg seg_of(const Model& m, const DevMat& d, int row0) {
     Seg s;
     s.a = m.arena + d.off_a;
@@ -545,6 +543,7 @@ Seg seg_of(const Model& m, const DevMat& d, int row0) {
     return s;
 }
 
+namespace {
 }  // namespace
 
 bool step_enqueue(Context& c, int kv_bound, std::string& err) {
