@@ -35,7 +35,7 @@ __device__ __forceinline__ float h2f(uint32_t h) {
 // it the compiler folds f2h(a * b) into v_fma_mixlo_f16, ONE rounding of the exact
 // product straight to f16, where ggml rounds to f32 first and then to f16 (a tie in
 // the f32 product then rounds differently: softmax probabilities left the oracle by one
-// f16 ulp, tools/pf_diag9.py).
+// f16 ulp, experiments/pf_diag9.py).
 __device__ __forceinline__ uint16_t f2h(float f) {
     __asm__("" : "+v"(f));
     return __builtin_bit_cast(uint16_t, (_Float16)f);

@@ -78,7 +78,7 @@ def test_pipelined_loaders_single_device_equal_plain_load():
     import llmi
 
     path = os.path.join(ROOT, "tests", "golden", "tiny-mixed.gguf")
-    prompt = [1, 50, 300, 7, 99, 1000, 42]
+    prompt = [1, 50, 30, 7, 99, 100, 42]
     outs = []
     for load in (lambda: llmi.Model(path), lambda: llmi.Model.load_fanout(path, 0, b"\0" * 128, 1, 0),
                  lambda: llmi.Model.load_replicated(path, 0, [])[0]):
