@@ -234,7 +234,15 @@ static inline double old_share() {
 static inline int wide_cols() {
     static const int v = [] {
         const char* e = getenv("LLMI_MV_WIDE");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 12288;  // ffn_down of the 8B / Mistral / 70B shapes
+    }();
+    return v;
+}
+// LLMI_MV_WIDE_EPI: bitmask of epilogues that may go wide (A/B; default ADD | SWIGLU | QKV)
+static inline int wide_epis() {
+    static const int v = [] {
+        const char* e = getenv("LLMI_MV_WIDE_EPI");
+        return e ? atoi(e) : (1 << EPI_ADD) | (1 << EPI_SWIGLU) | (1 << EPI_QKV);
     }();
     return v;
 }
@@ -259,9 +267,9 @@ static hipError_t mv_launch_wide(const MVArgs& a, hipStream_t s) {
 }
 template <int ACT, bool NORM, int T, int EPI>
 static bool mv_try_wide(const MVArgs& a, hipStream_t s, hipError_t& e) {
-    if constexpr (EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV) {
+    if constexpr (EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV || EPI == EPI_LOGITS) {
         const int wc = wide_cols();
-        if (wc <= 0 || a.cols < wc || cu_count() <= 0) return false;
+        if (wc <= 0 || a.cols < wc || cu_count() <= 0 || !(wide_epis() >> EPI & 1)) return false;
         for (int i = 0; i < a.nseg; ++i)
             if (a.seg[i].type != T) return false;  // single-type launches only
         const int per = (a.cols / 16 + kMVWide - 1) / kMVWide;

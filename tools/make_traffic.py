@@ -11,7 +11,9 @@ import shutil
 import sys
 
 out, preset = sys.argv[1], sys.argv[2]
-DOM = "k_matvec<0, true, 3,"  # fused ffn_gate+ffn_up + SwiGLU (bench.py DOMINANT)
+
+# fused ffn_gate+ffn_up + SwiGLU (bench.py DOMINANT); Q8_0 models quantize to q8_0 (ACT 1)
+DOM = "k_matvec<1, true, 3," if "q8_0" in preset else "k_matvec<0, true, 3,"
 stats = glob.glob(os.path.join(out, "stats", "**", "*kernel_stats.csv"), recursive=True)
 pmc = glob.glob(os.path.join(out, "pmc", "**", "*counter_collection.csv"), recursive=True)
 assert stats and pmc, (stats, pmc)
