@@ -593,6 +593,59 @@ __device__ __forceinline__ void unit_terms(const UnitW<T>& w, const uint8_t* rec
     }
 }
 
+// Q6_K with the activation pre-masked (k_matvec's pipelined Q6_K path): a Q6_K dword holds
+// bytes of two sub-blocks (elements l, l+8 | l+16, l+24), so each sdot4 needs the
+// activation with the other sub-block's two bytes zeroed -- 128 v_and per unit in
+// unit_terms<T_Q6_K>.  The workgroup builds both masked copies of its image once
+// (q6_masks_build) and reads them instead: per unit 8 parts x {lo & 0x0000ffff,
+// lo & 0xffff0000, hi & 0x0000ffff, hi & 0xffff0000} x 16 B.  Same integer sums, same
+// fp32 terms: bit-identical.
+// bytes of masked activation per unit: 8 parts x 64 B, padded to 33 x 16 B so that the 16
+// lanes of a ds_read_b128 group (16 consecutive units) hit 16 distinct bank quads (an odd
+// stride in 16-B units, as kRec's 19)
+constexpr int kQ6MaskRec = 8 * 64 + 16;
+template <int NT>
+__device__ __forceinline__ void q6_masks_build(const Lds& L, int U, uint8_t* mbase) {
+    for (int i = threadIdx.x; i < U * 64; i += NT) {  // dword i: unit i / 64, part (i % 64) / 8, word i % 8
+        const int u = i >> 6, p = (i >> 3) & 7, wd = i & 7;  // wd < 4: LO words, else HI
+        const uint32_t v = *(const uint32_t*)(L.act + (size_t)u * kRec + 32 * p + 4 * wd);
+        uint8_t* m = mbase + (size_t)u * kQ6MaskRec + 64 * p + 32 * (wd >> 2) + 4 * (wd & 3);
+        *(uint32_t*)m = v & 0x0000ffffu;
+        *(uint32_t*)(m + 16) = v & 0xffff0000u;
+    }
+}
+__device__ __forceinline__ void unit_terms_q6m(const UnitW<T_Q6_K>& w, const uint8_t* mrec, float da, float (&tm)[9]) {
+    int t[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) t[l] = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const int c = p >> 1, k = p & 1;
+        const uint32_t s4 = w.s[c];
+        const int c0 = (int)(int8_t)(s4 & 0xff), c1 = (int)(int8_t)((s4 >> 8) & 0xff),
+                  c2 = (int)(int8_t)((s4 >> 16) & 0xff), c3 = (int)(int8_t)(s4 >> 24);
+        const i32x4 a0 = *(const i32x4*)(mrec + 64 * p), a1 = *(const i32x4*)(mrec + 64 * p + 16),
+                    a2 = *(const i32x4*)(mrec + 64 * p + 32), a3 = *(const i32x4*)(mrec + 64 * p + 48);
+        const uint32_t hl = w.h[c][k], hh = w.h[c][2 + k];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t q = w.q[p][m];
+            const uint32_t wl = (q & M4) | q6_hi_bytes((hl >> (2 * m)) & M2);
+            const uint32_t wh = ((q >> 4) & M4) | q6_hi_bytes((hh >> (2 * m)) & M2);
+            int a = t[4 * k + m];
+            a = __mul24(c0, dot4(wl, a0[m], 0)) + a;
+            a = __mul24(c1, dot4(wl, a1[m], 0)) + a;
+            a = __mul24(c2, dot4(wh, a2[m], 0)) + a;
+            a = __mul24(c3, dot4(wh, a3[m], 0)) + a;
+            t[4 * k + m] = a;
+        }
+    }
+    const float d = h2f(w.d) * da;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) tm[l] = d * (float)t[l];
+    tm[8] = 0.f;
+}
+
 // ----------------------------------------------------------------------------------
 // Row tasks.  A matvec launch's rows are cut into TASKS of R rows (gate/up launches: R
 // gate rows then the same R up rows); lane L works on row r = L / Lr of the task, units

@@ -15,6 +15,19 @@
 
 namespace llmi {
 
+#ifndef LLMI_MV_PINGPONG
+#define LLMI_MV_PINGPONG 1
+#endif
+#ifndef LLMI_Q6_MASKED
+#define LLMI_Q6_MASKED 1
+#endif
+constexpr bool kQ6Masked = LLMI_Q6_MASKED != 0;
+// LDS of a k_matvec launch of NW waves whose pipelined types are T / T2
+__host__ inline size_t mv_lds_total(int act, int cols, int nw, int t, int t2) {
+    const size_t base = fold_off(act, cols, nw) + (size_t)nw * kFoldFloats * 4;
+    return base + ((kQ6Masked && (t == T_Q6_K || t2 == T_Q6_K)) ? (size_t)(cols >> 8) * kQ6MaskRec : 0);
+}
+
 static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_SPLIT_BY_PAIRS")) : 0;  // A/B only
 
 
@@ -70,12 +83,23 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     if (img) mv_img_finish<2 * NP + 1, NT>(A, L, RI);
     else mv_prologue_finish<ACT, NORM, NP, NT>(A, L, R);
     __syncthreads();
+    // Q6_K: the masked activation copies (mv_device.h q6_masks_build), after the fold buffers
+    [[maybe_unused]] uint8_t* q6m = nullptr;
+    if constexpr (T == T_Q6_K && kQ6Masked) {
+        q6m = (uint8_t*)L.act + fold_off(ACT, A.cols, NT / 64) + (size_t)(NT / 64) * kFoldFloats * 4;
+        q6_masks_build<NT>(L, g.U, q6m);
+        __syncthreads();
+    }
     MV_STAMP(1, MV_NOW)
 
     if (pipe) {
         int s = 0;
         float acc = 0.f, vg = 0.f;
-        for (;;) {
+        // One sub-item: prefetch the next one into `nxt`, reduce `cur`.  The loop runs it
+        // twice per trip with the two register buffers' roles swapped (ping-pong), so no
+        // `cur = nxt` copy of the 36-52 registers of a unit is made per sub-item (Q6_K:
+        // ~130 v_mov of the ~885 VALU of a sub-item, and its matvecs are VALU-bound).
+        auto step = [&](UnitW<T>& cur, UnitW<T>& nxt) -> bool {
             // next sub-item: (task, s+1) or (task+G, 0); uniform control flow
             int tn = task, sn = s + 1;
             Sub bn = b;
@@ -92,35 +116,39 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             }
             const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
             // always issue the prefetch (a valid re-load of the current unit if none)
-            const UnitW<T> nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
-#if defined(LLMI_EXPERIMENTS)
-            // experiment: alternate the wave priority per sub-item, opposite phases for the
-            // first and second dispatch round of workgroups (co-resident pairs), so that
-            // neither workgroup of a CU loses every VALU arbitration to the older one
-            if (A.prio_alt) {
-                if (((nsub_alt++) + ((int)blockIdx.x >= A.prio_alt ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-#endif
+            nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
             float tm[9];
-            unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
+            if constexpr (T == T_Q6_K && kQ6Masked)
+                unit_terms_q6m(cur, q6m + (size_t)lu.u * kQ6MaskRec, *(const float*)(L.act + (size_t)lu.u * kRec + kRecD), tm);
+            else
+                unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
             sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
 #if defined(LLMI_EXP_TRACE)
             ++nsub_done;
             if (nsub_done == 1) { MV_STAMP(2, MV_NOW) }
             else if (nsub_done <= 9) { MV_STAMP(6 + nsub_done, MV_NOW) }
 #endif
-            if (!has_next) {
-                task = tn;
-                break;
-            }
-            cur = nxt;
             task = tn;
+            if (!has_next) return false;
             s = sn;
             b = bn;
             sg = sgn;
             lu = lun;
+            return true;
+        };
+#if LLMI_MV_PINGPONG
+        UnitW<T> other;
+        for (;;) {
+            if (!step(cur, other)) break;
+            if (!step(other, cur)) break;
         }
+#else
+        for (;;) {
+            UnitW<T> nxt;
+            if (!step(cur, nxt)) break;
+            cur = nxt;
+        }
+#endif
     }
     // remaining tasks of other types (or all tasks if the first was not of type T)
     for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
@@ -259,7 +287,7 @@ constexpr int kMVWide = 512;
 template <int ACT, bool NORM, int T, int EPI, int NP>
 static hipError_t mv_launch_wide(const MVArgs& a, hipStream_t s) {
     constexpr int NW = kMVWide / 64;
-    const size_t lds = fold_off(ACT, a.cols, NW) + (size_t)NW * kFoldFloats * 4;
+    const size_t lds = mv_lds_total(ACT, a.cols, NW, T, T);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int blocks = std::max(1, std::min(cu_count(), (a.ntasks + NW - 1) / NW));
     launch_k(k_matvec<ACT, NORM, EPI, T, NP, T, kMVWide>, dim3(blocks), dim3(kMVWide), lds, s, true, true, a);
@@ -282,7 +310,9 @@ static bool mv_try_wide(const MVArgs& a, hipStream_t s, hipError_t& e) {
     }
 }
 template <int ACT, bool NORM, int T, int EPI, int NP>
-static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds, hipStream_t s) {
+static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds_in, hipStream_t s) {
+    const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T));
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
     auto k = k_matvec<ACT, NORM, EPI, T, NP>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
@@ -319,7 +349,9 @@ static inline int split_groups(int wgs, int p1, int p2, double b1, double b2) {
     return best;
 }
 template <int ACT, bool NORM, int T, int T2, int EPI, int NP>
-static hipError_t mv_launch2(const MVArgs& a0, int split_tasks, dim3 grid, size_t lds, hipStream_t s) {
+static hipError_t mv_launch2(const MVArgs& a0, int split_tasks, dim3 grid, size_t lds_in, hipStream_t s) {
+    const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T2));
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
     auto k = k_matvec<ACT, NORM, EPI, T, NP, T2>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
