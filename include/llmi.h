@@ -296,6 +296,16 @@ double llmi_bench_stream(const void* dev, int32_t n_bufs, uint64_t stride, uint6
  * [n_head*head_dim].  n_ctx a multiple of 256.  0 on success. */
 int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_kv, int32_t n_ctx, const float* q,
                        const uint16_t* kc, const uint16_t* vc, float* out, int32_t mode);
+/* One batched-prefill attention (prefill_enqueue's launch_pf_attn) of T query tokens at
+ * positions pos0..pos0+T-1 (q f32 [T][n_head*head_dim], roped; token t attends to
+ * positions 0..pos0+t) over one layer's caches in the step's layout (as llmi_attention);
+ * out f32 [T][n_head*head_dim].  mode 0: the tiled FP64-MFMA kernel (k_pf_fa), 1: the
+ * grouped LDS kernel, 2: one head per workgroup.  scratch_bytes > 0 bounds k_pf_fa's
+ * score scratch (so the launch is chunked), <= 0 takes the engine's size.  Returns
+ * elapsed device microseconds (>= 0) or < 0 on error. */
+double llmi_pf_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t T, int32_t pos0, int32_t n_ctx,
+                         const float* q, const uint16_t* kc, const uint16_t* vc, float* out, int32_t mode,
+                         int64_t scratch_bytes);
 /* Attention microbenchmark: n_kv positions, one launch per layer over >= 512 MB of
  * distinct KV caches, graph-replayed `reps` times; microseconds per launch (< 0 error).
  * mode: 0 auto, 1 fused, 2 split, 3 two-kernel.  trace_dev != NULL (LLMI_EXP_TRACE

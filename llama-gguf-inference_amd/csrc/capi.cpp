@@ -596,6 +596,8 @@ int32_t llmi_test_option(const char* name, int32_t value) {
     if (!name) return -1;
     int* opt = nullptr;
     if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
+    else if (!strcmp(name, "pf_attn_fa")) opt = &g_pf_attn_fa;
+    else if (!strcmp(name, "pf_fa_cfg")) opt = &g_pf_fa_cfg;
     else if (!strcmp(name, "pf_max_kv")) opt = &g_pf_max_kv;
     else if (!strcmp(name, "xspin_limit")) opt = &g_xspin_limit;
     else if (!strcmp(name, "xtag_skew")) opt = &g_xtag_skew;
@@ -1346,6 +1348,50 @@ int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int3
     (void)hipFree(st);
     if (e != hipSuccess) { set_err(std::string("llmi_attention: ") + hip_err(e)); return -3; }
     return 0;
+    API_CATCH(-5)
+}
+
+double llmi_pf_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t T, int32_t pos0, int32_t n_ctx,
+                         const float* q, const uint16_t* kc, const uint16_t* vc, float* out, int32_t mode,
+                         int64_t scratch_bytes) {
+    if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || (head_dim != 64 && head_dim != 128) || T <= 0 ||
+        pos0 < 0 || n_ctx % 256 || pos0 + T > n_ctx || pos0 + T > kPfAttnMaxKV || mode < 0 || mode > 2 || !q || !kc ||
+        !vc || !out) {
+        set_err("llmi_pf_attention: bad arguments");
+        return -1;
+    }
+    API_TRY
+    PfAttn at;
+    at.q = q; at.out = out; at.ldq = n_head * head_dim; at.kc = kc; at.vc = vc;
+    at.n_ctx = n_ctx; at.pos0 = pos0; at.gqa = n_head / n_head_kv; at.max_kv = pos0 + T;
+    at.scale = 1.0f / sqrtf((float)head_dim);
+    float* wsc = nullptr;
+    if (mode == 0) {
+        size_t bytes = pf_fa_scratch_bytes(n_head, n_head_kv, head_dim, std::max(T, 512), n_ctx);
+        if (!bytes) { set_err("llmi_pf_attention: no tiled kernel for this head shape"); return -1; }
+        if (scratch_bytes > 0) bytes = (size_t)scratch_bytes;
+        if (hipMalloc(&wsc, bytes) != hipSuccess) { set_err("llmi_pf_attention: out of device memory"); return -2; }
+        at.wsc = wsc; at.wsc_bytes = bytes;
+    }
+    const int fa_old = g_pf_attn_fa, simple_old = g_pf_attn_simple;
+    g_pf_attn_fa = mode == 0;
+    g_pf_attn_simple = mode == 2;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, nullptr);
+    hipError_t e = launch_pf_attn(at, n_head, head_dim, T, nullptr);
+    (void)hipEventRecord(e1, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    g_pf_attn_fa = fa_old;
+    g_pf_attn_simple = simple_old;
+    float ms = 0.f;
+    if (e == hipSuccess) (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(wsc);
+    if (e != hipSuccess) { set_err(std::string("llmi_pf_attention: ") + hip_err(e)); return -3; }
+    return (double)ms * 1e3;
     API_CATCH(-5)
 }
 

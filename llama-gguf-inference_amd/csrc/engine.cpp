@@ -51,7 +51,7 @@ Context::~Context() {
     if (m) (void)hipSetDevice(device);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
-    void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad,
+    void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad, pf_wsc,
                     bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -876,6 +876,11 @@ static bool prefill_alloc(Context& c, std::string& err) {
     HIPC(hipMemsetAsync(c.pf_aq, 0, cap * maxc * 2, c.stream));
     HIPC(hipMemsetAsync(c.pf_abs, 0, cap * (maxc / 16) * 2, c.stream));
     HIPC(hipMemsetAsync(c.pf_ad, 0, cap * (maxc / 32) * 4, c.stream));
+    // the tiled attention's score rows (<= kPfFaScratchCap, launches chunked to fit); a
+    // failed allocation leaves the LDS kernels in charge
+    const size_t wsc = pf_fa_scratch_bytes(hp.n_head, hp.n_head_kv, hp.head_dim, cap, c.n_ctx);
+    if (wsc && hipMalloc(&c.pf_wsc, wsc) == hipSuccess) c.pf_wsc_bytes = wsc;
+    else { c.pf_wsc = nullptr; (void)hipGetLastError(); }
     c.pf_cap = cap;
     return true;
 }
@@ -922,6 +927,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
             at.q = c.pf_q; at.out = c.pf_att; at.ldq = nq; at.kc = g.kc; at.vc = g.vc;
             at.n_ctx = c.n_ctx; at.pos0 = p0; at.gqa = hp.n_head / hp.n_head_kv; at.max_kv = p0 + T;
             at.scale = 1.0f / sqrtf((float)D);
+            at.wsc = c.pf_wsc; at.wsc_bytes = c.pf_wsc_bytes;
             PFC(launch_pf_attn(at, hp.n_head, D, T, c.stream));
             // attn_output + residual
             PFC(launch_pf_quant(c.pf_att, nq, nullptr, 0.f, nq, act_kind(L.wo.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.stream));

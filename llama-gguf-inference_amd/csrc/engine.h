@@ -120,6 +120,8 @@ struct Context {
     void* pf_aq = nullptr;         // f16 MFMA fragments of the ubatch's activations
     int16_t* pf_abs = nullptr;
     float* pf_ad = nullptr;
+    float* pf_wsc = nullptr;       // k_pf_fa score scratch (pf_fa_scratch_bytes; null: LDS attention kernels)
+    size_t pf_wsc_bytes = 0;
     ~Context();
 };
 

@@ -22,7 +22,7 @@ constexpr int kDimAttnMaxKV = 1024;  // dim-split one-launch attention (k_attn_d
 constexpr int kRegAttnMaxKV = 512;  // register-prefetched one-launch attention (k_attn_r) up to this KV bound  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
-extern int g_pf_attn_simple, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
+extern int g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
 int pf_max_kv();  // llama_decode hands prompt runs reaching past this KV length to decode steps
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
 // + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
@@ -167,7 +167,13 @@ struct PfAttn {
     const uint16_t* kc = nullptr, *vc = nullptr;  // layer caches
     int n_ctx = 0, pos0 = 0, gqa = 1, max_kv = 0;  // max_kv >= pos0 + T (LDS score space)
     float scale = 0.f;
+    float* wsc = nullptr;      // k_pf_fa score scratch (pf_fa_scratch_bytes), null: LDS kernels only
+    size_t wsc_bytes = 0;
 };
+// score scratch k_pf_fa wants for ubatches of T tokens over n_ctx positions (0: the
+// head shape has no tiled kernel); launches are chunked to fit a smaller scratch
+size_t pf_fa_scratch_bytes(int n_head, int n_head_kv, int head_dim, int T, int n_ctx);
+constexpr size_t kPfFaScratchCap = (size_t)1 << 30;
 bool pf_gemm_ok(int type, int rows, int cols);
 hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* toks, float* X, int T, int32_t* hist,
                            int pos0, int n_ctx, hipStream_t s);

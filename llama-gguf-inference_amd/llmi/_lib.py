@@ -109,6 +109,8 @@ SIGNATURES = {
                                  C.POINTER(C.c_double)]),
     "llmi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "llmi_attention": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32]),
+    "llmi_pf_attention": (C.c_double, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P,
+                                       _P, C.c_int32, C.c_int64]),
     "llmi_replicate": (C.c_int32, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_void_p)]),
     "llmi_rccl_unique_id": (C.c_int32, [C.c_char_p, C.c_int32]),
     "llmi_model_fanout": (C.c_int32, [_P, C.c_char_p, C.c_int32, C.c_int32]),

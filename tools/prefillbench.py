@@ -28,15 +28,17 @@ preset = sys.argv[1] if len(sys.argv) > 1 else "llama3-8b-q4km"
 lens = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "128,512,2048").split(",") if x.strip()]
 GEMM_T = [int(x) for x in os.environ.get("PF_GEMM_T", "128,512").split(",")]
 path = f"/tmp/llmi_bench/{preset}-s3.gguf"
-if not os.path.exists(path):
+if lens and not os.path.exists(path):
     os.makedirs(os.path.dirname(path), exist_ok=True)
     llmi.write_synthetic_gguf(path + ".tmp", preset, seed=3)
     os.replace(path + ".tmp", path)
-m = llmi.Model(path)
-n_ctx = (max(lens + [1]) + 2 + 255) // 256 * 256
-c = llmi.Context(m, n_ctx=n_ctx)
+out = {"preset": preset, "prompts": {}}
+if lens:  # an empty length list times the GEMM shapes alone (no model)
+    m = llmi.Model(path)
+    n_ctx = (max(lens + [1]) + 2 + 255) // 256 * 256
+    c = llmi.Context(m, n_ctx=n_ctx)
+    out["prefill_supported"] = m.prefill_supported
 rng = np.random.default_rng(4)
-out = {"preset": preset, "prefill_supported": m.prefill_supported, "prompts": {}}
 for n in lens:
     prompt = [1] + [int(t) for t in rng.integers(3, min(30000, m.n_vocab), n - 1)]
     rec = {}
@@ -65,7 +67,8 @@ from helpers import Q4_K, Q6_K, empty_dev, random_blocks, to_dev  # noqa: E402
 
 L = lib()
 g = {}
-for (qt, rows, cols) in ((Q4_K, 14336, 4096), (Q4_K, 4096, 14336), (Q6_K, 4096, 14336), (Q4_K, 4096, 4096)):
+for (qt, rows, cols) in ((Q4_K, 14336, 4096), (Q4_K, 4096, 14336), (Q6_K, 4096, 14336), (Q4_K, 4096, 4096),
+                         (Q6_K, 14336, 4096), (Q6_K, 4096, 4096)):
     r = np.random.default_rng(1)
     raw = random_blocks(qt, rows, cols, r)
     wd = empty_dev(L.llmi_device_layout_bytes(qt, rows, cols))
