@@ -597,6 +597,7 @@ int32_t llmi_test_option(const char* name, int32_t value) {
     int* opt = nullptr;
     if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
     else if (!strcmp(name, "pf_attn_fa")) opt = &g_pf_attn_fa;
+    else if (!strcmp(name, "pf_gemm_ng")) opt = &g_pf_gemm_ng;
     else if (!strcmp(name, "pf_fa_cfg")) opt = &g_pf_fa_cfg;
     else if (!strcmp(name, "pf_max_kv")) opt = &g_pf_max_kv;
     else if (!strcmp(name, "xspin_limit")) opt = &g_xspin_limit;
@@ -1157,20 +1158,23 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
 int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, const float* x, const float* nw, float eps,
                      int32_t n_tok, float* y, double* usec) {
     if (!pf_gemm_ok(type, (int)rows, (int)cols) || n_tok <= 0) { set_err("llmi_pf_gemm: unsupported type/shape"); return -1; }
-    const int tpad = (n_tok + 31) / 32 * 32;
+    const int tpad = (n_tok + 63) / 64 * 64;
     void* aq = nullptr;
     int16_t* abs = nullptr;
     float* ad = nullptr;
+    void* abf = nullptr;
     hipError_t e = hipMalloc(&aq, (size_t)tpad * cols * 2);
+    if (e == hipSuccess) e = hipMalloc(&abf, (size_t)tpad * (cols / 256) * 64);
+    if (e == hipSuccess) e = hipMemset(abf, 0, (size_t)tpad * (cols / 256) * 64);
     if (e == hipSuccess) e = hipMalloc(&abs, (size_t)tpad * (cols / 16) * 2);
     if (e == hipSuccess) e = hipMalloc(&ad, (size_t)tpad * (cols / 32) * 4);
     if (e == hipSuccess) e = hipMemset(aq, 0, (size_t)tpad * cols * 2);
     if (e == hipSuccess) e = hipMemset(abs, 0, (size_t)tpad * (cols / 16) * 2);
     if (e == hipSuccess) e = hipMemset(ad, 0, (size_t)tpad * (cols / 32) * 4);
-    if (e == hipSuccess) e = launch_pf_quant(x, (int)cols, nw, eps, (int)cols, act_kind(type), n_tok, aq, abs, ad, nullptr);
+    if (e == hipSuccess) e = launch_pf_quant(x, (int)cols, nw, eps, (int)cols, act_kind(type), n_tok, aq, abs, ad, abf, nullptr);
     PfGemm g;
     g.w = seg_at(type, w, rows, cols); g.rows = (int)rows; g.cols = (int)cols; g.T = n_tok;
-    g.aq = aq; g.abs = abs; g.ad = ad; g.y = y; g.ldy = (int)rows;
+    g.aq = aq; g.abs = abs; g.ad = ad; g.abf = abf; g.y = y; g.ldy = (int)rows;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess && usec) { (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventRecord(e0, nullptr); }
     if (e == hipSuccess) e = launch_pf_gemm(g, EPI_STORE, nullptr);
@@ -1184,7 +1188,7 @@ int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, co
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-    (void)hipFree(aq); (void)hipFree(abs); (void)hipFree(ad);
+    (void)hipFree(aq); (void)hipFree(abs); (void)hipFree(ad); (void)hipFree(abf);
     if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
     return 0;
 }

@@ -51,7 +51,7 @@ Context::~Context() {
     if (m) (void)hipSetDevice(device);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
-    void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad, pf_wsc,
+    void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad, pf_abf, pf_wsc,
                     bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -739,7 +739,7 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     auto bmv = [&](const MVArgs& a, int epi, bool& quantized) -> hipError_t {
         if (nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
         if (!quantized) {
-            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, c.stream);
+            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, nullptr, c.stream);
             if (e != hipSuccess) return e;
             quantized = true;
         }
@@ -872,10 +872,12 @@ static bool prefill_alloc(Context& c, std::string& err) {
     HIPC(hipMalloc(&c.pf_aq, cap * maxc * 2));
     HIPC(hipMalloc(&c.pf_abs, cap * (maxc / 16) * 2));
     HIPC(hipMalloc(&c.pf_ad, cap * (maxc / 32) * 4));
+    HIPC(hipMalloc(&c.pf_abf, cap * (maxc / 256) * 64));
     // padded token rows of the activation buffers are read (never stored): keep them finite
     HIPC(hipMemsetAsync(c.pf_aq, 0, cap * maxc * 2, c.stream));
     HIPC(hipMemsetAsync(c.pf_abs, 0, cap * (maxc / 16) * 2, c.stream));
     HIPC(hipMemsetAsync(c.pf_ad, 0, cap * (maxc / 32) * 4, c.stream));
+    HIPC(hipMemsetAsync(c.pf_abf, 0, cap * (maxc / 256) * 64, c.stream));
     // the tiled attention's score rows (<= kPfFaScratchCap, launches chunked to fit); a
     // failed allocation leaves the LDS kernels in charge
     const size_t wsc = pf_fa_scratch_bytes(hp.n_head, hp.n_head_kv, hp.head_dim, cap, c.n_ctx);
@@ -905,7 +907,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
         for (int l = 0; l < hp.n_layer; ++l) {
             const Layer& L = m.layers[(size_t)l];
             PfGemm g;
-            g.T = T; g.aq = c.pf_aq; g.abs = c.pf_abs; g.ad = c.pf_ad;
+            g.T = T; g.aq = c.pf_aq; g.abs = c.pf_abs; g.ad = c.pf_ad; g.abf = c.pf_abf;
             g.kc = c.kc + l * kv_layer; g.vc = c.vc + l * kv_layer; g.rope = c.rope;
             g.pos0 = p0; g.head_dim = D; g.n_rot = hp.n_rot; g.n_ctx = c.n_ctx;
             // q, k, v (each quantized for its own activation kind)
@@ -916,7 +918,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
                 if (act_kind(W.type) != quant_kind) {
                     quant_kind = act_kind(W.type);
                     PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.attn_norm.off_a), hp.eps, E, quant_kind, T,
-                                        c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+                                        c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
                 }
                 g.w = seg_of(m, W, 0); g.rows = (int)W.rows; g.cols = E; g.part = part;
                 g.y = c.pf_q; g.ldy = nq;
@@ -930,16 +932,15 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
             at.wsc = c.pf_wsc; at.wsc_bytes = c.pf_wsc_bytes;
             PFC(launch_pf_attn(at, hp.n_head, D, T, c.stream));
             // attn_output + residual
-            PFC(launch_pf_quant(c.pf_att, nq, nullptr, 0.f, nq, act_kind(L.wo.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+            PFC(launch_pf_quant(c.pf_att, nq, nullptr, 0.f, nq, act_kind(L.wo.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
             g.w = seg_of(m, L.wo, 0); g.rows = (int)L.wo.rows; g.cols = nq; g.y = c.pf_x; g.ldy = E;
             PFC(launch_pf_gemm(g, EPI_ADD, c.stream));
             // gate/up + SwiGLU
             PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.ffn_norm.off_a), hp.eps, E, act_kind(L.wg.type), T,
-                                c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+                                c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
             g.w = seg_of(m, L.wg, 0); g.w2 = seg_of(m, L.wu, 0); g.rows = (int)L.wg.rows; g.cols = E; g.y = c.pf_h; g.ldy = F;
-            if (L.wg.type == L.wu.type) {
-                PFC(launch_pf_gemm(g, EPI_SWIGLU, c.stream));
-            } else {  // gate into h, then h = silu(h) * up
+            {  // gate into h, then h = silu(h) * up (two launches: a fused gate+up kernel
+               // holds both matrices' chains and ran at one wave per SIMD)
                 if (act_kind(L.wu.type) != act_kind(L.wg.type)) {
                     err = "prefill: ffn_gate/ffn_up of different activation kinds";
                     return false;
@@ -949,7 +950,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
                 PFC(launch_pf_gemm(g, EPI_SWIGLU_UP, c.stream));
             }
             // down + residual
-            PFC(launch_pf_quant(c.pf_h, F, nullptr, 0.f, F, act_kind(L.wd.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.stream));
+            PFC(launch_pf_quant(c.pf_h, F, nullptr, 0.f, F, act_kind(L.wd.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
             g.w = seg_of(m, L.wd, 0); g.rows = (int)L.wd.rows; g.cols = F; g.y = c.pf_x; g.ldy = E;
             PFC(launch_pf_gemm(g, EPI_ADD, c.stream));
         }

@@ -120,6 +120,7 @@ struct Context {
     void* pf_aq = nullptr;         // f16 MFMA fragments of the ubatch's activations
     int16_t* pf_abs = nullptr;
     float* pf_ad = nullptr;
+    void* pf_abf = nullptr;        // K-quants: bsum pairs as k_pf_gemm's sumi MFMA fragments
     float* pf_wsc = nullptr;       // k_pf_fa score scratch (pf_fa_scratch_bytes; null: LDS attention kernels)
     size_t pf_wsc_bytes = 0;
     ~Context();

@@ -11,6 +11,17 @@ namespace llmi {
 // (hipExtLaunchKernelGGL), i.e. kernel execution time without dependent-launch gaps.
 hipEvent_t launch_event(bool stop);
 
+// CUs of the current device (read once per translation unit)
+static inline int cu_count() {
+    static const int n = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 0;
+        return c;
+    }();
+    return n;
+}
+
 template <typename K, typename... Args>
 static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool first, bool last, Args... args) {
     hipEvent_t e0 = first ? launch_event(false) : nullptr, e1 = last ? launch_event(true) : nullptr;

@@ -274,15 +274,6 @@ static inline int wide_epis() {
     }();
     return v;
 }
-static inline int cu_count() {
-    static const int n = [] {
-        int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 0;
-        return c;
-    }();
-    return n;
-}
 constexpr int kMVWide = 512;
 template <int ACT, bool NORM, int T, int EPI, int NP>
 static hipError_t mv_launch_wide(const MVArgs& a, hipStream_t s) {

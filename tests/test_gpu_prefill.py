@@ -203,13 +203,28 @@ def _weights(qtype, rows, cols, rng):
 
 @pytest.mark.parametrize("qtype", [Q4_K, Q5_K, Q6_K, Q8_0])
 @pytest.mark.parametrize("rows,cols", [(32, 256), (96, 512), (128, 768), (160, 4096), (64, 14336)])
-@pytest.mark.parametrize("n_tok", [1, 5, 33])
+@pytest.mark.parametrize("n_tok", [1, 5, 33, 70])
 @pytest.mark.parametrize("norm", [False, True])
-def test_pf_gemm_equals_matvec(gpu, qtype, rows, cols, n_tok, norm):
+@pytest.mark.parametrize("ng", [2, 1])
+def test_pf_gemm_equals_matvec(gpu, qtype, rows, cols, n_tok, norm, ng):
+    """k_pf_gemm (64-token workgroups, NG = 2, above 32 tokens; 32-token ones forced by
+    the pf_gemm_ng option) against n_tok matvec launches, bit for bit."""
     import torch
     from llmi._lib import lib
 
     L = lib()
+    if ng == 1 and (n_tok < 33 or cols > 768):
+        pytest.skip("the 32-token workgroup variant is exercised on the ragged multi-group sizes")
+    old = L.llmi_test_option(b"pf_gemm_ng", ng)
+    try:
+        _pf_gemm_case(L, qtype, rows, cols, n_tok, norm)
+    finally:
+        L.llmi_test_option(b"pf_gemm_ng", old)
+
+
+def _pf_gemm_case(L, qtype, rows, cols, n_tok, norm):
+    import torch
+
     rng = np.random.default_rng(rows + cols + n_tok + qtype)
     wd = _weights(qtype, rows, cols, rng)
     x = rng.standard_normal((n_tok, cols)).astype(np.float32)

@@ -66,6 +66,8 @@ for n in lens:
 from helpers import Q4_K, Q6_K, empty_dev, random_blocks, to_dev  # noqa: E402
 
 L = lib()
+if os.environ.get("PF_GEMM_NG"):
+    L.llmi_test_option(b"pf_gemm_ng", int(os.environ["PF_GEMM_NG"]))
 g = {}
 for (qt, rows, cols) in ((Q4_K, 14336, 4096), (Q4_K, 4096, 14336), (Q6_K, 4096, 14336), (Q4_K, 4096, 4096),
                          (Q6_K, 14336, 4096), (Q6_K, 4096, 4096)):
