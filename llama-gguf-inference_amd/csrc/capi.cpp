@@ -232,9 +232,10 @@ static bool run_seq(llama_context* ctx, const llama_batch& batch, int seq, const
     const int p0 = pos[0];
     int run = 0;
     while (run < n - 1 && rows[(size_t)idx[(size_t)run]] < 0 && pos[(size_t)run] == p0 + run) ++run;
-    // the batched-prefill attention holds one head's scores in LDS: a run reaching past
-    // pf_max_kv() positions goes through decode steps from there on
-    if (p0 + run > pf_max_kv()) run = std::max(0, pf_max_kv() - p0);
+    // a run reaching past prefill_max_kv() positions (the LDS-resident attention kernels'
+    // limit where the tiled one does not apply) goes through decode steps from there on
+    const int pf_lim = prefill_max_kv(c);
+    if (p0 + run > pf_lim) run = std::max(0, pf_lim - p0);
     if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
         std::vector<int32_t> toks((size_t)run);
         for (int i = 0; i < run; ++i) toks[(size_t)i] = batch.token[idx[(size_t)i]];

@@ -887,6 +887,15 @@ static bool prefill_alloc(Context& c, std::string& err) {
     return true;
 }
 
+int prefill_max_kv(const Context& c) {
+    const HParams& hp = c.m->hp;
+    const int lim = pf_max_kv();
+    if (lim == kPfAttnMaxKV && g_pf_attn_fa && !g_pf_attn_simple &&
+        pf_fa_scratch_bytes(hp.n_head, hp.n_head_kv, hp.head_dim, 512, c.n_ctx) > 0)
+        return c.n_ctx;
+    return lim;
+}
+
 bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::string& err) {
     const Model& m = *c.m;
     const HParams& hp = m.hp;

@@ -159,6 +159,9 @@ bool step_run(Context& c, int pos, std::string& err);
 double bytes_per_token(const Model& m, int n_kv);
 // batched prefill: can the model's layers run through the MFMA prefill path?
 bool prefill_supported(const Model& m);
+// positions the batched prefill's attention reaches: the context when the tiled kernel
+// (k_pf_fa) takes the model's heads, else the LDS kernels' pf_max_kv()
+int prefill_max_kv(const Context& c);
 // run tokens [0, n) at positions pos0.. through every layer as batched launches (KV
 // cache written, no logits); enqueued on c.stream, no synchronisation
 bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::string& err);

@@ -174,42 +174,63 @@ def test_prompt_past_prefill_kv_limit(gpu, tiny_models, monkeypatch):
     _assert_same(got, steps)
 
 
+def _with_option(name, value, fn):
+    old = llmi.test_option(name, value)
+    try:
+        return fn()
+    finally:
+        llmi.test_option(name, old)
+
+
 def test_prefill_attention_past_16k_positions(gpu, tiny_models, monkeypatch):
-    """A 16500-token prompt: both batched-prefill attention kernels (G heads per
-    workgroup, and one head per workgroup) then hold > 64 KiB of scores in LDS (both once
-    failed with "invalid argument" from a refused LDS attribute call).  Prefilled logits and the decode steps after them (long-context
-    decode attention) equal all-decode-step processing of the prompt bit for bit."""
+    """A 16500-token prompt through every batched-prefill attention path: the tiled
+    FP64-MFMA kernel (default), the G-heads-per-workgroup LDS kernel and the one-head LDS
+    kernel (both then hold > 64 KiB of scores in LDS; both once failed with "invalid
+    argument" from a refused LDS attribute call).  Prefilled logits and the decode steps
+    after them (long-context decode attention) equal all-decode-step processing of the
+    prompt bit for bit."""
     path = tiny_models["tiny-mixed-d128"]
     rng = np.random.default_rng(16)
     prompt = [1] + [int(t) for t in rng.integers(3, 700, 16499)]
-    _, grouped = _gpu_run(path, prompt, 16640, 2)  # G = 2 heads per workgroup: 130 KiB LDS
-    old = llmi.test_option("pf_attn_simple", 1)
-    try:
-        _, pf = _gpu_run(path, prompt, 16640, 2)
-    finally:
-        llmi.test_option("pf_attn_simple", old)
+    _, tiled = _gpu_run(path, prompt, 16640, 2)
+    _, grouped = _with_option("pf_attn_fa", 0, lambda: _gpu_run(path, prompt, 16640, 2))  # G = 2: 130 KiB LDS
+    _, pf = _with_option("pf_attn_simple", 1, lambda: _gpu_run(path, prompt, 16640, 2))
     monkeypatch.setenv("LLMI_NO_PREFILL", "1")
     _, steps = _gpu_run(path, prompt, 16640, 2)
+    _assert_same(tiled, steps)
     _assert_same(pf, steps)
     _assert_same(grouped, steps)
+
+
+def test_prefill_past_the_lds_limit(gpu, tiny_models, monkeypatch):
+    """A 33000-token prompt: past kPfAttnMaxKV (32768) positions the LDS attention kernels
+    cannot run, so before the tiled kernel the run's tail went through decode steps; now
+    the whole prompt prefills (prefill_max_kv = the context) and still equals
+    all-decode-step processing bit for bit."""
+    path = tiny_models["tiny-mixed"]
+    rng = np.random.default_rng(33)
+    prompt = [1] + [int(t) for t in rng.integers(3, 700, 32999)]
+    _, pf = _gpu_run(path, prompt, 33280, 2)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    _, steps = _gpu_run(path, prompt, 33280, 2)
+    _assert_same(pf, steps)
 
 
 def test_prefill_attention_head_subgroups(gpu, synth_dir, monkeypatch):
     """Llama-3-8B widths (2 layers, GQA 4), a 10500-token prompt: past ~10k positions the
     four heads' scores no longer fit in LDS and the batched-prefill attention runs
-    sub-groups of 2 heads per workgroup.  Prefilled logits and the next decode steps equal
-    the one-head-per-workgroup kernel's and all-decode-step processing bit for bit."""
+    sub-groups of 2 heads per workgroup (with the tiled kernel switched off).  Prefilled
+    logits and the next decode steps equal the one-head-per-workgroup kernel's, the tiled
+    kernel's and all-decode-step processing bit for bit."""
     path = str(synth_dir / "llama3-8b-q4km-L2-sub.gguf")
     llmi.write_synthetic_gguf(path, "llama3-8b-q4km", seed=21, n_layer=2)
     rng = np.random.default_rng(17)
     prompt = [1] + [int(t) for t in rng.integers(3, 120000, 10499)]
-    _, sub = _gpu_run(path, prompt, 10752, 2)
-    old = llmi.test_option("pf_attn_simple", 1)
-    try:
-        _, simple = _gpu_run(path, prompt, 10752, 2)
-    finally:
-        llmi.test_option("pf_attn_simple", old)
+    _, sub = _with_option("pf_attn_fa", 0, lambda: _gpu_run(path, prompt, 10752, 2))
+    _, simple = _with_option("pf_attn_simple", 1, lambda: _gpu_run(path, prompt, 10752, 2))
+    _, tiled = _gpu_run(path, prompt, 10752, 2)
     _assert_same(sub, simple)
+    _assert_same(tiled, simple)
     monkeypatch.setenv("LLMI_NO_PREFILL", "1")
     _, steps = _gpu_run(path, prompt, 10752, 2)
     _assert_same(sub, steps)

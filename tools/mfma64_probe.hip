@@ -99,6 +99,35 @@ __global__ void k_mix(int iters, int valu_iters, double* out, long long* cyc) {
     if ((threadIdx.x & 63) == 0) cyc[w] = t1 - t0;
 }
 
+// the same mix for the f16 MFMA k_pf_gemm runs on (v_mfma_f32_16x16x32_f16)
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+__global__ void k_mix16(int iters, int valu_iters, double* out, long long* cyc) {
+    const int w = threadIdx.x >> 6;
+    const long long t0 = clock64();
+    double s = 0;
+    if (w < 4) {
+        f4 acc[4];
+        for (int i = 0; i < 4; ++i) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
+        h8 a, b;
+        for (int k = 0; k < 8; ++k) { a[k] = (_Float16)(threadIdx.x + k); b[k] = (_Float16)1.f; }
+        for (int it = 0; it < iters; ++it)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) s += acc[i][0];
+    } else if (valu_iters > 0) {
+        float g[8];
+        for (int k = 0; k < 8; ++k) g[k] = threadIdx.x + k;
+        for (int it = 0; it < valu_iters; ++it)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] = g[k] * 1.0001f + 0.5f;
+        for (int k = 0; k < 8; ++k) s += g[k];
+    }
+    const long long t1 = clock64();
+    out[threadIdx.x] = s;
+    if ((threadIdx.x & 63) == 0) cyc[w] = t1 - t0;
+}
+
 int main() {
     // ---- 1. semantics: row 0 / column 0 of the 16x16 result = sum_k A[0][k] B[k][0]
     double ha[64], hb[64], hc = 0.0, hd[256];
@@ -181,6 +210,13 @@ int main() {
     }
     k_mix<<<1, 512>>>(0, 4 * iters, dout, dc8);
     hipMemcpy(c8, dc8, 64, hipMemcpyDeviceToHost);
-    printf("\"valu_alone_cycles\": %lld}\n", c8[4]);
+    printf("\"valu_alone_cycles\": %lld, ", c8[4]);
+    for (int vi : {0, 4 * iters}) {
+        k_mix16<<<1, 512>>>(4 * iters, vi, dout, dc8);
+        hipMemcpy(c8, dc8, 64, hipMemcpyDeviceToHost);
+        printf("\"f16_mix_valu%d_mfma_cycles_per_mfma\": %.2f, \"f16_mix_valu%d_valu_wave_cycles\": %lld, ", vi ? 1 : 0,
+               (double)c8[0] / iters / 16, vi ? 1 : 0, c8[4]);
+    }
+    printf("\"end\": 0}\n");
     return 0;
 }
