@@ -555,172 +555,6 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
     }
 }
 
-// ---- the batched matvec, one wave per row tile ----------------------------------------
-// k_bmt: each WAVE owns one 16-row tile (SWIGLU: 16 gate rows and the same up rows) and
-// walks every 256-element stage of K in order with its chains in registers: no LDS, no
-// barrier, so a wave never waits for another and the next stage's weights and token
-// fragments (prefetched into registers one stage ahead) overlap the current stage.  Per
-// stage and residue l: B = q * scale (pf_build_b, exact f16), one v_mfma_f32_16x16x32_f16
-// against the nt <= 8 tokens' q8 fragments (A rows = tokens: lanes with lane & 15 < nt load
-// theirs, the padding rows stay zero), the term (d_w d_a) aux32[l] added onto chain l;
-// sumi = mins . bsums on the MFMA from k_pf_quant's bsum fragments (abf; exact integers
-// < 2^24) for the dmin chain.  C layout: lane = row lane & 15, tokens 4 (lane >> 4) + i;
-// lanes 32..63 hold padding tokens.  Every chain sees the blocks in order, so a token's
-// results equal its single decode (k_matvec) and the oracle bit for bit.
-template <int T, int NW>
-struct BtStage {
-    PfW<T> w[NW];
-    h8 a[8];
-    h8 bs;        // sumi A fragment (K-quants with mins)
-    float da[4];  // d_a of tokens 4 grp + i
-};
-template <int T, int NW>
-__device__ __forceinline__ void bt_load(BtStage<T, NW>& st, const RowPtr (&rp)[NW], const uint8_t* aq, const float* ad,
-                                        const uint8_t* abf, int s, int S, int nt) {
-    const int lane = threadIdx.x & 63, n = lane & 15, grp = lane >> 4;
-#pragma unroll
-    for (int wi = 0; wi < NW; ++wi) st.w[wi] = pf_w_load<T>(rp[wi], s, S);
-#pragma unroll
-    for (int l = 0; l < 8; ++l) st.a[l] = n < nt ? *(const h8*)(aq + pf_aq_off(n, s, 4 * l + grp, S)) : h8{};
-    if constexpr (T != T_Q6_K) st.bs = n < nt ? *(const h8*)(abf + pf_abf_off(n, s, grp, S)) : h8{};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int t = 4 * grp + i;
-        st.da[i] = t < nt ? ad[(size_t)t * S + s] : 0.f;
-    }
-}
-
-template <int T, int EPI>
-__global__ __launch_bounds__(256) void k_bmt(MVArgs A, const uint8_t* aq, const float* ad, const uint8_t* abf, int nt,
-                                             int ntiles) {
-    constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;  // weight matrices (SWIGLU: gate, up)
-    const int wave = uniform((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63, n = lane & 15, grp = lane >> 4;
-    const int tile = blockIdx.x * 4 + wave;
-    if (tile >= ntiles) return;  // whole waves only: nothing below synchronizes across waves
-    const int S = A.cols >> 8;
-    int si, row0;
-    RowPtr rp[NW];
-    bm_tile<T, EPI, NW>(A, tile, si, row0, rp);
-    f2v sums[NW][8][2], sumf[NW][2];
-#pragma unroll
-    for (int wi = 0; wi < NW; ++wi)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            sumf[wi][h] = f2v{0.f, 0.f};
-#pragma unroll
-            for (int l = 0; l < 8; ++l) sums[wi][l][h] = f2v{0.f, 0.f};
-        }
-    BtStage<T, NW> cur;
-    bt_load<T, NW>(cur, rp, aq, ad, abf, 0, S, nt);
-    for (int s = 0; s < S; ++s) {
-        BtStage<T, NW> nxt;
-        bt_load<T, NW>(nxt, rp, aq, ad, abf, s + 1 < S ? s + 1 : s, S, nt);  // unconditional (no scratch copies)
-#pragma unroll
-        for (int wi = 0; wi < NW; ++wi) {
-            const PfW<T>& w = cur.w[wi];
-            h2 slo{}, shi{}, slo_o{}, shi_o{};
-            h2 s6[8], s6o[8];
-            float dw, dmw = 0.f;
-            h8 bm{};
-            if constexpr (T == T_Q4_K || T == T_Q5_K) {
-                int sc0, m0, sc1, m1;
-                scale_min(2 * grp, w.hdr.y, w.hdr.z, w.hdr.w, sc0, m0);
-                scale_min(2 * grp + 1, w.hdr.y, w.hdr.z, w.hdr.w, sc1, m1);
-                slo = h2{(_Float16)(float)sc0, (_Float16)(float)sc0};
-                shi = h2{(_Float16)(float)sc1, (_Float16)(float)sc1};
-                slo_o = slo * h2{(_Float16)1024.f, (_Float16)1024.f};
-                shi_o = shi * h2{(_Float16)1024.f, (_Float16)1024.f};
-                dw = h2f(w.hdr.x);
-                dmw = h2f(w.hdr.x >> 16);
-                bm[0] = (_Float16)(float)m0;
-                bm[1] = (_Float16)(float)(64 * m0);
-                bm[2] = (_Float16)(float)m1;
-                bm[3] = (_Float16)(float)(64 * m1);
-            } else {  // Q6_K: sc = 16 sh + sl per sub-block 4 grp + k
-                dw = h2f(w.d);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int sc = (int)(int8_t)(w.sc >> (8 * k));
-                    const int sh = sc >> 4, sl = sc & 15;
-                    const _Float16 fl = (_Float16)(float)sl, fh = (_Float16)(float)sh;
-                    s6[2 * k] = h2{fl, fl};
-                    s6[2 * k + 1] = h2{fh, fh};
-                    s6o[2 * k] = s6[2 * k] * h2{(_Float16)1056.f, (_Float16)1056.f};
-                    s6o[2 * k + 1] = s6[2 * k + 1] * h2{(_Float16)1056.f, (_Float16)1056.f};
-                }
-            }
-            const f2v d[2] = {f2v{dw, dw} * f2v{cur.da[0], cur.da[1]}, f2v{dw, dw} * f2v{cur.da[2], cur.da[3]}};
-#pragma unroll
-            for (int l = 0; l < 8; ++l) {
-                h8 bf[2];
-                pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf);
-                f4 acc = mfma16(cur.a[l], bf[0], f4{0.f, 0.f, 0.f, 0.f});
-                if constexpr (T == T_Q6_K) {
-                    const f4 acc_h = mfma16(cur.a[l], bf[1], f4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[i] = acc_h[i] * 16.f + acc[i];  // exact (< 2^24)
-                }
-#pragma unroll
-                for (int h = 0; h < 2; ++h) sums[wi][l][h] = sums[wi][l][h] + d[h] * f2v{acc[2 * h], acc[2 * h + 1]};
-            }
-            if constexpr (T != T_Q6_K) {  // sumf -= (dmin * d_a) * sumi
-                const f4 sm = mfma16(cur.bs, bm, f4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const f2v dm = f2v{dmw, dmw} * f2v{cur.da[2 * h], cur.da[2 * h + 1]};
-                    sumf[wi][h] = sumf[wi][h] - dm * f2v{sm[2 * h], sm[2 * h + 1]};
-                }
-            }
-        }
-        cur = nxt;
-    }
-    // row values: sumf, then + sums[0..7] (the generic order's final adds)
-    float v[NW][4];
-#pragma unroll
-    for (int wi = 0; wi < NW; ++wi)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            f2v x = sumf[wi][h];
-#pragma unroll
-            for (int l = 0; l < 8; ++l) x = x + sums[wi][l][h];
-            v[wi][2 * h] = x[0];
-            v[wi][2 * h + 1] = x[1];
-        }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int t = 4 * grp + i;  // uniform per 16-lane row group
-        const float vp = xor_partner<1>(v[0][i]);  // the pair's other row (row n ^ 1)
-        unsigned long long best = 0;
-        int seq = 0, pos = 0;
-        if (t < nt) {
-            seq = A.tseq ? A.tseq[t] : 0;
-            pos = A.tpos ? A.tpos[t] : 0;
-            const MVArgs B = token_view(A, t, seq);
-            PairRef ref;
-            ref.sa = ref.sb = pick(A, si);
-            ref.ra = row0 + (n & ~1);
-            ref.rb = ref.ra + 1;
-            ref.vb = 1;
-            ref.type = T;
-            if constexpr (EPI == EPI_SWIGLU) {
-                epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n, PairSum{v[0][i], v[NW - 1][i]}, pos, best);
-            } else if ((n & 1) == 0) {
-                epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][i], vp}, pos, best);
-            }
-        }
-        if constexpr (EPI == EPI_LOGITS) {  // per token: max over the row group's pairs, one atomic
-            best = max(best, __shfl_xor(best, 2));
-            best = max(best, __shfl_xor(best, 4));
-            best = max(best, __shfl_xor(best, 8));
-            if (n == 0 && t < nt) {
-                StepState* st = A.st + seq;
-                if (best) atomicMax(&st->key[pos & 1][tile % kArgSlots], best);
-                if (tile == 0) st->pos_next = pos + 1;
-            }
-        }
-    }
-}
-
 // ---- launchers -----------------------------------------------------------------------------
 size_t mvn_lds_bytes(int act, int cols, int nt) {
     return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * kFoldFloats * 4;
@@ -893,34 +727,6 @@ static hipError_t bmm_launch(const MVArgs& a, const void* aq, const int16_t* abs
     return hipGetLastError();
 }
 
-// k_bmt for segments with at least LLMI_BMT_TILES 16-row tiles (default 0: every
-// launch k_bmm would take), else k_bmm; LLMI_BMT=0 turns it off (A/B)
-static int bmt_min_tiles() {
-    const char* e = getenv("LLMI_BMT");  // read per call (step capture): tests switch it
-    if (e && atoi(e) == 0) return 1 << 30;
-    const char* m = getenv("LLMI_BMT_TILES");
-    return m ? atoi(m) : 0;
-}
-template <int T, int EPI>
-static hipError_t bmt_launch(const MVArgs& a, const void* aq, const float* ad, const void* abf, int nt, int ntiles,
-                             hipStream_t s) {
-    auto k = k_bmt<T, EPI>;
-    hipLaunchKernelGGL(k, dim3((ntiles + 3) / 4), dim3(256), 0, s, a, (const uint8_t*)aq, ad, (const uint8_t*)abf, nt, ntiles);
-    return hipGetLastError();
-}
-template <int T>
-static hipError_t bmt_epi(const MVArgs& a, int epi, const void* aq, const float* ad, const void* abf, int nt, int ntiles,
-                          hipStream_t s) {
-    switch (epi) {
-        case EPI_STORE: return bmt_launch<T, EPI_STORE>(a, aq, ad, abf, nt, ntiles, s);
-        case EPI_ADD: return bmt_launch<T, EPI_ADD>(a, aq, ad, abf, nt, ntiles, s);
-        case EPI_QKV: return bmt_launch<T, EPI_QKV>(a, aq, ad, abf, nt, ntiles, s);
-        case EPI_SWIGLU: return bmt_launch<T, EPI_SWIGLU>(a, aq, ad, abf, nt, ntiles, s);
-        case EPI_LOGITS: return bmt_launch<T, EPI_LOGITS>(a, aq, ad, abf, nt, ntiles, s);
-        default: return hipErrorInvalidValue;
-    }
-}
-
 template <int T>
 static hipError_t bmm_epi(const MVArgs& a, int epi, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
     switch (epi) {
@@ -933,21 +739,8 @@ static hipError_t bmm_epi(const MVArgs& a, int epi, const void* aq, const int16_
     }
 }
 
-hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const int16_t* abs, const float* ad,
-                      const void* abf, hipStream_t s) {
+hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const int16_t* abs, const float* ad, hipStream_t s) {
     if (nt < 1 || nt > kMaxBatch || !bmm_ok(a, epi)) return hipErrorInvalidValue;
-    int rows = 0;
-    if (epi == EPI_SWIGLU) rows = a.seg[0].rows;
-    else
-        for (int i = 0; i < a.nseg; ++i) rows += a.seg[i].rows;
-    if (abf && rows / 16 >= bmt_min_tiles()) {
-        switch (a.seg[0].type) {
-            case T_Q4_K: return bmt_epi<T_Q4_K>(a, epi, aq, ad, abf, nt, rows / 16, s);
-            case T_Q5_K: return bmt_epi<T_Q5_K>(a, epi, aq, ad, abf, nt, rows / 16, s);
-            case T_Q6_K: return bmt_epi<T_Q6_K>(a, epi, aq, ad, abf, nt, rows / 16, s);
-            default: return hipErrorInvalidValue;
-        }
-    }
     switch (a.seg[0].type) {
         case T_Q4_K: return bmm_epi<T_Q4_K>(a, epi, aq, abs, ad, nt, s);
         case T_Q5_K: return bmm_epi<T_Q5_K>(a, epi, aq, abs, ad, nt, s);
