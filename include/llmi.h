@@ -217,7 +217,8 @@ int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_
  * uploaded weights, ranks 1..n-1 loaded the same GGUF with params.no_upload.  Every rank
  * calls llmi_model_fanout with the same 128-byte RCCL unique id (made by rank 0 with
  * llmi_rccl_unique_id and shared by any out-of-band channel); the arena is broadcast
- * from rank 0 over xGMI with one ncclBroadcast.  Returns 0 on success. */
+ * from rank 0 over xGMI as 256 MB ncclBroadcast pieces on a dedicated stream.  Returns
+ * 0 on success. */
 int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n);
 int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank);
 
