@@ -274,12 +274,12 @@ struct BmStage {
     PfW<T> w[NW];
     h8 a[8];
     float da[4];
-    u32x4 bp[4];
+    h8 bs;  // sumi A fragment (K-quants with mins): the bsum pairs of token lane & 15
 };
 
 template <int T, int NW>
 __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[NW], const uint8_t* aq,
-                                        const int16_t* abs, const float* ad, int s, int S, int nt, int exp = 0) {
+                                        const uint8_t* abf, const float* ad, int s, int S, int nt, int exp = 0) {
     const int lane = threadIdx.x & 63, n = lane & 15, grp = lane >> 4;
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) st.w[wi] = pf_w_load<T>(rp[wi], s, S);
@@ -298,12 +298,11 @@ __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[N
     for (int i = 0; i < 4; ++i) {
         const int t = 4 * grp + i;
         st.da[i] = 0.f;
-        if constexpr (T != T_Q6_K) st.bp[i] = u32x4{0u, 0u, 0u, 0u};
         if (t < ntl) {
             st.da[i] = ad[(size_t)t * S + s];
-            if constexpr (T != T_Q6_K) st.bp[i] = *(const u32x4*)(abs + ((size_t)t * S + s) * 8);
         }
     }
+    if constexpr (T != T_Q6_K) st.bs = n < ntl ? *(const h8*)(abf + pf_abf_off(n, s, grp, S)) : h8{};
 }
 
 // the stage's terms tm[wi][chain][i] (token 4 grp + i, row lane & 15)
@@ -316,7 +315,7 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
         h2 slo{}, shi{}, slo_o{}, shi_o{};
         h2 s6[8], s6o[8];
         float dw, dmw = 0.f;
-        uint32_t mp[4] = {0u, 0u, 0u, 0u};
+        h8 bm{};  // sumi B fragment: (min, 64 min) of sub-blocks 2 grp, 2 grp + 1
         if constexpr (T == T_Q4_K || T == T_Q5_K) {
             int sc0, m0, sc1, m1;
             scale_min(2 * grp, w.hdr.y, w.hdr.z, w.hdr.w, sc0, m0);
@@ -327,13 +326,10 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
             shi_o = shi * h2{(_Float16)1024.f, (_Float16)1024.f};
             dw = h2f(w.hdr.x);
             dmw = h2f(w.hdr.x >> 16);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                int a0, b0, a1, b1;
-                scale_min(2 * j, w.hdr.y, w.hdr.z, w.hdr.w, a0, b0);
-                scale_min(2 * j + 1, w.hdr.y, w.hdr.z, w.hdr.w, a1, b1);
-                mp[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
-            }
+            bm[0] = (_Float16)(float)m0;
+            bm[1] = (_Float16)(float)(64 * m0);
+            bm[2] = (_Float16)(float)m1;
+            bm[3] = (_Float16)(float)(64 * m1);
         } else {  // Q6_K: sc = 16 sh + sl per sub-block 4 grp + k
             dw = h2f(w.d);
 #pragma unroll
@@ -366,17 +362,12 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
 #pragma unroll
             for (int i = 0; i < 4; ++i) tm[wi][l][i] = d[i] * acc[i];
         }
+        // sumi = mins . bsum pairs on the MFMA (every product and partial sum an integer
+        // < 2^24: exact, prefill.hip.inc k_pf_quant); the term -(dmin * d_a) * sumi
+        f4 sm{0.f, 0.f, 0.f, 0.f};
+        if constexpr (T != T_Q6_K) sm = mfma16(st.bs, bm, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if constexpr (T != T_Q6_K) {
-                int si = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) si = __builtin_amdgcn_sdot2(as_h2s(mp[j]), as_h2s(st.bp[i][j]), si, false);
-                tm[wi][8][i] = -(dm[i] * (float)si);
-            } else {
-                tm[wi][8][i] = 0.f;
-            }
-        }
+        for (int i = 0; i < 4; ++i) tm[wi][8][i] = T != T_Q6_K ? -(dm[i] * sm[i]) : 0.f;
     }
 }
 
@@ -410,7 +401,7 @@ __device__ __forceinline__ void bm_tile(const MVArgs& A, int tile, int& si, int&
 // this tile's last fold and epilogue.  LDS: two round buffers of terms (parity of the
 // iteration) and the chain results G of the tile just finished.
 template <int T, int EPI>
-__global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const int16_t* abs, const float* ad, int nt,
+__global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
                                               int ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;   // weight matrices (SWIGLU: gate, up)
@@ -430,7 +421,7 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
     constexpr int NI = NW * NC * 32;
     float4 fs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
     BmStage<T, NW> cur;
-    bm_load<T, NW>(cur, rp, aq, abs, ad, wave < S ? wave : S - 1, S, nt, A.prio_alt);
+    bm_load<T, NW>(cur, rp, aq, abf, ad, wave < S ? wave : S - 1, S, nt, A.prio_alt);
     int rho = 0, it = 0;
     for (;;) {
         // the next iteration: (tile, rho + 1) or (tile + grid, 0); its loads now
@@ -445,7 +436,7 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
         bm_tile<T, EPI, NW>(A, has_next ? tn : tile, sin, row0n, rpn);  // unconditional (no scratch copies)
         const int s = rho * kBmW + wave, sn = rn * kBmW + wave;
         BmStage<T, NW> nxt;
-        bm_load<T, NW>(nxt, rpn, aq, abs, ad, sn < S ? sn : S - 1, S, nt, A.prio_alt);
+        bm_load<T, NW>(nxt, rpn, aq, abf, ad, sn < S ? sn : S - 1, S, nt, A.prio_alt);
         float4* Tm = TmB + (it & 1) * kBuf;
         if (s < S) {
             float tm[NW][9][4];
@@ -706,7 +697,7 @@ static int bmm_cap(const void* k, size_t lds) {
 }
 
 template <int T, int EPI>
-static hipError_t bmm_launch(const MVArgs& a, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
+static hipError_t bmm_launch(const MVArgs& a, const void* aq, const void* abf, const float* ad, int nt, hipStream_t s) {
     auto k = k_bmm<T, EPI>;
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
     const size_t lds = (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
@@ -720,31 +711,31 @@ static hipError_t bmm_launch(const MVArgs& a, const void* aq, const int16_t* abs
 #if defined(LLMI_EXPERIMENTS)
     MVArgs ax = a;
     ax.prio_alt = getenv("LLMI_BMM_EXP") ? atoi(getenv("LLMI_BMM_EXP")) : 0;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, ax, (const uint8_t*)aq, abs, ad, nt, ntiles);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, ax, (const uint8_t*)aq, (const uint8_t*)abf, ad, nt, ntiles);
 #else
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, a, (const uint8_t*)aq, abs, ad, nt, ntiles);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, a, (const uint8_t*)aq, (const uint8_t*)abf, ad, nt, ntiles);
 #endif
     return hipGetLastError();
 }
 
 template <int T>
-static hipError_t bmm_epi(const MVArgs& a, int epi, const void* aq, const int16_t* abs, const float* ad, int nt, hipStream_t s) {
+static hipError_t bmm_epi(const MVArgs& a, int epi, const void* aq, const void* abf, const float* ad, int nt, hipStream_t s) {
     switch (epi) {
-        case EPI_STORE: return bmm_launch<T, EPI_STORE>(a, aq, abs, ad, nt, s);
-        case EPI_ADD: return bmm_launch<T, EPI_ADD>(a, aq, abs, ad, nt, s);
-        case EPI_QKV: return bmm_launch<T, EPI_QKV>(a, aq, abs, ad, nt, s);
-        case EPI_SWIGLU: return bmm_launch<T, EPI_SWIGLU>(a, aq, abs, ad, nt, s);
-        case EPI_LOGITS: return bmm_launch<T, EPI_LOGITS>(a, aq, abs, ad, nt, s);
+        case EPI_STORE: return bmm_launch<T, EPI_STORE>(a, aq, abf, ad, nt, s);
+        case EPI_ADD: return bmm_launch<T, EPI_ADD>(a, aq, abf, ad, nt, s);
+        case EPI_QKV: return bmm_launch<T, EPI_QKV>(a, aq, abf, ad, nt, s);
+        case EPI_SWIGLU: return bmm_launch<T, EPI_SWIGLU>(a, aq, abf, ad, nt, s);
+        case EPI_LOGITS: return bmm_launch<T, EPI_LOGITS>(a, aq, abf, ad, nt, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const int16_t* abs, const float* ad, hipStream_t s) {
+hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const void* abf, const float* ad, hipStream_t s) {
     if (nt < 1 || nt > kMaxBatch || !bmm_ok(a, epi)) return hipErrorInvalidValue;
     switch (a.seg[0].type) {
-        case T_Q4_K: return bmm_epi<T_Q4_K>(a, epi, aq, abs, ad, nt, s);
-        case T_Q5_K: return bmm_epi<T_Q5_K>(a, epi, aq, abs, ad, nt, s);
-        case T_Q6_K: return bmm_epi<T_Q6_K>(a, epi, aq, abs, ad, nt, s);
+        case T_Q4_K: return bmm_epi<T_Q4_K>(a, epi, aq, abf, ad, nt, s);
+        case T_Q5_K: return bmm_epi<T_Q5_K>(a, epi, aq, abf, ad, nt, s);
+        case T_Q6_K: return bmm_epi<T_Q6_K>(a, epi, aq, abf, ad, nt, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -52,7 +52,7 @@ Context::~Context() {
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
     void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad, pf_abf, pf_wsc,
-                    bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad};
+                    bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad, babf};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -702,6 +702,8 @@ static bool balloc(Context& c, std::string& err) {
     HIPC(hipMalloc(&c.babs, B * (maxc / 16) * 2));
     HIPC(hipMalloc(&c.bad, B * (maxc / 32) * 4));
     HIPC(hipMemsetAsync(c.baq, 0, 32 * maxc * 2, c.stream));
+    HIPC(hipMalloc(&c.babf, 32 * (maxc / 256) * 64));
+    HIPC(hipMemsetAsync(c.babf, 0, 32 * (maxc / 256) * 64, c.stream));
     // padded slots read these rows: finite (zeros); their positions 0.  On the context
     // stream (a null-stream memset is not ordered with it: it could land after the slot
     // map upload that follows and point every slot at sequence 0)
@@ -739,11 +741,11 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     auto bmv = [&](const MVArgs& a, int epi, bool& quantized) -> hipError_t {
         if (nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
         if (!quantized) {
-            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, nullptr, c.stream);
+            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream);
             if (e != hipSuccess) return e;
             quantized = true;
         }
-        return launch_bmm(a, epi, nt, c.baq, c.babs, c.bad, c.stream);
+        return launch_bmm(a, epi, nt, c.baq, c.babf, c.bad, c.stream);
     };
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m.layers[(size_t)l];

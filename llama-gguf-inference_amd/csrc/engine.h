@@ -106,6 +106,7 @@ struct Context {
     void* baq = nullptr;           // k_bmm: the step's quantized activations (pf_quant layout, 32 token rows)
     int16_t* babs = nullptr;
     float* bad = nullptr;
+    void* babf = nullptr;          // k_bmm: the step's bsum pairs as sumi MFMA fragments (pf_abf_off)
     std::vector<int> btseq_host;            // the slot -> sequence map btseq holds
     std::map<std::string, hipGraphExec_t> bgraphs;  // by (slots, sequences, KV bucket)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -129,7 +129,8 @@ hipError_t launch_mvn(const MVArgs& a, int epi, int nt, int max_blocks, hipStrea
 // abs, ad) first.  bmm_ok: whether launch_bmm takes these segments (else launch_mvn).
 bool bmm_ok(const MVArgs& a, int epi);
 int bmm_min_tokens();
-hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const int16_t* abs, const float* ad, hipStream_t s);
+// (abf: k_pf_quant's bsum fragments; the dmin chain's sumi runs on the MFMA)
+hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const void* abf, const float* ad, hipStream_t s);
 hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
                              hipStream_t s);
 size_t mvn_lds_bytes(int act, int cols, int nt);

@@ -20,6 +20,12 @@ __host__ __device__ inline size_t pf_aq_off(int t, int stage, int entry, int nst
     return ((((size_t)(t >> 5) * nstage + stage) * 32 + entry) * 32 + (t & 31)) * 16;
 }
 
+// bsum pairs as the A fragments of the sumi MFMA (k_pf_quant's abf): [T/32][stage][4 g]
+// [32 tokens][8 f16] = (lo, hi) of pairs 2g, 2g + 1 and four zeros, pair = 64 hi + lo
+__host__ __device__ inline size_t pf_abf_off(int t, int stage, int g, int nstage) {
+    return ((((size_t)(t >> 5) * nstage + stage) * 4 + g) * 32 + (t & 31)) * 16;
+}
+
 // one lane's weights of a stage: row lane & 15, chunk(s) of lane group lane >> 4
 template <int T>
 struct PfW {
