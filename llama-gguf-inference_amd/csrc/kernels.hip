@@ -1123,7 +1123,7 @@ static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipSt
 // bit-identical results, or limits lowered so a test reaches a fallback / fault path.
 int g_pf_attn_simple = 0;               // batched-prefill attention: one head per workgroup
 int g_pf_gemm_ng = 2;                   // k_pf_gemm 32-token groups per workgroup (1 or 2)
-int g_pf_fa_cfg = 441;                  // k_pf_fa configuration (prefill.hip.inc pf_fa_launch)
+int g_pf_fa_cfg = 440;                  // k_pf_fa configuration (prefill.hip.inc pf_fa_launch)
 int g_pf_attn_fa = 1;                   // batched-prefill attention: tiled FP64-MFMA kernel when it applies
 int g_pf_max_kv = kPfAttnMaxKV;         // longest KV the batched-prefill attention takes
 int g_xspin_limit = kXSpinLimit;        // k_attn_x bounded-wait polls before it faults

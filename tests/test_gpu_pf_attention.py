@@ -166,7 +166,7 @@ def test_pf_attention_rejects_bad_shapes(gpu):
     assert L.llmi_pf_attention(24, 8, 128, 16, 0, 256, 1, 1, 1, 1, 0, 0) < 0   # G = 3: no tiled kernel
 
 
-@pytest.mark.parametrize("cfg", [410, 420, 421, 220, 221, 241])
+@pytest.mark.parametrize("cfg", [410, 420, 421, 441, 220, 221, 241])
 @pytest.mark.parametrize("H,HK,D,T,pos0", [(32, 8, 128, 37, 700), (32, 4, 64, 40, 300), (8, 8, 64, 70, 130)])
 def test_pf_attention_kernel_configurations(gpu, cfg, H, HK, D, T, pos0):
     """k_pf_fa's other configurations (row blocks per workgroup, waves per block, e kept

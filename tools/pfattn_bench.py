@@ -33,9 +33,9 @@ for pos0 in P0:
     out = torch.empty(T * H * D, device="cuda")
     pairs = H * sum(pos0 + t + 1 for t in range(T))
     flops = 4.0 * D * pairs
-    for mv in MODES + ([-410, -420, -421, -221, -241] if 0 in MODES else []):
+    for mv in MODES + ([-410, -420, -421, -441, -221, -241] if 0 in MODES else []):
         mode = max(mv, 0)
-        L.llmi_test_option(b"pf_fa_cfg", -mv if mv < 0 else 441)
+        L.llmi_test_option(b"pf_fa_cfg", -mv if mv < 0 else 440)
         best = None
         for _ in range(3):
             us = L.llmi_pf_attention(H, HK, D, T, pos0, n_ctx, q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
@@ -45,12 +45,12 @@ for pos0 in P0:
             best = us if best is None else min(best, us)
         rec = {"pos0": pos0, "mode": mode, "us": None if best is None else round(best, 1)}
         if mode == 0:
-            rec["fa_cfg"] = -mv if mv < 0 else 441
+            rec["fa_cfg"] = -mv if mv < 0 else 440
         if best is not None:
             rec["tflops"] = round(flops / best / 1e6, 2)
         else:
             rec["error"] = llmi.last_error()
         res["runs"].append(rec)
         print(f"[pfattn] pos0={pos0} mode={mode}: {rec}", file=sys.stderr, flush=True)
-L.llmi_test_option(b"pf_fa_cfg", 441)
+L.llmi_test_option(b"pf_fa_cfg", 440)
 print(json.dumps(res))
