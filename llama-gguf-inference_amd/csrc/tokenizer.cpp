@@ -304,7 +304,8 @@ void Tokenizer::init_common() {
 std::unique_ptr<Tokenizer> Tokenizer::from_gguf(const GgufFile& f, int n_vocab_fallback) {
     std::vector<std::string> tokens;
     if (const GgufKV* kv = f.kv("tokenizer.ggml.tokens")) tokens = kv->arr_str;
-    if (tokens.empty()) {
+    const bool synthetic = tokens.empty();
+    if (synthetic) {
         tokens.resize((size_t)std::max(0, n_vocab_fallback));
         for (size_t i = 0; i < tokens.size(); ++i) tokens[i] = "<tok_" + std::to_string(i) + ">";
     }
@@ -314,6 +315,9 @@ std::unique_ptr<Tokenizer> Tokenizer::from_gguf(const GgufFile& f, int n_vocab_f
     std::vector<int> types;
     if (const GgufKV* kv = f.kv("tokenizer.ggml.token_type"))
         for (double d : kv->arr_num) types.push_back((int)d);
+    // placeholder pieces of a GGUF without a vocabulary are UNUSED, not CONTROL: they never
+    // enter the special-token partition (a scan over n_vocab specials per tokenize call)
+    if (synthetic) types.assign(tokens.size(), TT_UNUSED);
     std::vector<std::string> merges;
     if (const GgufKV* kv = f.kv("tokenizer.ggml.merges")) merges = kv->arr_str;
     auto tk = build(f.str("tokenizer.ggml.model", "llama"), f.str("tokenizer.ggml.pre", "default"), std::move(tokens),
