@@ -863,7 +863,13 @@ bool prefill_supported(const Model& m) {
 static bool prefill_alloc(Context& c, std::string& err) {
     if (c.pf_cap) return true;
     const HParams& hp = c.m->hp;
-    const int cap = 512;  // ubatch (llama.cpp's default n_ubatch), a multiple of 32
+    // ubatch (llama.cpp's default n_ubatch 512; LLMI_PF_UBATCH, a multiple of 64 up to
+    // 4096, for A/B), a multiple of 64 (k_pf_gemm's token groups)
+    int cap = 512;
+    if (const char* e = getenv("LLMI_PF_UBATCH")) {
+        const int v = atoi(e);
+        if (v >= 64 && v <= 4096 && v % 64 == 0) cap = v;
+    }
     const size_t E = hp.n_embd, QD = (size_t)hp.n_head * hp.head_dim, F = hp.n_ff;
     const size_t maxc = std::max({E, QD, F});
     HIPC(hipMalloc(&c.pf_tok, cap * 4));
@@ -950,8 +956,9 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
             PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.ffn_norm.off_a), hp.eps, E, act_kind(L.wg.type), T,
                                 c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
             g.w = seg_of(m, L.wg, 0); g.w2 = seg_of(m, L.wu, 0); g.rows = (int)L.wg.rows; g.cols = E; g.y = c.pf_h; g.ldy = F;
-            {  // gate into h, then h = silu(h) * up (two launches: a fused gate+up kernel
-               // holds both matrices' chains and ran at one wave per SIMD)
+            {  // gate into h, then h = silu(h) * up (two launches: a fused gate+up launch
+               // spills past 256 VGPRs and measured slower: Mistral 2048 TTFT 229 vs 225
+               // ms, 8B 180 vs 165, profiles/r04/prefill/swiglu_fused_vs_two.txt)
                 if (act_kind(L.wu.type) != act_kind(L.wg.type)) {
                     err = "prefill: ffn_gate/ffn_up of different activation kinds";
                     return false;
