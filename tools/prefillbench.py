@@ -33,6 +33,10 @@ if lens and not os.path.exists(path):
     llmi.write_synthetic_gguf(path + ".tmp", preset, seed=3)
     os.replace(path + ".tmp", path)
 out = {"preset": preset, "prompts": {}}
+for env, opt in (("PF_GEMM_NG", b"pf_gemm_ng"),):  # A/B knobs (test options)
+    if os.environ.get(env):
+        lib().llmi_test_option(opt, int(os.environ[env]))
+        out[env.lower()] = int(os.environ[env])
 if lens:  # an empty length list times the GEMM shapes alone (no model)
     m = llmi.Model(path)
     n_ctx = (max(lens + [1]) + 2 + 255) // 256 * 256
@@ -66,8 +70,6 @@ for n in lens:
 from helpers import Q4_K, Q6_K, empty_dev, random_blocks, to_dev  # noqa: E402
 
 L = lib()
-if os.environ.get("PF_GEMM_NG"):
-    L.llmi_test_option(b"pf_gemm_ng", int(os.environ["PF_GEMM_NG"]))
 g = {}
 for (qt, rows, cols) in ((Q4_K, 14336, 4096), (Q4_K, 4096, 14336), (Q6_K, 4096, 14336), (Q4_K, 4096, 4096),
                          (Q6_K, 14336, 4096), (Q6_K, 4096, 4096)):
