@@ -1122,6 +1122,11 @@ static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipSt
 // Test options (llmi_test_option; never read from the environment): paths that give
 // bit-identical results, or limits lowered so a test reaches a fallback / fault path.
 int g_pf_attn_simple = 0;               // batched-prefill attention: one head per workgroup
+#ifndef LLMI_PF_QUANT_BPC
+#define LLMI_PF_QUANT_BPC 2
+#endif
+int g_pf_quant_bpc = LLMI_PF_QUANT_BPC;  // k_pf_quant: 256-element blocks per workgroup when rows are split (0: never)
+int g_pf_quant_split_below = 64;  // ... i.e. below this many rows (batched decode)
 int g_pf_gemm_ng = 2;                   // k_pf_gemm 32-token groups per workgroup (1 or 2)
 int g_pf_fa_cfg = 440;                  // k_pf_fa configuration (prefill.hip.inc pf_fa_launch)
 int g_pf_attn_fa = 1;                   // batched-prefill attention: tiled FP64-MFMA kernel when it applies

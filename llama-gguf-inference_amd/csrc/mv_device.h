@@ -308,8 +308,10 @@ __device__ __forceinline__ void load_sub(const MVArgs& A, const ProRegs<NORM, NP
         }
     }
 }
-template <int ACT, bool NORM, int NP, int NT = kMVThreads>
-__device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
+// RMSNorm scale of the row (1 without NORM): per-thread double sums over sub-blocks tid,
+// tid + NT, ... then the block reduction (every caller the same order, so the same bits)
+template <bool NORM, int NP, int NT = kMVThreads>
+__device__ __forceinline__ float mv_norm_scale(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
     const int tid = threadIdx.x, cols = A.cols;
     const int nsub = cols / 16;
     float scale = 1.0f;
@@ -331,6 +333,13 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
         const float mean = (float)(s / (double)cols);
         scale = 1.0f / sqrtf(mean + A.eps);
     }
+    return scale;
+}
+template <int ACT, bool NORM, int NP, int NT = kMVThreads>
+__device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
+    const int tid = threadIdx.x, cols = A.cols;
+    const int nsub = cols / 16;
+    const float scale = mv_norm_scale<NORM, NP, NT>(A, L, R);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
         const int sb = tid + i * NT;
