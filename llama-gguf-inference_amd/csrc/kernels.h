@@ -22,7 +22,7 @@ constexpr int kDimAttnMaxKV = 1024;  // dim-split one-launch attention (k_attn_d
 constexpr int kRegAttnMaxKV = 512;  // register-prefetched one-launch attention (k_attn_r) up to this KV bound  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
-extern int g_pf_gemm_ng, g_pf_quant_bpc, g_pf_quant_split_below, g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
+extern int g_pf_gemm_ng, g_pf_xcd_map, g_pf_quant_bpc, g_pf_quant_split_below, g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
 int pf_max_kv();  // llama_decode hands prompt runs reaching past this KV length to decode steps
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
 // + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
@@ -150,6 +150,7 @@ struct PfGemm {
     Seg w, w2;                 // weights (SWIGLU: w = gate, w2 = up)
     int rows = 0, cols = 0;
     int T = 0;                 // tokens (activation rows are padded to a multiple of 64)
+    int xcd_map = 0;           // set by the launcher: XCD-aware tile order (k_pf_gemm)
     const void* aq = nullptr;     // f16 MFMA fragments of the q8 activations (prefill.hip.inc pf_aq_off), Tpad x cols x 2 B
     const int16_t* abs = nullptr; // [Tpad][cols/32] bsum pairs (q8_K)
     const float* ad = nullptr;    // [Tpad][cols/256] (q8_K) or [Tpad][cols/32] (q8_0) d

@@ -1127,6 +1127,10 @@ int g_pf_attn_simple = 0;               // batched-prefill attention: one head p
 #endif
 int g_pf_quant_bpc = LLMI_PF_QUANT_BPC;  // k_pf_quant: 256-element blocks per workgroup when rows are split (0: never)
 int g_pf_quant_split_below = 64;  // ... i.e. below this many rows (batched decode)
+#ifndef LLMI_PF_XCD_MAP
+#define LLMI_PF_XCD_MAP 1
+#endif
+int g_pf_xcd_map = LLMI_PF_XCD_MAP;  // k_pf_gemm: XCD-aware tile order
 int g_pf_gemm_ng = 2;                   // k_pf_gemm 32-token groups per workgroup (1 or 2)
 int g_pf_fa_cfg = 440;                  // k_pf_fa configuration (prefill.hip.inc pf_fa_launch)
 int g_pf_attn_fa = 1;                   // batched-prefill attention: tiled FP64-MFMA kernel when it applies
