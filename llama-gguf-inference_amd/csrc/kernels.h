@@ -150,7 +150,7 @@ struct PfGemm {
     Seg w, w2;                 // weights (SWIGLU: w = gate, w2 = up)
     int rows = 0, cols = 0;
     int T = 0;                 // tokens (activation rows are padded to a multiple of 64)
-    int xcd_map = 0;           // set by the launcher: XCD-aware tile order (k_pf_gemm)
+    int xcd_map = 0;           // set by the launcher: XCD-aware tile order, token-group chunk (k_pf_gemm; 0 off)
     const void* aq = nullptr;     // f16 MFMA fragments of the q8 activations (prefill.hip.inc pf_aq_off), Tpad x cols x 2 B
     const int16_t* abs = nullptr; // [Tpad][cols/32] bsum pairs (q8_K)
     const float* ad = nullptr;    // [Tpad][cols/256] (q8_K) or [Tpad][cols/32] (q8_0) d

@@ -51,3 +51,17 @@ def gpu():
 
     assert llmi.device_count() > 0
     return torch.device("cuda:0")
+
+
+def pytest_sessionstart(session):
+    """LLMI_TEST_OPTIONS="name=value,...": set libllmi test options (A/B launch knobs,
+    every value bit-identical) for the whole session, e.g. to run the parity tests under
+    a non-default kernel configuration."""
+    opts = os.environ.get("LLMI_TEST_OPTIONS")
+    if not opts:
+        return
+    import llmi
+
+    for kv in opts.split(","):
+        name, value = kv.split("=")
+        llmi.test_option(name.strip(), int(value))
