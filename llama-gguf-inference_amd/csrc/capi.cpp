@@ -599,6 +599,7 @@ int32_t llmi_test_option(const char* name, int32_t value) {
     if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
     else if (!strcmp(name, "pf_attn_fa")) opt = &g_pf_attn_fa;
     else if (!strcmp(name, "pf_gemm_ng")) opt = &g_pf_gemm_ng;
+    else if (!strcmp(name, "pf_qkv_merge")) opt = &g_pf_qkv_merge;
     else if (!strcmp(name, "pf_xcd_map")) opt = &g_pf_xcd_map;
     else if (!strcmp(name, "pf_quant_bpc")) opt = &g_pf_quant_bpc;
     else if (!strcmp(name, "pf_quant_split_below")) opt = &g_pf_quant_split_below;

@@ -930,17 +930,32 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
             // q, k, v (each quantized for its own activation kind)
             const DevMat* qkv[3] = {&L.wq, &L.wk, &L.wv};
             int quant_kind = -1;
-            for (int part = 0; part < 3; ++part) {
+            // consecutive same-type parts (rows multiples of 64) share one launch
+            for (int part = 0; part < 3;) {
                 const DevMat& W = *qkv[part];
                 if (act_kind(W.type) != quant_kind) {
                     quant_kind = act_kind(W.type);
                     PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.attn_norm.off_a), hp.eps, E, quant_kind, T,
                                         c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
                 }
-                g.w = seg_of(m, W, 0); g.rows = (int)W.rows; g.cols = E; g.part = part;
+                int end = part + 1;
+                while (g_pf_qkv_merge && end < 3 && qkv[end]->type == W.type && qkv[end - 1]->rows % 64 == 0) ++end;
+                g.w = seg_of(m, W, 0); g.rows = (int)W.rows; g.cols = E; g.part = part; g.r1 = g.r2 = 0;
+                if (end > part + 1) {
+                    g.wk = seg_of(m, *qkv[part + 1], 0);
+                    g.r1 = (int)W.rows;
+                    g.r2 = g.r1 + (int)qkv[part + 1]->rows;
+                    g.rows = g.r2;
+                    if (end > part + 2) {
+                        g.wv = seg_of(m, *qkv[part + 2], 0);
+                        g.rows += (int)qkv[part + 2]->rows;
+                    }
+                }
                 g.y = c.pf_q; g.ldy = nq;
                 PFC(launch_pf_gemm(g, EPI_QKV, c.stream));
+                part = end;
             }
+            g.r1 = g.r2 = 0;
             (void)nk;
             PfAttn at;
             at.q = c.pf_q; at.out = c.pf_att; at.ldq = nq; at.kc = g.kc; at.vc = g.vc;

@@ -22,7 +22,7 @@ constexpr int kDimAttnMaxKV = 1024;  // dim-split one-launch attention (k_attn_d
 constexpr int kRegAttnMaxKV = 512;  // register-prefetched one-launch attention (k_attn_r) up to this KV bound  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
-extern int g_pf_gemm_ng, g_pf_xcd_map, g_pf_quant_bpc, g_pf_quant_split_below, g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
+extern int g_pf_gemm_ng, g_pf_qkv_merge, g_pf_xcd_map, g_pf_quant_bpc, g_pf_quant_split_below, g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
 int pf_max_kv();  // llama_decode hands prompt runs reaching past this KV length to decode steps
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
 // + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
@@ -158,6 +158,11 @@ struct PfGemm {
     float* y = nullptr;        // STORE / ADD / SWIGLU / QKV q: [T][ldy]
     int ldy = 0;
     int part = 0;              // QKV: 0 q (RoPE, f32 to y), 1 k (RoPE, f16 cache), 2 v (f16 cache)
+    // QKV over consecutive same-type parts in one launch: rows [0, r1) are part `part` of w,
+    // [r1, r2) part + 1 of wk, [r2, rows) part + 2 of wv (r1 = 0: one part); r1, r2
+    // multiples of 64 (workgroup rows)
+    Seg wk, wv;
+    int r1 = 0, r2 = 0;
     uint16_t* kc = nullptr;    // layer K cache [HK][n_ctx][D]
     uint16_t* vc = nullptr;    // layer V cache [HK][D][n_ctx]
     const float* rope = nullptr;

@@ -1131,6 +1131,7 @@ int g_pf_quant_split_below = 64;  // ... i.e. below this many rows (batched deco
 #define LLMI_PF_XCD_MAP 1
 #endif
 int g_pf_xcd_map = LLMI_PF_XCD_MAP;  // k_pf_gemm: XCD-aware tile order
+int g_pf_qkv_merge = 1;            // prefill: consecutive same-type q/k/v parts in one GEMM launch
 int g_pf_gemm_ng = 2;                   // k_pf_gemm 32-token groups per workgroup (1 or 2)
 int g_pf_fa_cfg = 440;                  // k_pf_fa configuration (prefill.hip.inc pf_fa_launch)
 int g_pf_attn_fa = 1;                   // batched-prefill attention: tiled FP64-MFMA kernel when it applies

@@ -33,7 +33,7 @@ if lens and not os.path.exists(path):
     llmi.write_synthetic_gguf(path + ".tmp", preset, seed=3)
     os.replace(path + ".tmp", path)
 out = {"preset": preset, "prompts": {}}
-for env, opt in (("PF_GEMM_NG", b"pf_gemm_ng"), ("PF_XCD_MAP", b"pf_xcd_map")):  # A/B knobs (test options)
+for env, opt in (("PF_GEMM_NG", b"pf_gemm_ng"), ("PF_XCD_MAP", b"pf_xcd_map"), ("PF_QKV_MERGE", b"pf_qkv_merge")):  # A/B knobs (test options)
     if os.environ.get(env):
         lib().llmi_test_option(opt, int(os.environ[env]))
         out[env.lower()] = int(os.environ[env])
