@@ -49,7 +49,14 @@ struct llama_model_params {
     bool use_mmap;         /* always true in llmi; kept for signature parity */
     bool no_upload;        /* llmi: build the device arena layout but leave it unfilled
                               (a replica that will receive the arena by RCCL broadcast) */
+    int32_t numerics;      /* llmi: the fp32 association every kernel reproduces bit for bit,
+                              fixed at load (the weights' device byte order depends on it):
+                              LLMI_NUMERICS_GENERIC (default) ggml's generic scalar order;
+                              LLMI_NUMERICS_X86 upstream's x86 AVX2 build, the reference's
+                              NGL=0 path (Dockerfile.cpu:11) — DESIGN.md §5 */
 };
+#define LLMI_NUMERICS_GENERIC 0
+#define LLMI_NUMERICS_X86 1
 
 /* upstream llama_context_params (subset) */
 struct llama_context_params {
@@ -153,6 +160,8 @@ int32_t llmi_seq_pos_max(const struct llama_context* ctx, llama_seq_id seq_id);
 
 /* ---------- llmi extras ---------- */
 const char* llmi_last_error(void);
+/* the model's numerics (llama_model_params.numerics), -1 for NULL */
+int32_t llmi_model_numerics(const struct llama_model* model);
 int32_t llmi_device_count(void);
 /* device-side argmax of the logits of batch entry i (-1 = last); first max wins, as
  * upstream llama_sampler_greedy.  Avoids the n_vocab*4 B logits copy. */
@@ -194,7 +203,10 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
  *   "xspin_limit"     polls before k_attn_x's bounded wait gives up; a give-up makes the
  *                     decode call return -6 with llmi_last_error set (fault surfacing)
  *   "xtag_skew"       1: k_attn_x consumers wait for a tag no producer writes (with
- *                     xspin_limit 0: every such wait gives up at once; fault-path test) */
+ *                     xspin_limit 0: every such wait gives up at once; fault-path test)
+ *   "numerics"        this thread's numerics for the kernel-level entry points below
+ *                     (llmi_repack's byte order, llmi_matvec, llmi_quantize_act,
+ *                     llmi_attention, llmi_pf_attention): LLMI_NUMERICS_* */
 int32_t llmi_test_option(const char* name, int32_t value);
 /* Algorithmic bytes of one decode step at KV length n_kv (weights + one embedding row
  * + norms + KV read/write), the numerator of achieved GB/s. */

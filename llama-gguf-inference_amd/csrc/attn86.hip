@@ -1,0 +1,296 @@
+// attn86.hip — decode and prefill attention in the x86 association mode (model numerics
+// LLMI_NUMERICS_X86; mv_device.h "x86 numerics").
+//
+// Upstream's non-flash CPU attention [upstream ggml-cpu ops.cpp mul_mat + soft_max,
+// vec.h ggml_vec_dot_f16 / ggml_vec_soft_max_f32, simd-mappings.h; recalled, not
+// vendored] on an x86 AVX2+F16C build, as the oracle's x86 mode restates it
+// (oracle/ggml_oracle.c x86_dot_f16f, attn_head with OR_X86_F16DOT | OR_X86_VEXP):
+//   kq[t]  = dot_f16(K[t], f16(q)): element i accumulates into lane (i % 32) of 4 x 8 fp32
+//            fma chains (i in order), reduced acc0 + acc2, acc1 + acc3, then those two,
+//            then lo4 + hi4 and two hadds: ((t0 + t1) + (t2 + t3))
+//   w[t]   = kq[t] * (1 / sqrt(D)); M = max w
+//   e[t]   = ggml_v_expf(w[t] - M); S = double sum over 8-position chunks of the chunk's
+//            fp32 hsum_float_8 (the row padded to 32 with masked zeros)
+//   p[t]   = f16(e[t] * (float)(1 / S))
+//   out[d] = dot_f16(V[d][.], p) over the positions padded to 32 (p = 0, V = 0 past n_kv),
+//            the same 4 x 8-lane association over positions.
+// The fp32 chains are exact sequences (one lane per chain); only the double sum of chunk
+// sums is reordered (a lane tree, absorbed by double as on every other path).
+//
+//   decode:  k_a86_scores (KV group x 64-position tile) -> k_a86_softmax (one workgroup
+//            per head, p in place of the scores) -> k_a86_pv (KV group x 16 dims)
+//   prefill: k_pf_a86 (KV group x query token), scores and p in LDS
+#include "kernels.h"
+#include "launch_util.h"
+#include "mv_device.h"
+
+namespace llmi {
+
+// the 32 fp32 chains of ggml_vec_dot_f16 (x86), reduced as upstream's GGML_F16_VEC_REDUCE
+__device__ __forceinline__ float x86_f16dot_reduce(const float (&acc)[32]) {
+    float c[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) c[l] = (acc[l] + acc[16 + l]) + (acc[8 + l] + acc[24 + l]);
+    const float t0 = c[0] + c[4], t1 = c[1] + c[5], t2 = c[2] + c[6], t3 = c[3] + c[7];
+    return (t0 + t1) + (t2 + t3);
+}
+// the same reduction over 32 lanes (lane c holds chain c) of a 32-lane group; lane c = 0 of
+// the group gets the result
+__device__ __forceinline__ float x86_f16dot_reduce_lanes(float v) {
+    v = v + __shfl_xor(v, 16, 64);
+    v = v + __shfl_xor(v, 8, 64);
+    v = v + __shfl_xor(v, 4, 64);
+    const float a = v + __shfl_xor(v, 1, 64);  // lane 0: t0 + t1, lane 2: t2 + t3
+    return a + __shfl_xor(a, 2, 64);
+}
+
+// ---- decode ------------------------------------------------------------------------
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_a86_scores(AttnArgs a) {
+    const int g = blockIdx.x, t0 = blockIdx.y * 64;
+    const int n_kv = a.st->pos + 1;
+    if (t0 >= n_kv) return;
+    const int nt = min(64, n_kv - t0);
+    __shared__ float qs[G][D];
+    __shared__ __attribute__((aligned(16))) uint16_t ks[64][D + 8];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = h2f(f2h(a.q[(size_t)g * G * D + i]));
+    constexpr int PPR = D * 2 / 16;
+    const uint16_t* kb = a.kc + ((size_t)g * a.n_ctx + t0) * D;
+    for (int i = tid; i < nt * PPR; i += 256) *(u32x4*)&ks[i / PPR][(i % PPR) * 8] = *(const u32x4*)(kb + (size_t)(i / PPR) * D + (i % PPR) * 8);
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane >= nt) return;
+    for (int hh = wave; hh < G; hh += 4) {
+        float acc[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int d0 = 0; d0 < D; d0 += 8) {
+            const u32x4 kv = *(const u32x4*)&ks[lane][d0];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = d0 + j;
+                acc[i & 31] = __builtin_fmaf(h2f(kv[j >> 1] >> (16 * (j & 1))), qs[hh][i], acc[i & 31]);
+            }
+        }
+        a.scores[(size_t)(g * G + hh) * a.n_ctx + t0 + lane] = x86_f16dot_reduce(acc) * a.scale;
+    }
+}
+
+// softmax of one head over its scores row (in place -> p, padded with zeros to 32)
+__global__ __launch_bounds__(256) void k_a86_softmax(AttnArgs a) {
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_kv = a.st->pos + 1, np = (n_kv + 31) & ~31;
+    float* w = a.scores + (size_t)h * a.n_ctx;
+    __shared__ float redm[4];
+    __shared__ double reds[4];
+    float m = -INFINITY;
+    for (int t = tid; t < n_kv; t += 256) m = fmaxf(m, w[t]);
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
+    __syncthreads();
+    const float mx = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    // chunk c = positions 8c .. 8c+7 (masked positions: exactly 0, as v_expf(-inf))
+    double sum = 0.0;
+    for (int c = tid; 8 * c < n_kv; c += 256) {
+        float e[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) e[l] = 8 * c + l < n_kv ? x86_v_expf(w[8 * c + l] - mx) : 0.f;
+        sum += (double)x86_hsum8(e);
+    }
+    sum = wave_sum_d(sum);
+    if (lane == 0) reds[wave] = sum;
+    __syncthreads();
+    const float inv = (float)(1.0 / ((reds[0] + reds[1]) + (reds[2] + reds[3])));
+    // p over the thread's own chunks (e taken again: no thread reads another's writes)
+    for (int c = tid; 8 * c < np; c += 256) {
+        float p[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const int t = 8 * c + l;
+            p[l] = t < n_kv ? h2f(f2h(x86_v_expf(w[t] - mx) * inv)) : 0.f;
+        }
+        *(float4*)(w + 8 * c) = make_float4(p[0], p[1], p[2], p[3]);
+        *(float4*)(w + 8 * c + 4) = make_float4(p[4], p[5], p[6], p[7]);
+    }
+}
+
+// PV: thread (dim d of 16, chain c of 32): chain c runs positions c, c + 32, ... < np
+template <int D, int G>
+__global__ __launch_bounds__(512) void k_a86_pv(AttnArgs a) {
+    const int g = blockIdx.x, tid = threadIdx.x, c = tid & 31, d = blockIdx.y * 16 + (tid >> 5);
+    const int n_kv = a.st->pos + 1, np = (n_kv + 31) & ~31;
+    const uint16_t* vr = a.vc + ((size_t)g * D + d) * a.n_ctx;
+    const float* p = a.scores + (size_t)g * G * a.n_ctx;
+    float acc[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) acc[hh] = 0.f;
+    constexpr int U = 4;  // positions of a chain loaded ahead
+    for (int t0 = c; t0 < np; t0 += 32 * U) {
+        float v[U], pv[U][G];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + 32 * u;
+            const int tc = min(t, a.n_ctx - 1);
+            v[u] = t < n_kv ? h2f(vr[tc]) : 0.f;
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh) pv[u][hh] = p[(size_t)hh * a.n_ctx + tc];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + 32 * u < np)
+#pragma unroll
+                for (int hh = 0; hh < G; ++hh) acc[hh] = __builtin_fmaf(v[u], pv[u][hh], acc[hh]);
+    }
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        const float r = x86_f16dot_reduce_lanes(acc[hh]);
+        if (c == 0) a.out[(size_t)(g * G + hh) * D + d] = r;
+    }
+}
+
+template <int D, int G>
+static hipError_t a86_launch(const AttnArgs& a, int n_head, int hk, int kv_bound, hipStream_t s) {
+    launch_k(k_a86_scores<D, G>, dim3(hk, (kv_bound + 63) / 64), dim3(256), 0, s, true, false, a);
+    launch_k(k_a86_softmax, dim3(n_head), dim3(256), 0, s, false, false, a);
+    launch_k(k_a86_pv<D, G>, dim3(hk, D / 16), dim3(512), 0, s, false, true, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
+    if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    const int g = n_head / n_head_kv;
+#define LLMI_A86(D_, G_) \
+    if (head_dim == D_ && g == G_) return a86_launch<D_, G_>(a, n_head, n_head_kv, kv_bound, s);
+    LLMI_A86(128, 1) LLMI_A86(128, 2) LLMI_A86(128, 4) LLMI_A86(128, 8)
+    LLMI_A86(64, 1) LLMI_A86(64, 2) LLMI_A86(64, 4) LLMI_A86(64, 8)
+#undef LLMI_A86
+    return hipErrorInvalidValue;
+}
+
+// ---- prefill -----------------------------------------------------------------------
+// k_pf_a86: grid (HK, T), 256 threads: query token t (position pos0 + t) for the G heads of
+// KV group g, scores and p in LDS ([G][ldw], ldw = max_kv rounded up to 32); the same
+// operations as the decode kernels above.
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_pf_a86(PfAttn a) {
+    extern __shared__ __attribute__((aligned(16))) float wl[];  // [G][ldw]
+    __shared__ float qs[G][D];
+    __shared__ float redm[4][G];
+    __shared__ double reds[4][G];
+    const int g = blockIdx.x, t = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ldw = (a.max_kv + 31) & ~31;
+    const int n_kv = a.pos0 + t + 1, np = (n_kv + 31) & ~31;
+    for (int i = tid; i < G * D; i += 256) qs[i / D][i % D] = h2f(f2h(a.q[(size_t)t * a.ldq + (size_t)g * G * D + i]));
+    __syncthreads();
+    const uint16_t* K = a.kc + (size_t)g * a.n_ctx * D;
+    float mx[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) mx[hh] = -INFINITY;
+    for (int p = tid; p < n_kv; p += 256) {
+        u32x4 kr[D / 8];
+#pragma unroll
+        for (int k = 0; k < D / 8; ++k) kr[k] = *(const u32x4*)(K + (size_t)p * D + 8 * k);
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            float acc[32];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                acc[i & 31] = __builtin_fmaf(h2f(kr[i >> 3][(i & 7) >> 1] >> (16 * (i & 1))), qs[hh][i], acc[i & 31]);
+            const float w = x86_f16dot_reduce(acc) * a.scale;
+            wl[hh * ldw + p] = w;
+            mx[hh] = fmaxf(mx[hh], w);
+        }
+    }
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        const float m = wave_max(mx[hh]);
+        if (lane == 0) redm[wave][hh] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) mx[hh] = fmaxf(fmaxf(redm[0][hh], redm[1][hh]), fmaxf(redm[2][hh], redm[3][hh]));
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        double sum = 0.0;
+        for (int c = tid; 8 * c < n_kv; c += 256) {
+            float e[8];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) e[l] = 8 * c + l < n_kv ? x86_v_expf(wl[hh * ldw + 8 * c + l] - mx[hh]) : 0.f;
+            sum += (double)x86_hsum8(e);
+        }
+        sum = wave_sum_d(sum);
+        if (lane == 0) reds[wave][hh] = sum;
+    }
+    __syncthreads();  // also: every score written before any p replaces it
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        const float inv = (float)(1.0 / ((reds[0][hh] + reds[1][hh]) + (reds[2][hh] + reds[3][hh])));
+        for (int c = tid; 8 * c < np; c += 256)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) {
+                const int q = 8 * c + l;
+                wl[hh * ldw + q] = q < n_kv ? h2f(f2h(x86_v_expf(wl[hh * ldw + q] - mx[hh]) * inv)) : 0.f;
+            }
+    }
+    __syncthreads();
+    // PV: thread (chain c, dim group dg): dims dg + 8 k, G heads
+    const int c = tid & 31, dg = tid >> 5;
+    constexpr int ND = D / 8;
+    const uint16_t* V = a.vc + (size_t)g * D * a.n_ctx;
+    float acc[ND][G];
+#pragma unroll
+    for (int k = 0; k < ND; ++k)
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) acc[k][hh] = 0.f;
+    for (int q = c; q < np; q += 32) {
+        float pv[G];
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) pv[hh] = wl[hh * ldw + q];
+        const int qc = min(q, a.n_ctx - 1);
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+            const float v = q < n_kv ? h2f(V[(size_t)(dg + 8 * k) * a.n_ctx + qc]) : 0.f;
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh) acc[k][hh] = __builtin_fmaf(v, pv[hh], acc[k][hh]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < ND; ++k)
+#pragma unroll
+        for (int hh = 0; hh < G; ++hh) {
+            const float r = x86_f16dot_reduce_lanes(acc[k][hh]);
+            if (c == 0) a.out[(size_t)t * a.ldq + (size_t)(g * G + hh) * D + dg + 8 * k] = r;
+        }
+}
+
+// longest KV the prefill kernel's LDS score rows take (the rest of a prompt: decode steps)
+int pf_attn_x86_max_kv(int n_head, int n_head_kv, int head_dim) {
+    (void)head_dim;
+    const int g = n_head / n_head_kv;
+    const size_t static_lds = (size_t)g * head_dim * 4 + 4 * g * 12 + 64;
+    return (int)(((160u * 1024u - static_lds) / (4u * (size_t)g)) & ~(size_t)31);
+}
+
+hipError_t launch_pf_attn_x86(const PfAttn& a, int n_head, int n_head_kv, int head_dim, int T, hipStream_t s) {
+    if (n_head_kv <= 0 || n_head % n_head_kv || T <= 0) return hipErrorInvalidValue;
+    const int g = n_head / n_head_kv;
+    if (a.max_kv > pf_attn_x86_max_kv(n_head, n_head_kv, head_dim)) return hipErrorInvalidValue;
+    // (gfx950 takes up to 160 KiB of dynamic LDS as is; the attribute call is refused,
+    // prefill.hip.inc launch_pf_attn)
+    const size_t lds = (size_t)g * ((a.max_kv + 31) & ~31) * 4;
+#define LLMI_PA86(D_, G_)                                                                     \
+    if (head_dim == D_ && g == G_) {                                                          \
+        launch_k(k_pf_a86<D_, G_>, dim3(n_head_kv, T), dim3(256), lds, s, true, true, a);     \
+        return hipGetLastError();                                                             \
+    }
+    LLMI_PA86(128, 1) LLMI_PA86(128, 2) LLMI_PA86(128, 4) LLMI_PA86(128, 8)
+    LLMI_PA86(64, 1) LLMI_PA86(64, 2) LLMI_PA86(64, 4) LLMI_PA86(64, 8)
+#undef LLMI_PA86
+    return hipErrorInvalidValue;
+}
+
+}  // namespace llmi

@@ -87,6 +87,8 @@ extern "C" {
 
 const char* llmi_last_error(void) { return g_err.c_str(); }
 
+int32_t llmi_model_numerics(const struct llama_model* model) { return model ? model->m.numerics : -1; }
+
 void llama_backend_init(void) { (void)hipInit(0); }
 void llama_backend_free(void) {}
 
@@ -97,6 +99,7 @@ struct llama_model_params llama_model_default_params(void) {
     p.vocab_only = false;
     p.use_mmap = true;
     p.no_upload = false;
+    p.numerics = LLMI_NUMERICS_GENERIC;
     return p;
 }
 
@@ -132,7 +135,7 @@ struct llama_model* llama_model_load_from_file(const char* path, struct llama_mo
     }
     auto* m = new llama_model();
     std::string err;
-    if (!model_load(path, params.main_gpu, params.vocab_only, params.no_upload, m->m, err)) {
+    if (!model_load(path, params.main_gpu, params.vocab_only, params.no_upload, m->m, err, nullptr, params.numerics)) {
         set_err(err);
         delete m;
         return nullptr;
@@ -234,8 +237,10 @@ static bool run_seq(llama_context* ctx, const llama_batch& batch, int seq, const
     while (run < n - 1 && rows[(size_t)idx[(size_t)run]] < 0 && pos[(size_t)run] == p0 + run) ++run;
     // a run reaching past prefill_max_kv() positions (the LDS-resident attention kernels'
     // limit where the tiled one does not apply) goes through decode steps from there on
-    const int pf_lim = prefill_max_kv(c);
-    if (p0 + run > pf_lim) run = std::max(0, pf_lim - p0);
+    if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
+        const int pf_lim = prefill_max_kv(c);
+        if (p0 + run > pf_lim) run = std::max(0, pf_lim - p0);
+    }
     if (!no_pf && run >= kPrefillMin && prefill_supported(*c.m)) {
         std::vector<int32_t> toks((size_t)run);
         for (int i = 0; i < run; ++i) toks[(size_t)i] = batch.token[idx[(size_t)i]];
@@ -470,6 +475,14 @@ int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const i
         context_select_seq(c, seqs[0]);
         return llmi_generate_greedy(ctx, first[0], pos0[0], n_gen, out);
     }
+    if (c.m->numerics != NUMERICS_GENERIC) {  // no batched step in x86 numerics: one sequence after another
+        for (int k = 0; k < n; ++k) {
+            context_select_seq(c, seqs[k]);
+            const int32_t r = llmi_generate_greedy(ctx, first[k], pos0[k], n_gen, out + (size_t)k * n_gen);
+            if (r != n_gen) return r;
+        }
+        return n_gen;
+    }
     (void)hipSetDevice(c.m->device);
     (void)hipGetLastError();
     std::string err;
@@ -593,10 +606,20 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
 }
 
 
+// numerics of this thread's kernel-level entry points (llmi_test_option "numerics")
+static thread_local int t_hook_numerics = 0;
+
 int32_t llmi_test_option(const char* name, int32_t value) {
     if (!name) return -1;
     int* opt = nullptr;
+    if (!strcmp(name, "numerics")) {
+        const int old = t_hook_numerics;
+        if (value == NUMERICS_GENERIC || value == NUMERICS_X86) t_hook_numerics = value;
+        else if (value >= 0) { set_err("llmi_test_option: numerics must be 0 or 1"); return -1; }
+        return old;
+    }
     if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
+    else if (!strcmp(name, "pf_fa_noalloc")) opt = &g_pf_fa_noalloc;
     else if (!strcmp(name, "pf_attn_fa")) opt = &g_pf_attn_fa;
     else if (!strcmp(name, "pf_gemm_ng")) opt = &g_pf_gemm_ng;
     else if (!strcmp(name, "pf_qkv_merge")) opt = &g_pf_qkv_merge;
@@ -698,7 +721,9 @@ struct Fanout {
     std::vector<hipStream_t> st;
     size_t bytes = 0, next = 0;  // arena bytes; first piece not yet issued
     std::vector<hipEvent_t> evs;
-    bool ok = true;
+    bool ok = true;        // every step so far succeeded
+    bool nccl_ok = true;   // no ncclBroadcast failed: pieces must still be issued (the other
+                           // ranks wait in their matching broadcasts), whatever else failed
 
     ~Fanout() {
         for (size_t r = 0; r < st.size(); ++r) {
@@ -725,13 +750,16 @@ struct Fanout {
     // `wait`: an event on the root's upload stream the broadcast streams wait on first
     bool issue(size_t prefix, hipEvent_t wait) {
         bool waited = false;
-        while (ok && next * kFanoutChunk < bytes) {
+        while (nccl_ok && next * kFanoutChunk < bytes) {
             const size_t off = next * kFanoutChunk, len = std::min(kFanoutChunk, bytes - off);
             if (off + len > prefix) break;
             if (wait && !waited) {
                 for (size_t r = 0; r < dev.size(); ++r) {
                     (void)hipSetDevice(dev[r]);
-                    if (hipStreamWaitEvent(st[r], wait, 0) != hipSuccess) ok = false;
+                    if (hipStreamWaitEvent(st[r], wait, 0) != hipSuccess) {
+                        ok = false;  // the piece still goes out, after the upload reached it
+                        (void)hipEventSynchronize(wait);
+                    }
                 }
                 waited = true;
             }
@@ -744,7 +772,7 @@ struct Fanout {
                 const ncclResult_t ne = ncclGroupEnd();
                 if (nr == ncclSuccess) nr = ne;
             }
-            if (nr != ncclSuccess) ok = false;
+            if (nr != ncclSuccess) ok = nccl_ok = false;
             ++next;
         }
         return ok;
@@ -762,12 +790,18 @@ struct Fanout {
         return [this](size_t prefix_end, hipStream_t us) -> bool {
             hipEvent_t e = nullptr;
             (void)hipSetDevice(dev[0]);
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return ok = false;
-            evs.push_back(e);
-            if (hipEventRecord(e, us) != hipSuccess) return ok = false;
-            const bool r = issue(prefix_end, e);
+            bool local = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (local) {
+                evs.push_back(e);
+                local = hipEventRecord(e, us) == hipSuccess;
+            }
+            if (!local) {  // no event to order the pieces behind the upload: wait for it here
+                ok = false;
+                (void)hipStreamSynchronize(us);
+            }
+            issue(prefix_end, local ? e : nullptr);
             (void)hipSetDevice(dev[0]);
-            return r;
+            return ok;  // false aborts the upload; finish() still issues every remaining piece
         };
     }
 };
@@ -844,6 +878,10 @@ struct llama_model* llmi_model_load_replicated(const char* path, struct llama_mo
         set_err("llmi_model_load_replicated: bad arguments");
         return nullptr;
     }
+    if (params.n_gpu_layers == 0) {
+        set_err("llmi_model_load_replicated: n_gpu_layers=0 requests the CPU path; llmi is GPU-only");
+        return nullptr;
+    }
     const int nd = llmi_device_count();
     if (nd <= 0) { set_err("no HIP device visible"); return nullptr; }
     if (params.main_gpu < 0 || params.main_gpu >= nd) { set_err("main_gpu out of range"); return nullptr; }
@@ -852,7 +890,7 @@ struct llama_model* llmi_model_load_replicated(const char* path, struct llama_mo
     std::string err;
     // the layout first (no upload), then the replicas and the communicator, then the
     // upload with the pieces going out behind it
-    if (!model_load(path, params.main_gpu, false, true, m->m, err)) {
+    if (!model_load(path, params.main_gpu, false, true, m->m, err, nullptr, params.numerics)) {
         set_err(err);
         delete m;
         return nullptr;
@@ -927,12 +965,16 @@ struct llama_model* llmi_model_load_fanout(const char* path, struct llama_model_
         set_err("llmi_model_load_fanout: bad arguments");
         return nullptr;
     }
+    if (params.n_gpu_layers == 0) {
+        set_err("llmi_model_load_fanout: n_gpu_layers=0 requests the CPU path; llmi is GPU-only");
+        return nullptr;
+    }
     const int nd = llmi_device_count();
     if (nd <= 0) { set_err("no HIP device visible"); return nullptr; }
     if (params.main_gpu < 0 || params.main_gpu >= nd) { set_err("main_gpu out of range"); return nullptr; }
     auto* m = new llama_model();
     std::string err;
-    if (!model_load(path, params.main_gpu, false, true, m->m, err)) {
+    if (!model_load(path, params.main_gpu, false, true, m->m, err, nullptr, params.numerics)) {
         set_err(err);
         delete m;
         return nullptr;
@@ -1111,6 +1153,7 @@ static Seg seg_at(int32_t type, const void* w, int64_t rows, int64_t cols) {
     s.rows = (int)rows;
     s.row0 = 0;
     s.rgs = dm.rgs;
+    s.x86 = t_hook_numerics == NUMERICS_X86;
     return s;
 }
 
@@ -1129,7 +1172,8 @@ int32_t llmi_repack(int32_t type, const void* raw, void* w, int64_t rows, int64_
     hipError_t e;
     if (needs_repack(type)) {
         e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_h, (uint8_t*)w + dm.off_s,
-                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), cols, dm.rgs, nullptr);
+                          (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), cols, dm.rgs,
+                          t_hook_numerics == NUMERICS_X86, nullptr);
     } else {
         e = hipMemcpy(w, raw, dm.bytes, hipMemcpyDeviceToDevice);
     }
@@ -1150,6 +1194,7 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
     a.cols = (int)cols;
     a.npairs = (int)((rows + 1) / 2);
     a.x = x; a.nw = nw; a.eps = eps; a.y = y;
+    a.num = t_hook_numerics;
     int dev = 0;
     (void)hipGetDevice(&dev);
     hipDeviceProp_t prop;
@@ -1163,6 +1208,8 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
 int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, const float* x, const float* nw, float eps,
                      int32_t n_tok, float* y, double* usec) {
     if (!pf_gemm_ok(type, (int)rows, (int)cols) || n_tok <= 0) { set_err("llmi_pf_gemm: unsupported type/shape"); return -1; }
+    const int x86 = t_hook_numerics == NUMERICS_X86;
+    if (x86 && type == T_Q8_0) { set_err("llmi_pf_gemm: x86 numerics take K-quants only"); return -1; }
     const int tpad = (n_tok + 63) / 64 * 64;
     void* aq = nullptr;
     int16_t* abs = nullptr;
@@ -1176,7 +1223,7 @@ int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, co
     if (e == hipSuccess) e = hipMemset(aq, 0, (size_t)tpad * cols * 2);
     if (e == hipSuccess) e = hipMemset(abs, 0, (size_t)tpad * (cols / 16) * 2);
     if (e == hipSuccess) e = hipMemset(ad, 0, (size_t)tpad * (cols / 32) * 4);
-    if (e == hipSuccess) e = launch_pf_quant(x, (int)cols, nw, eps, (int)cols, act_kind(type), n_tok, aq, abs, ad, abf, nullptr);
+    if (e == hipSuccess) e = launch_pf_quant(x, (int)cols, nw, eps, (int)cols, act_kind(type), n_tok, aq, abs, ad, abf, nullptr, x86);
     PfGemm g;
     g.w = seg_at(type, w, rows, cols); g.rows = (int)rows; g.cols = (int)cols; g.T = n_tok;
     g.aq = aq; g.abs = abs; g.ad = ad; g.abf = abf; g.y = y; g.ldy = (int)rows;
@@ -1202,6 +1249,7 @@ int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x, const floa
     if (cols % 256) { set_err("cols must be a multiple of 256"); return -1; }
     MVArgs a;
     a.cols = (int)cols; a.x = x; a.nw = nw; a.eps = eps;
+    a.num = t_hook_numerics;
     hipError_t e = launch_quant_dump(a, act_kind(type), out, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
@@ -1348,6 +1396,7 @@ int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int3
     a.tmax = scores + (size_t)n_head * n_ctx;
     a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
     a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);
+    a.num = t_hook_numerics;
     set_attn_mode(mode);
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
     hipError_t e = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, nullptr);

@@ -122,9 +122,11 @@ size_t fanout_plan(size_t arena_bytes, size_t chunk, const std::vector<size_t>& 
 }
 
 bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& M, std::string& err,
-                const UploadHook* hook) {
+                const UploadHook* hook, int numerics) {
     M.path = path;
     M.device = device;
+    if (numerics != NUMERICS_GENERIC && numerics != NUMERICS_X86) { err = "unknown numerics " + std::to_string(numerics); return false; }
+    M.numerics = numerics;
     M.file = std::make_shared<GgufFile>();
     GgufFile& f = *M.file;
     if (!f.open(path, err)) return false;
@@ -323,7 +325,8 @@ bool model_upload(Model& M, std::string& err, const UploadHook* hook) {
                 e = hipMemcpyAsync(dstage[slot], pin[slot], n, hipMemcpyHostToDevice, us);
                 if (e == hipSuccess)
                     e = launch_repack(m.type, dstage[slot], M.arena + m.off_a + b0 * pa, M.arena + m.off_h + b0 * ph,
-                                      M.arena + m.off_s + b0 * ps, M.arena + m.off_d + b0 * pd, nr * bpr, m.cols, m.rgs, us);
+                                      M.arena + m.off_s + b0 * ps, M.arena + m.off_d + b0 * pd, nr * bpr, m.cols, m.rgs,
+                                      M.numerics == NUMERICS_X86, us);
                 if (e == hipSuccess) e = hipEventRecord(ev[slot], us);
                 used[slot] = true;
                 slot ^= 1;
@@ -357,6 +360,7 @@ bool model_upload(Model& M, std::string& err, const UploadHook* hook) {
 
 bool model_clone_layout(const Model& src, int device, Model& dst, std::string& err) {
     dst.device = device;
+    dst.numerics = src.numerics;
     dst.path = src.path;
     dst.desc = src.desc;
     dst.file = src.file;
@@ -540,6 +544,7 @@ Seg seg_of(const Model& m, const DevMat& d, int row0) {
     s.rows = (int)d.rows;
     s.row0 = row0;
     s.rgs = d.rgs;
+    s.x86 = m.numerics == NUMERICS_X86;
     return s;
 }
 
@@ -593,7 +598,8 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m.layers[(size_t)l];
         // --- QKV + RoPE + KV write (grouped by activation kind) ---
-        MVArgs a; a.xfirst = exp_xfirst >> 0 & 1;
+        const int num = m.numerics;
+        MVArgs a; a.xfirst = exp_xfirst >> 0 & 1; a.num = num;
         a.cols = E; a.x = c.x; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps; a.y = c.q;
         a.kc = c.kc + l * kv_layer; a.vc = c.vc + l * kv_layer; a.rope = c.rope; a.st = c.st;
         a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = nq; a.nk = nk;
@@ -624,27 +630,29 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         at.layer = l;
         at.gran = (unsigned long long*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx));
         at.fault = c.fault_dev;
+        at.num = num;
         LLMI_RUN(K_ATTN, launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---
-        MVArgs o; o.xfirst = exp_xfirst >> 1 & 1;
+        MVArgs o; o.xfirst = exp_xfirst >> 1 & 1; o.num = num;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
         LLMI_RUN(K_ATTN_OUT, launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
         if (P) P->add(K_ATTN_OUT, (double)L.wo.bytes + 4.0 * nq + 8.0 * E);
         // --- gate/up + SwiGLU ---
-        MVArgs gu; gu.xfirst = exp_xfirst >> 2 & 1;
+        MVArgs gu; gu.xfirst = exp_xfirst >> 2 & 1; gu.num = num;
         gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2;
         gu.cols = E; gu.x = c.x; gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps;
         gu.y = c.h; gu.npairs = hp.n_ff;
         LLMI_RUN(K_FFN_GATE_UP, launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
         if (P) P->add(K_FFN_GATE_UP, (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff);
         // --- down + residual ---
-        MVArgs dn; dn.xfirst = exp_xfirst >> 3 & 1;
+        MVArgs dn; dn.xfirst = exp_xfirst >> 3 & 1; dn.num = num;
         dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
         LLMI_RUN(K_FFN_DOWN, launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
         if (P) P->add(K_FFN_DOWN, (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E);
     }
     MVArgs lo;
+    lo.num = m.numerics;
     lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
     lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
     lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = &c.st->key[0][0]; lo.st = c.st;
@@ -715,8 +723,6 @@ static bool balloc(Context& c, std::string& err) {
     HIPC(hipStreamSynchronize(c.stream));
     return true;
 }
-
-static int bpad(int nt) { return nt <= 1 ? 1 : nt == 2 ? 2 : nt <= 4 ? 4 : 8; }
 
 static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std::string& err) {
     const Model& m = *c.m;
@@ -800,6 +806,7 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
 bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err) {
     const HParams& hp = c.m->hp;
     if (nt < 1 || nt > kMaxBatch || c.n_seq < 2) { err = "batched step: 1..8 slots of a context with n_seq_max >= 2"; return false; }
+    if (c.m->numerics != NUMERICS_GENERIC) { err = "batched step: generic numerics only (x86 numerics decode one sequence per step)"; return false; }
     for (const Layer& L : c.m->layers)
         if (L.wg.type != L.wu.type) { err = "batched step: ffn_gate / ffn_up of different types"; return false; }
     if (!balloc(c, err)) return false;
@@ -851,10 +858,13 @@ bool prefill_supported(const Model& m) {
     const HParams& hp = m.hp;
     if (hp.head_dim != 128 && hp.head_dim != 64) return false;
     if (hp.n_rot % 2 || hp.n_rot > hp.head_dim) return false;
+    const bool x86 = m.numerics == NUMERICS_X86;
     for (const Layer& L : m.layers) {
         const DevMat* ms[] = {&L.wq, &L.wk, &L.wv, &L.wo, &L.wg, &L.wu, &L.wd};
-        for (const DevMat* d : ms)
+        for (const DevMat* d : ms) {
             if (!pf_gemm_ok(d->type, (int)d->rows, (int)d->cols)) return false;
+            if (x86 && d->type == T_Q8_0) return false;  // x86 Q8_0 prompts: decode steps
+        }
         if (act_kind(L.wg.type) != act_kind(L.wu.type)) return false;
     }
     return true;
@@ -889,17 +899,22 @@ static bool prefill_alloc(Context& c, std::string& err) {
     // the tiled attention's score rows (<= kPfFaScratchCap, launches chunked to fit); a
     // failed allocation leaves the LDS kernels in charge
     const size_t wsc = pf_fa_scratch_bytes(hp.n_head, hp.n_head_kv, hp.head_dim, cap, c.n_ctx);
-    if (wsc && hipMalloc(&c.pf_wsc, wsc) == hipSuccess) c.pf_wsc_bytes = wsc;
+    if (wsc && !g_pf_fa_noalloc && hipMalloc(&c.pf_wsc, wsc) == hipSuccess) c.pf_wsc_bytes = wsc;
     else { c.pf_wsc = nullptr; (void)hipGetLastError(); }
     c.pf_cap = cap;
     return true;
 }
 
-int prefill_max_kv(const Context& c) {
+int prefill_max_kv(Context& c) {
     const HParams& hp = c.m->hp;
     const int lim = pf_max_kv();
-    if (lim == kPfAttnMaxKV && g_pf_attn_fa && !g_pf_attn_simple &&
-        pf_fa_scratch_bytes(hp.n_head, hp.n_head_kv, hp.head_dim, 512, c.n_ctx) > 0)
+    if (c.m->numerics == NUMERICS_X86)  // k_pf_a86 keeps the G heads' scores in LDS
+        return std::min(lim, pf_attn_x86_max_kv(hp.n_head, hp.n_head_kv, hp.head_dim));
+    // the whole context only where the tiled kernel can run: its score scratch must exist
+    // (allocated here, before the limit is chosen; a failed allocation leaves the LDS
+    // kernels' limit)
+    std::string err;
+    if (lim == kPfAttnMaxKV && g_pf_attn_fa && !g_pf_attn_simple && prefill_alloc(c, err) && c.pf_wsc)
         return c.n_ctx;
     return lim;
 }
@@ -912,6 +927,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
     if (!prefill_alloc(c, err)) return false;
     const int E = hp.n_embd, D = hp.head_dim, nq = hp.n_head * D, nk = hp.n_head_kv * D, F = hp.n_ff;
     const size_t kv_layer = (size_t)hp.n_head_kv * c.n_ctx * D;
+    const int x86 = m.numerics == NUMERICS_X86;
 #define PFC(expr)                                                              \
     do {                                                                       \
         hipError_t e_ = (expr);                                                \
@@ -936,7 +952,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
                 if (act_kind(W.type) != quant_kind) {
                     quant_kind = act_kind(W.type);
                     PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.attn_norm.off_a), hp.eps, E, quant_kind, T,
-                                        c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
+                                        c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream, x86));
                 }
                 int end = part + 1;
                 while (g_pf_qkv_merge && end < 3 && qkv[end]->type == W.type && qkv[end - 1]->rows % 64 == 0) ++end;
@@ -962,14 +978,15 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
             at.n_ctx = c.n_ctx; at.pos0 = p0; at.gqa = hp.n_head / hp.n_head_kv; at.max_kv = p0 + T;
             at.scale = 1.0f / sqrtf((float)D);
             at.wsc = c.pf_wsc; at.wsc_bytes = c.pf_wsc_bytes;
+            at.num = x86;
             PFC(launch_pf_attn(at, hp.n_head, D, T, c.stream));
             // attn_output + residual
-            PFC(launch_pf_quant(c.pf_att, nq, nullptr, 0.f, nq, act_kind(L.wo.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
+            PFC(launch_pf_quant(c.pf_att, nq, nullptr, 0.f, nq, act_kind(L.wo.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream, x86));
             g.w = seg_of(m, L.wo, 0); g.rows = (int)L.wo.rows; g.cols = nq; g.y = c.pf_x; g.ldy = E;
             PFC(launch_pf_gemm(g, EPI_ADD, c.stream));
             // gate/up + SwiGLU
             PFC(launch_pf_quant(c.pf_x, E, (const float*)(m.arena + L.ffn_norm.off_a), hp.eps, E, act_kind(L.wg.type), T,
-                                c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
+                                c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream, x86));
             g.w = seg_of(m, L.wg, 0); g.w2 = seg_of(m, L.wu, 0); g.rows = (int)L.wg.rows; g.cols = E; g.y = c.pf_h; g.ldy = F;
             {  // gate into h, then h = silu(h) * up (two launches: a fused gate+up launch
                // spills past 256 VGPRs and measured slower: Mistral 2048 TTFT 229 vs 225
@@ -983,7 +1000,7 @@ bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::st
                 PFC(launch_pf_gemm(g, EPI_SWIGLU_UP, c.stream));
             }
             // down + residual
-            PFC(launch_pf_quant(c.pf_h, F, nullptr, 0.f, F, act_kind(L.wd.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream));
+            PFC(launch_pf_quant(c.pf_h, F, nullptr, 0.f, F, act_kind(L.wd.type), T, c.pf_aq, c.pf_abs, c.pf_ad, c.pf_abf, c.stream, x86));
             g.w = seg_of(m, L.wd, 0); g.rows = (int)L.wd.rows; g.cols = F; g.y = c.pf_x; g.ldy = E;
             PFC(launch_pf_gemm(g, EPI_ADD, c.stream));
         }

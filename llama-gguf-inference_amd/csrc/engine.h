@@ -27,8 +27,16 @@ struct Layer {
     DevMat attn_norm, wq, wk, wv, wo, ffn_norm, wg, wu, wd;
 };
 
+// Model numerics: the fp32 association every kernel reproduces.
+//   0 ggml's generic scalar order (the oracle's default)
+//   1 upstream's x86 AVX2 association (the oracle's or_set_x86_mode(X86_ALL)): the weight
+//     planes in the x86 byte order (common.h), fma chains per 4-byte lane, the x86
+//     attention (attn86.hip), ggml_v_expf softmax / SiLU, round-half-even q8_0
+enum : int { NUMERICS_GENERIC = 0, NUMERICS_X86 = 1 };
+
 struct Model {
     int device = 0;
+    int numerics = NUMERICS_GENERIC;      // fixed at load: the weight planes' byte order depends on it
     std::string path, desc;
     std::shared_ptr<GgufFile> file;
     HParams hp;
@@ -134,7 +142,7 @@ struct Context {
 // upload order, so the prefix grows monotonically); false aborts the load.
 using UploadHook = std::function<bool(size_t prefix_end, hipStream_t us)>;
 bool model_load(const std::string& path, int device, bool vocab_only, bool no_upload, Model& m, std::string& err,
-                const UploadHook* hook = nullptr);
+                const UploadHook* hook = nullptr, int numerics = NUMERICS_GENERIC);
 // the upload half of model_load (after a load with no_upload)
 bool model_upload(Model& m, std::string& err, const UploadHook* hook = nullptr);
 // a matrix of the arena as a matvec segment (rows start at row0 of the launch)
@@ -162,7 +170,7 @@ double bytes_per_token(const Model& m, int n_kv);
 bool prefill_supported(const Model& m);
 // positions the batched prefill's attention reaches: the context when the tiled kernel
 // (k_pf_fa) takes the model's heads, else the LDS kernels' pf_max_kv()
-int prefill_max_kv(const Context& c);
+int prefill_max_kv(Context& c);
 // run tokens [0, n) at positions pos0.. through every layer as batched launches (KV
 // cache written, no logits); enqueued on c.stream, no synchronisation
 bool prefill_enqueue(Context& c, const int32_t* tokens, int n, int pos0, std::string& err);

@@ -22,7 +22,7 @@ constexpr int kDimAttnMaxKV = 1024;  // dim-split one-launch attention (k_attn_d
 constexpr int kRegAttnMaxKV = 512;  // register-prefetched one-launch attention (k_attn_r) up to this KV bound  // one-launch exchange attention (k_attn_x) up to this KV bound
 constexpr int kPfAttnMaxKV = 32768;  // batched-prefill attention: scores of one head in LDS
 // test options (llmi_test_option in capi.cpp): bit-identical path selection and lowered limits
-extern int g_pf_gemm_ng, g_pf_qkv_merge, g_pf_xcd_map, g_pf_quant_bpc, g_pf_quant_split_below, g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
+extern int g_pf_fa_noalloc, g_pf_gemm_ng, g_pf_qkv_merge, g_pf_xcd_map, g_pf_quant_bpc, g_pf_quant_split_below, g_pf_attn_simple, g_pf_attn_fa, g_pf_fa_cfg, g_pf_max_kv, g_xspin_limit, g_xtag_skew;
 int pf_max_kv();  // llama_decode hands prompt runs reaching past this KV length to decode steps
 // scratch floats an attention context needs: scores [H][n_ctx] + tile maxima [H][n_ctx/32]
 // + k_attn_x's 8-byte {tag, score} granules [H][kXAttnMaxKV] + a fault word
@@ -50,6 +50,7 @@ struct Seg {
     int rows = 0;
     int row0 = 0;                // first row of this segment in the launch's output space
     int rgs = 0;                 // log2 of the row group of the A / H planes (common.h)
+    int x86 = 0;                 // 1: the x86-numerics byte order of the A / H planes (common.h)
 };
 
 struct MVArgs {
@@ -88,6 +89,7 @@ struct MVArgs {
     const int* tpos = nullptr;
     const int* tseq = nullptr;
     size_t kv_stride = 0;
+    int num = 0;                 // numerics: 0 ggml's generic order, 1 upstream's x86 association (mv_device.h)
 };
 
 struct AttnArgs {
@@ -106,6 +108,7 @@ struct AttnArgs {
     int spin_limit = 1 << 22;             // k_attn_x: polls before a wait gives up (set at launch)
     int tag_skew = 0;                     // test option: consumers expect tag + skew
     unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [kernel][block][wave][4] stamps
+    int num = 0;                          // numerics (MVArgs::num): 1 = the x86 attention kernels (attn86.hip)
 };
 
 // Batched decode (batch.hip): up to kMaxBatch sequences advance one token per step.
@@ -177,6 +180,7 @@ struct PfAttn {
     float scale = 0.f;
     float* wsc = nullptr;      // k_pf_fa score scratch (pf_fa_scratch_bytes), null: LDS kernels only
     size_t wsc_bytes = 0;
+    int num = 0;               // numerics (MVArgs::num): 1 = k_pf_a86 (attn86.hip)
 };
 // score scratch k_pf_fa wants for ubatches of T tokens over n_ctx positions (0: the
 // head shape has no tiled kernel); launches are chunked to fit a smaller scratch
@@ -186,7 +190,7 @@ bool pf_gemm_ok(int type, int rows, int cols);
 hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* toks, float* X, int T, int32_t* hist,
                            int pos0, int n_ctx, hipStream_t s);
 hipError_t launch_pf_quant(const float* x, int ldx, const float* nw, float eps, int cols, int act, int T, void* aq,
-                           int16_t* abs, float* ad, void* abf, hipStream_t s);
+                           int16_t* abs, float* ad, void* abf, hipStream_t s, int x86 = 0);
 hipError_t launch_pf_gemm(const PfGemm& g, int epi, hipStream_t s);
 hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipStream_t s);
 
@@ -197,9 +201,9 @@ __host__ __device__ inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
 bool mv_geometry(MVArgs& a, int epi);
 size_t mv_lds_bytes(int act, int cols);
 // per-type matvec launchers (mv_kernels.h; instantiated in mv_q4k/q5k/q6k/q80.hip)
-template <int ACT, bool NORM, int T>
+template <int ACT, bool NORM, int T, int X86>
 hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s);
-template <bool NORM, int T, int T2>
+template <bool NORM, int T, int T2, int X86>
 hipError_t mv_qkv2_launch(const MVArgs& a, int split_tasks, dim3 grid, size_t lds, hipStream_t s);
 
 // All launches are asynchronous on `stream` and graph-capturable (no allocation, no sync).
@@ -217,7 +221,12 @@ hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
 // the last step's embedding row again (debug tap 0)
 hipError_t launch_embed_row(const EmbArgs& a, const StepState* st, float* out, hipStream_t stream);
 hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* s, uint8_t* d, int64_t nblk, int64_t cols, int rgs,
-                         hipStream_t stream);
+                         int x86, hipStream_t stream);
+// x86 numerics attention (attn86.hip): upstream's non-flash CPU attention in its x86 AVX2
+// association (f16 dots in 4 x 8 fp32 fma lanes, ggml_v_expf softmax with per-8 sums)
+hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s);
+hipError_t launch_pf_attn_x86(const PfAttn& a, int n_head, int n_head_kv, int head_dim, int T, hipStream_t s);
+int pf_attn_x86_max_kv(int n_head, int n_head_kv, int head_dim);
 // writes the prologue's quantized activation in ggml block form (test hook)
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);
 hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int blocks, hipStream_t stream);

@@ -56,19 +56,20 @@ size_t mv_lds_bytes(int act, int cols) { return fold_off(act, cols, kMVWaves) + 
 
 
 // The prologue's quantized activation written out in ggml block form (test hook).
-template <int ACT>
+template <int ACT, int X86>
 __global__ __launch_bounds__(kMVThreads) void k_quant_dump(MVArgs A, uint8_t* out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Lds L = carve(smem, ACT, A.cols);
-    if (A.nw) mv_prologue<ACT, true>(A, L);
-    else mv_prologue<ACT, false>(A, L);
+    if (A.nw) mv_prologue<ACT, true, X86>(A, L);
+    else mv_prologue<ACT, false, X86>(A, L);
     __syncthreads();
     const int cols = A.cols;
     for (int e = threadIdx.x; e < cols; e += blockDim.x) {
         const uint8_t* rec = L.act + (size_t)(e >> 8) * kRec;
         const int t = e & 255;
         if (ACT == 0) {  // residue order: element 64c + 32h + l + 8i at part 2c + l/4, half h, byte 4 (l % 4) + i
-            const int c = t >> 6, h = (t >> 5) & 1, l = t & 7, i = (t & 31) >> 3;
+                         // (x86: element 64c + 32h + 4l + i)
+            const int c = t >> 6, h = (t >> 5) & 1, l = X86 ? (t & 31) >> 2 : t & 7, i = X86 ? t & 3 : (t & 31) >> 3;
             out[(size_t)(e >> 8) * 292 + 4 + t] = rec[32 * (2 * c + (l >> 2)) + 16 * h + 4 * (l & 3) + i];
         } else {
             out[(size_t)(e >> 5) * 34 + 2 + (e & 31)] = rec[t];
@@ -853,8 +854,10 @@ __global__ void k_state_set(StepState* st, int token_in, int pos_next) {
 // Load-time repack of GGUF blocks into the unit-major layout (common.h).
 // One thread per (block, chunk c in 0..3); nbr = blocks (units) per row.
 // ----------------------------------------------------------------------------------
+// x86 = 1: the x86-numerics byte order (common.h): part 2c + k = native bytes, i.e. byte
+// 4m + i of part 2c + k holds chunk elements t = 16k + 4m + i (low nibble) and 32 + t
 __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H, uint8_t* S, uint8_t* Dp, int64_t nblk,
-                            int nbr, int rgs) {
+                            int nbr, int rgs, int x86) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t b = gid >> 2;
     const int c = (int)(gid & 3);
@@ -868,19 +871,21 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
         const int bb = type == T_Q4_K ? 144 : 176;
         const uint8_t* x = raw + b * bb;
         const uint8_t* qs = x + (type == T_Q4_K ? 16 : 48);
+        // chunk element of (l = 4k + m, byte i): residue order l + 8i, x86 order 4l + i
+        auto el = [&](int l, int i) { return x86 ? 4 * l + i : l + 8 * i; };
         for (int k = 0; k < 2; ++k)
             for (int m = 0; m < 4; ++m)
-                for (int i = 0; i < 4; ++i) apiece(2 * c + k)[4 * m + i] = qs[32 * c + 4 * k + m + 8 * i];
+                for (int i = 0; i < 4; ++i) apiece(2 * c + k)[4 * m + i] = qs[32 * c + el(4 * k + m, i)];
         if (c == 0)
             for (int i = 0; i < 16; ++i) S[b * 16 + i] = x[i];
-        if (type == T_Q5_K) {  // byte i, bit l of the lo word: qh[l + 8i] bit 2c; hi word: bit 2c+1
+        if (type == T_Q5_K) {  // byte i, bit l of the lo word: qh[el(l, i)] bit 2c; hi word: bit 2c+1
             const uint8_t* qh = x + 16;
             uint8_t* h = H + piece_off((uint32_t)row, (uint32_t)(c >> 1), (uint32_t)u, (uint32_t)U, 2, rgs) + 8 * (c & 1);
             for (int i = 0; i < 4; ++i) {
                 uint8_t lo = 0, hi = 0;
                 for (int l = 0; l < 8; ++l) {
-                    lo |= (uint8_t)(((qh[l + 8 * i] >> (2 * c)) & 1) << l);
-                    hi |= (uint8_t)(((qh[l + 8 * i] >> (2 * c + 1)) & 1) << l);
+                    lo |= (uint8_t)(((qh[el(l, i)] >> (2 * c)) & 1) << l);
+                    hi |= (uint8_t)(((qh[el(l, i)] >> (2 * c + 1)) & 1) << l);
                 }
                 h[i] = lo;
                 h[4 + i] = hi;
@@ -897,21 +902,22 @@ __global__ void k_repack_kq(int type, const uint8_t* raw, uint8_t* A, uint8_t* H
             const int hi = (qh[32 * n + l] >> (2 * quad)) & 3;
             return lo | (hi << 4);
         };
+        auto el = [&](int l, int i) { return x86 ? 4 * l + i : l + 8 * i; };
         for (int k = 0; k < 2; ++k)
             for (int m = 0; m < 4; ++m)
                 for (int i = 0; i < 4; ++i) {
-                    const int t = 4 * k + m + 8 * i;
+                    const int t = el(4 * k + m, i);
                     apiece(2 * c + k)[4 * m + i] =
                         (uint8_t)((u6(64 * c + t) & 15) | ((u6(64 * c + 32 + t) & 15) << 4));
                 }
         // H part c, dword g = 2*hi + k: byte i bits [2m, 2m+1] = (high 2 bits of chunk
-        // element 32*hi + 4k + m + 8i) XOR 2, which v_perm turns into the high part of q - 32
+        // element 32*hi + el(4k + m, i)) XOR 2, which v_perm turns into the high part of q - 32
         uint8_t* h = H + piece_off((uint32_t)row, (uint32_t)c, (uint32_t)u, (uint32_t)U, 4, rgs);
         for (int g = 0; g < 4; ++g)
             for (int i = 0; i < 4; ++i) {
                 uint8_t v = 0;
                 for (int m = 0; m < 4; ++m)
-                    v |= (uint8_t)(((u6(64 * c + 32 * (g >> 1) + 4 * (g & 1) + m + 8 * i) >> 4) ^ 2) << (2 * m));
+                    v |= (uint8_t)(((u6(64 * c + 32 * (g >> 1) + el(4 * (g & 1) + m, i)) >> 4) ^ 2) << (2 * m));
                 h[4 * g + i] = v;
             }
         for (int i = 0; i < 4; ++i) S[b * 16 + 4 * c + i] = x[192 + 4 * c + i];
@@ -953,7 +959,7 @@ hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int bl
 // ----------------------------------------------------------------------------------
 // QKV whose segments form two contiguous type groups split at a task boundary: both groups
 // pipelined (k_matvec's T2 path).  Returns hipErrorNotSupported when not applicable.
-template <bool NORM>
+template <bool NORM, int X86>
 static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     if (a.nseg < 2 || grid.x < 2) return hipErrorNotSupported;
     int t1 = a.seg[0].type, t2 = -1, split_row = -1;
@@ -966,7 +972,7 @@ static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipSt
     if (t2 < 0 || split_row % a.rpt || a.cols > 16 * kMVThreads) return hipErrorNotSupported;
     const int sp = split_row / a.rpt;
 #define LLMI_QKV2(A_, B_)                                                                            \
-    if (t1 == A_ && t2 == B_) return mv_qkv2_launch<NORM, A_, B_>(a, sp, grid, lds, s);
+    if (t1 == A_ && t2 == B_) return mv_qkv2_launch<NORM, A_, B_, X86>(a, sp, grid, lds, s);
     if constexpr (NORM) {
         LLMI_QKV2(T_Q4_K, T_Q6_K) LLMI_QKV2(T_Q4_K, T_Q5_K) LLMI_QKV2(T_Q5_K, T_Q6_K)
     }
@@ -974,11 +980,11 @@ static hipError_t mv_dispatch_qkv2(const MVArgs& a, dim3 grid, size_t lds, hipSt
     return hipErrorNotSupported;
 }
 
-template <bool NORM>
+template <bool NORM, int X86>
 static hipError_t mv_dispatch_type(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
     static const bool qkv2 = !getenv("LLMI_NO_QKV2");  // A/B switch for measurements
     if (epi == EPI_QKV && qkv2) {
-        const hipError_t e = mv_dispatch_qkv2<NORM>(a, grid, lds, s);
+        const hipError_t e = mv_dispatch_qkv2<NORM, X86>(a, grid, lds, s);
         if (e != hipErrorNotSupported) return e;
     }
     // primary (pipelined) type = the type owning the most rows of the launch
@@ -990,10 +996,10 @@ static hipError_t mv_dispatch_type(const MVArgs& a, int epi, dim3 grid, size_t l
         if (rows > best_rows) { best_rows = rows; best = a.seg[i].type; }
     }
     switch (best) {
-        case T_Q4_K: return mv_dispatch_epi<0, NORM, T_Q4_K>(a, epi, grid, lds, s);
-        case T_Q5_K: return mv_dispatch_epi<0, NORM, T_Q5_K>(a, epi, grid, lds, s);
-        case T_Q6_K: return mv_dispatch_epi<0, NORM, T_Q6_K>(a, epi, grid, lds, s);
-        case T_Q8_0: return mv_dispatch_epi<1, NORM, T_Q8_0>(a, epi, grid, lds, s);
+        case T_Q4_K: return mv_dispatch_epi<0, NORM, T_Q4_K, X86>(a, epi, grid, lds, s);
+        case T_Q5_K: return mv_dispatch_epi<0, NORM, T_Q5_K, X86>(a, epi, grid, lds, s);
+        case T_Q6_K: return mv_dispatch_epi<0, NORM, T_Q6_K, X86>(a, epi, grid, lds, s);
+        case T_Q8_0: return mv_dispatch_epi<1, NORM, T_Q8_0, X86>(a, epi, grid, lds, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1052,14 +1058,23 @@ hipError_t launch_matvec(const MVArgs& a0, int epi, int max_blocks, hipStream_t 
     if (exp_blocks > 0 && exp_blocks < blocks) blocks = exp_blocks;
 #endif
     const dim3 grid(blocks);
-    return a.nw ? mv_dispatch_type<true>(a, epi, grid, lds, s) : mv_dispatch_type<false>(a, epi, grid, lds, s);
+    // the weights' byte order must be the numerics' (common.h: x86 planes for x86 numerics)
+    for (int i = 0; i < a.nseg; ++i)
+        if ((a.seg[i].x86 != 0) != (a.num != 0)) return hipErrorInvalidValue;
+    if (a.num) return a.nw ? mv_dispatch_type<true, 1>(a, epi, grid, lds, s) : mv_dispatch_type<false, 1>(a, epi, grid, lds, s);
+    return a.nw ? mv_dispatch_type<true, 0>(a, epi, grid, lds, s) : mv_dispatch_type<false, 0>(a, epi, grid, lds, s);
 }
 
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t s) {
     if (a.cols <= 0 || a.cols % 256) return hipErrorInvalidValue;
     const size_t lds = mv_lds_bytes(act, a.cols);
-    if (act == 0) hipLaunchKernelGGL((k_quant_dump<0>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
-    else hipLaunchKernelGGL((k_quant_dump<1>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+    if (a.num) {
+        if (act == 0) hipLaunchKernelGGL((k_quant_dump<0, 1>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+        else hipLaunchKernelGGL((k_quant_dump<1, 1>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+    } else {
+        if (act == 0) hipLaunchKernelGGL((k_quant_dump<0, 0>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+        else hipLaunchKernelGGL((k_quant_dump<1, 0>), dim3(1), dim3(kMVThreads), lds, s, a, (uint8_t*)out);
+    }
     return hipGetLastError();
 }
 
@@ -1122,6 +1137,7 @@ static hipError_t attn_x_g(const AttnArgs& a, int g, int hk, int kv_bound, hipSt
 // Test options (llmi_test_option; never read from the environment): paths that give
 // bit-identical results, or limits lowered so a test reaches a fallback / fault path.
 int g_pf_attn_simple = 0;               // batched-prefill attention: one head per workgroup
+int g_pf_fa_noalloc = 0;               // prefill: never allocate k_pf_fa's score scratch (its failure path)
 #ifndef LLMI_PF_QUANT_BPC
 #define LLMI_PF_QUANT_BPC 2
 #endif
@@ -1202,6 +1218,7 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
 
 hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    if (a0.num) return launch_attention_x86(a0, n_head, n_head_kv, head_dim, kv_bound, s);
     AttnArgs a = a0;
     a.spin_limit = g_xspin_limit;
     a.tag_skew = g_xtag_skew;
@@ -1281,13 +1298,13 @@ hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream
 }
 
 hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint8_t* sp, uint8_t* d, int64_t nblk,
-                         int64_t cols, int rgs, hipStream_t s) {
+                         int64_t cols, int rgs, int x86, hipStream_t s) {
     if (nblk <= 0) return hipSuccess;
     if (cols % 256) return hipErrorInvalidValue;
     if (type == T_Q4_K || type == T_Q5_K || type == T_Q6_K) {
         const int64_t thr = nblk * 4;
         hipLaunchKernelGGL(k_repack_kq, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, type, (const uint8_t*)raw, a,
-                           h, sp, d, nblk, (int)(cols / 256), rgs);
+                           h, sp, d, nblk, (int)(cols / 256), rgs, x86);
     } else if (type == T_Q8_0) {
         hipLaunchKernelGGL(k_repack_q80, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, (const uint8_t*)raw, a, d,
                            nblk, (int)(cols / 32), rgs);

@@ -11,14 +11,18 @@ namespace llmi {
 // (hipExtLaunchKernelGGL), i.e. kernel execution time without dependent-launch gaps.
 hipEvent_t launch_event(bool stop);
 
-// CUs of the current device (read once per translation unit)
+// CUs of the current device, cached per device (in-process replicas run one scheduler
+// thread per GPU; a benign race writes the same value twice)
 static inline int cu_count() {
-    static const int n = [] {
-        int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 0;
-        return c;
-    }();
+    static int cache[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    int n = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+    if (n == 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 0) n = 0;
+        __atomic_store_n(&cache[dev], n, __ATOMIC_RELAXED);
+    }
     return n;
 }
 

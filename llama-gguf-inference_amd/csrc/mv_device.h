@@ -184,7 +184,11 @@ __device__ double block_sum_d(double v, double* red) {
 //   q8_0:     d = amax/127 (stored f16), q = roundf(y * (d ? 1/d : 0))   (quantize_row_q8_0_ref)
 // ----------------------------------------------------------------------------------
 // Quantize one 16-element sub-block (values already normed) into the LDS image.
-template <int ACT>
+//   X86 = 1 (the x86 association mode, "x86 numerics" below): K-quant records hold the
+//   block in NATURAL order (part 2c + k, half h = elements 64c + 32h + 16k .. +15), the
+//   weights' x86 layout (common.h); q8_0 is upstream's AVX2 quantize_row_q8_0:
+//   id = 127/amax, q = round-half-even(y * id) (oracle x86_quantize_row_q8_0).
+template <int ACT, int X86 = 0>
 __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const float (&v)[16]) {
     int q[16];
     if constexpr (ACT == 0) {
@@ -228,10 +232,19 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
         // q[j] and q[j+8] are one 16-bit store
         const int s = sb & 15;
         uint8_t* rec = L.act + (size_t)(sb >> 4) * kRec;
-        uint8_t* base = rec + 64 * (s >> 2) + 16 * ((s >> 1) & 1) + 2 * (s & 1);
+        if constexpr (X86) {  // s = 4c + 2h + k: part 2c + k, half h, bytes 0..15 in order
+            u32x4 pk;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            *(uint16_t*)(base + 32 * (j >> 2) + 4 * (j & 3)) = (uint16_t)((q[j] & 0xff) | ((q[j + 8] & 0xff) << 8));
+            for (int w = 0; w < 4; ++w)
+                pk[w] = (uint32_t)(q[4 * w] & 0xff) | ((uint32_t)(q[4 * w + 1] & 0xff) << 8) |
+                        ((uint32_t)(q[4 * w + 2] & 0xff) << 16) | ((uint32_t)(q[4 * w + 3] & 0xff) << 24);
+            *(u32x4*)(rec + 64 * (s >> 2) + 32 * (s & 1) + 16 * ((s >> 1) & 1)) = pk;
+        } else {
+            uint8_t* base = rec + 64 * (s >> 2) + 16 * ((s >> 1) & 1) + 2 * (s & 1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                *(uint16_t*)(base + 32 * (j >> 2) + 4 * (j & 3)) = (uint16_t)((q[j] & 0xff) | ((q[j + 8] & 0xff) << 8));
+        }
         *(int16_t*)(rec + kRecBs + 2 * s) = (int16_t)bsum;
         if (s == 0) *(float*)(rec + kRecD) = dval;
     } else {
@@ -240,9 +253,15 @@ __device__ __forceinline__ void quant_sub(const Lds& L, int cols, int sb, const 
         for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
         am = fmaxf(am, xor_partner<1>(am));
         const float d = am / 127;
-        const float id = d != 0.f ? 1.0f / d : 0.0f;
+        if constexpr (X86) {
+            const float id = am != 0.f ? 127.f / am : 0.0f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
+            for (int j = 0; j < 16; ++j) q[j] = (int)__builtin_rintf(v[j] * id);
+        } else {
+            const float id = d != 0.f ? 1.0f / d : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) q[j] = (int)roundf(v[j] * id);
+        }
         uint8_t* rec = L.act + (size_t)(sb >> 4) * kRec;
         if ((sb & 1) == 0) *(float*)(rec + kRecBs + 2 * (sb & 15)) = h2f(f2h(d));
         u32x4 pk;
@@ -335,7 +354,7 @@ __device__ __forceinline__ float mv_norm_scale(const MVArgs& A, const Lds& L, co
     }
     return scale;
 }
-template <int ACT, bool NORM, int NP, int NT = kMVThreads>
+template <int ACT, bool NORM, int NP, int NT = kMVThreads, int X86 = 0>
 __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L, const ProRegs<NORM, NP>& R) {
     const int tid = threadIdx.x, cols = A.cols;
     const int nsub = cols / 16;
@@ -350,7 +369,7 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
                 v[j] = R.x[i][j];
                 if constexpr (NORM) v[j] = (v[j] * scale) * R.w[i][j];
             }
-            quant_sub<ACT>(L, cols, sb, v);
+            quant_sub<ACT, X86>(L, cols, sb, v);
         }
     }
     for (int sb = tid + NP * NT; sb < nsub; sb += NT) {
@@ -360,7 +379,7 @@ __device__ __forceinline__ void mv_prologue_finish(const MVArgs& A, const Lds& L
 #pragma unroll
             for (int j = 0; j < 16; ++j) v[j] = (v[j] * scale) * w[j];
         }
-        quant_sub<ACT>(L, cols, sb, v);
+        quant_sub<ACT, X86>(L, cols, sb, v);
     }
 }
 // Pre-quantized activation (MVArgs::xq): the LDS image is copied from global memory.
@@ -384,11 +403,11 @@ __device__ __forceinline__ void mv_img_finish(const MVArgs& A, const Lds& L, con
     for (int i = (int)threadIdx.x + NI * NT; i < n16; i += NT) ((u32x4*)L.act)[i] = *(const u32x4*)(A.xq + 16 * i);
 }
 
-template <int ACT, bool NORM>
+template <int ACT, bool NORM, int X86 = 0>
 __device__ __forceinline__ void mv_prologue(const MVArgs& A, const Lds& L) {
     ProRegs<NORM, 1> R;
     mv_prologue_issue<NORM, 1>(A, R);
-    mv_prologue_finish<ACT, NORM, 1>(A, L, R);
+    mv_prologue_finish<ACT, NORM, 1, kMVThreads, X86>(A, L, R);
 }
 
 // ----------------------------------------------------------------------------------
@@ -656,6 +675,222 @@ __device__ __forceinline__ void unit_terms_q6m(const UnitW<T_Q6_K>& w, const uin
 }
 
 // ----------------------------------------------------------------------------------
+// x86 numerics (model numerics LLMI_NUMERICS_X86): the association upstream's x86 AVX2
+// kernels use [upstream ggml-cpu arch/x86/quants.c ggml_vec_dot_{q4_K,q5_K,q6_K}_q8_K,
+// ggml_vec_dot_q8_0_q8_0; recalled, not vendored], as restated by the oracle's x86 mode
+// (oracle/ggml_oracle.c x86_q4_K .. x86_q8_0).  Per row:
+//   K-quants: per 256-block b, in order
+//       sumi[k] = sum over the block's elements e with (e % 32) / 4 == k of scale(e)*q(e)*a(e)
+//                 (the 8 int32 lanes of maddubs + madd over 32-byte vectors, k = 0..7)
+//       acc[k]  = fma(d_a(b) * d_w(b), (float)sumi[k], acc[k])
+//       Q4_K:  prod[k] = m[2k](bs[4k] + bs[4k+1]) + m[2k+1](bs[4k+2] + bs[4k+3]) (k < 4),
+//              acc_m[k] = fma(-d_a(b) * dmin_w(b), (float)prod[k], acc_m[k])
+//       Q5_K:  summs = fma(-d_a(b) * dmin_w(b), (float)sum_j m[j/2] bs[j], summs)
+//     result  hsum_float_8(acc) [+ (acc_m[0] + acc_m[2]) + (acc_m[1] + acc_m[3])] [+ summs]
+//   Q8_0:     per 32-block b: sumi[k] over bytes 4k..4k+3, acc[k] = fma(d_w*d_a, (float)sumi[k],
+//             acc[k]); result hsum_float_8(acc)
+// with hsum_float_8(a) = ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7)).  The weights'
+// x86 layout (common.h) puts the 4 elements of one lane k of one 32-element vector in one
+// dword, so the integer code is the generic one with l read as the lane; the fold runs
+// the fma chains (d and the lane sums kept apart until the chain's fma).
+// Fold buffer per wave (floats): K-quants S[R][12][Lr] | D[R][2][Lr] (d, -dmin) | G[R][12];
+// Q8_0 S[R][8][8 Lr] | D[R][8 Lr] | G[R][8].
+// ----------------------------------------------------------------------------------
+constexpr int kFoldF = 9 * 64, kFoldFloats = kFoldF + 9 * 16;
+constexpr int kX86KD = 12 * 64, kX86KG = kX86KD + 2 * 64, kX86KFloats = kX86KG + 12 * 16;
+constexpr int kX86QD = 8 * 8 * 64, kX86QG = kX86QD + 8 * 64, kX86QFloats = kX86QG + 8 * 16;
+template <int ACT, int X86>
+__host__ __device__ constexpr int fold_floats() { return X86 ? (ACT ? kX86QFloats : kX86KFloats) : kFoldFloats; }
+template <int ACT>
+__host__ __device__ constexpr int x86_chains() { return ACT ? 8 : 12; }
+
+// upstream hsum_float_8 (AVX: lo128 + hi128, movehl + add, movehdup + add_ss)
+__device__ __forceinline__ float x86_hsum8(const float* a) {
+    const float t0 = a[0] + a[4], t1 = a[1] + a[5], t2 = a[2] + a[6], t3 = a[3] + a[7];
+    return (t0 + t2) + (t1 + t3);
+}
+
+// the unit's x86 terms straight into the fold buffer (lane: row r, unit ul of the sub-item)
+template <int T>
+__device__ __forceinline__ void unit_store_x86(const UnitW<T>& w, const uint8_t* rec, float* F, int r, int ul, int lr,
+                                               bool valid) {
+    if constexpr (T == T_Q8_0) {
+        // per 32-block b: lanes k < 4 are dwords of part 2b, k >= 4 of part 2b + 1
+        float* S = F + (size_t)r * 8 * 8 * lr + 8 * ul;
+        float* D = F + kX86QD + (size_t)r * 8 * lr + 8 * ul;
+        float db[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const i32x4 a0 = *(const i32x4*)(rec + 32 * b), a1 = *(const i32x4*)(rec + 32 * b + 16);
+            const float dw = h2f(w.s[b >> 1] >> (16 * (b & 1))), da = *(const float*)(rec + kRecBs + 4 * b);
+            db[b] = dw * da;
+            float s[8];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                s[m] = (float)dot4(w.q[2 * b][m], a0[m], 0);
+                s[4 + m] = (float)dot4(w.q[2 * b + 1][m], a1[m], 0);
+            }
+            if (valid) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) S[(size_t)k * 8 * lr + b] = s[k];
+            }
+        }
+        if (valid) {
+            *(float4*)D = make_float4(db[0], db[1], db[2], db[3]);
+            *(float4*)(D + 4) = make_float4(db[4], db[5], db[6], db[7]);
+        }
+    } else {
+        int t[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) t[l] = 0;
+        float d, dm = 0.f;
+        float ms[4] = {0.f, 0.f, 0.f, 0.f};
+        const float da = *(const float*)(rec + kRecD);
+        if constexpr (T == T_Q4_K || T == T_Q5_K) {
+            u32x2 sc, mn;
+            scales_mins(w.s.y, w.s.z, w.s.w, sc, mn);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int c = p >> 1, k = p & 1;
+                const uint32_t sw = c < 2 ? sc.x : sc.y;
+                const int slo = (int)((sw >> (16 * (c & 1))) & 0xffu), shi = (int)((sw >> (16 * (c & 1) + 8)) & 0xffu);
+                const i32x4 alo = *(const i32x4*)(rec + 32 * p), ahi = *(const i32x4*)(rec + 32 * p + 16);
+                uint32_t hlo = 0, hhi = 0;
+                if constexpr (T == T_Q5_K) {
+                    hlo = w.h[c >> 1][2 * (c & 1)];
+                    hhi = w.h[c >> 1][2 * (c & 1) + 1];
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int l = 4 * k + m;
+                    uint32_t l4 = w.q[p][m] & M4, h4 = (w.q[p][m] >> 4) & M4;
+                    if constexpr (T == T_Q5_K) {
+                        l4 |= (l <= 4 ? hlo << (4 - l) : hlo >> (l - 4)) & 0x10101010u;
+                        h4 |= (l <= 4 ? hhi << (4 - l) : hhi >> (l - 4)) & 0x10101010u;
+                    }
+                    t[l] = __mul24(slo, dot4(l4, alo[m], 0)) + t[l];
+                    t[l] = __mul24(shi, dot4(h4, ahi[m], 0)) + t[l];
+                }
+            }
+            // bsum pairs (bs[2j], bs[2j+1]) against (m_j, m_j): prod[k] = pairs 2k, 2k+1
+            const i32x4 b0 = *(const i32x4*)(rec + kRecBs), b1 = *(const i32x4*)(rec + kRecBs + 16);
+            int pr[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t sel = 0x0c000c00u | (uint32_t)(j & 3) * 0x00010001u;
+                const uint32_t mm = __builtin_amdgcn_perm(0u, j < 4 ? mn.x : mn.y, sel);
+                const int bp = j < 4 ? b0[j] : b1[j - 4];
+                pr[j >> 1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, bp), __builtin_bit_cast(short2_t, mm), pr[j >> 1], false);
+            }
+            d = da * h2f(w.s.x);
+            dm = -da * h2f(w.s.x >> 16);
+            if constexpr (T == T_Q4_K) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ms[k] = (float)pr[k];
+            } else {
+                ms[0] = (float)(((pr[0] + pr[1]) + pr[2]) + pr[3]);
+            }
+        } else {  // Q6_K: a dword = 4 consecutive elements of one 16-element sub-block, one scale
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int c = p >> 1, k = p & 1;
+                const uint32_t s4 = w.s[c];
+                const int clo = (int)(int8_t)((s4 >> (8 * k)) & 0xff), chi = (int)(int8_t)((s4 >> (8 * (2 + k))) & 0xff);
+                const i32x4 alo = *(const i32x4*)(rec + 32 * p), ahi = *(const i32x4*)(rec + 32 * p + 16);
+                const uint32_t hl = w.h[c][k], hh = w.h[c][2 + k];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const uint32_t q = w.q[p][m];
+                    const uint32_t wl = (q & M4) | q6_hi_bytes((hl >> (2 * m)) & M2);
+                    const uint32_t wh = ((q >> 4) & M4) | q6_hi_bytes((hh >> (2 * m)) & M2);
+                    int a = t[4 * k + m];
+                    a = __mul24(clo, dot4(wl, alo[m], 0)) + a;
+                    a = __mul24(chi, dot4(wh, ahi[m], 0)) + a;
+                    t[4 * k + m] = a;
+                }
+            }
+            d = da * h2f(w.d);
+        }
+        if (valid) {
+            float* S = F + (size_t)r * 12 * lr + ul;
+#pragma unroll
+            for (int l = 0; l < 8; ++l) S[l * lr] = (float)t[l];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S[(8 + k) * lr] = ms[k];
+            float* D = F + kX86KD + (size_t)r * 2 * lr + ul;
+            D[0] = d;
+            D[lr] = dm;
+        }
+    }
+}
+
+// Fold lane f = (row f / NC, chain f % NC) runs its fma chain over the sub-item's n units
+// (Q8_0: 8 n blocks) in order; chains 0..7 take d, chains 8..11 (the min lanes) -dmin.
+template <int ACT>
+__device__ __forceinline__ void fold_sub_x86(float* F, int R, int lr, int n, bool last, float& acc) {
+    constexpr int NC = x86_chains<ACT>();
+    const int lane = threadIdx.x & 63, nf = R * NC;
+    for (int f = lane; f < nf; f += 64) {
+        const int r = f / NC, c = f - r * NC;
+        float a = acc;
+        if constexpr (ACT) {
+            const float* s = F + (size_t)(r * 8 + c) * 8 * lr;
+            const float* d = F + kX86QD + (size_t)r * 8 * lr;
+            for (int i = 0; i < 8 * n; i += 4) {
+                const float4 sv = *(const float4*)(s + i), dv = *(const float4*)(d + i);
+                a = __builtin_fmaf(dv.x, sv.x, a);
+                a = __builtin_fmaf(dv.y, sv.y, a);
+                a = __builtin_fmaf(dv.z, sv.z, a);
+                a = __builtin_fmaf(dv.w, sv.w, a);
+            }
+            if (last) F[kX86QG + f] = a;
+        } else {
+            const float* s = F + (size_t)(r * 12 + c) * lr;
+            const float* d = F + kX86KD + (size_t)(r * 2 + (c >= 8 ? 1 : 0)) * lr;
+            for (int u = 0; u < n; ++u) a = __builtin_fmaf(d[u], s[u], a);
+            if (last) F[kX86KG + f] = a;
+        }
+        if (last) a = 0.f;
+        acc = a;
+    }
+}
+// final value of row r of the task (after a wave_lds_sync)
+template <int ACT>
+__device__ __forceinline__ float row_final_x86(const float* F, int r, int type) {
+    if constexpr (ACT) {
+        return x86_hsum8(F + kX86QG + 8 * r);
+    } else {
+        const float* g = F + kX86KG + 12 * r;
+        const float h = x86_hsum8(g);
+        if (type == T_Q4_K) return h + ((g[8] + g[10]) + (g[9] + g[11]));
+        if (type == T_Q5_K) return h + g[8];
+        return h;
+    }
+}
+
+// upstream ggml_v_expf (AVX2/AVX-512: the ARM optimized-routines polynomial exp; every
+// lane of a vector computes exactly this, the special-case blend included), and
+// ggml_v_silu(x) = x / (1 + ggml_v_expf(-x))
+__device__ __forceinline__ float x86_v_expf(float x) {
+    const float r = 0x1.8p23f;
+    const float z = __builtin_fmaf(x, 0x1.715476p+0f, r);
+    const float n = z - r;
+    const float b = __builtin_fmaf(-n, 0x1.7f7d1cp-20f, __builtin_fmaf(-n, 0x1.62e4p-1f, x));
+    const uint32_t e = __float_as_uint(z) << 23;
+    const float k = __uint_as_float(e + __float_as_uint(1.0f));
+    const float u = b * b;
+    const float j = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(0x1.0e4020p-7f, b, 0x1.573e2ep-5f), u,
+                                                  __builtin_fmaf(0x1.555e66p-3f, b, 0x1.fffdb6p-2f)),
+                                   u, 0x1.ffffecp-1f * b);
+    if (!(fabsf(n) > 126.f)) return __builtin_fmaf(j, k, k);
+    const uint32_t g = n <= 0.f ? 0x82000000u : 0u;
+    const float s1 = __uint_as_float(g + 0x7f000000u), s2 = __uint_as_float(e - g);
+    if (fabsf(n) > 192.f) return s1 * s1;
+    return __builtin_fmaf(s2, j, s2) * s1;
+}
+__device__ __forceinline__ float x86_silu(float x) { return x / (1.0f + x86_v_expf(-x)); }
+
+// ----------------------------------------------------------------------------------
 // Row tasks.  A matvec launch's rows are cut into TASKS of R rows (gate/up launches: R
 // gate rows then the same R up rows); lane L works on row r = L / Lr of the task, units
 // L % Lr + Lr j (Lr lanes per row, a multiple of 4; R = 64 / Lr rounded down to a power
@@ -674,8 +909,8 @@ __host__ __device__ inline TaskGeo task_geo(const MVArgs& A) {
     return g;
 }
 
-// Fold buffer per wave: F[row][chain][Lr] terms + G[row][chain] chain results.
-constexpr int kFoldF = 9 * 64, kFoldFloats = kFoldF + 9 * 16;
+// Fold buffer per wave: F[row][chain][Lr] terms + G[row][chain] chain results (kFoldF,
+// kFoldFloats: above, with the x86 buffers).
 
 // Fold lane f (< R * chains) adds its chain's n terms of the sub-item (K-quants: chain f
 // = (row f / 9, chain f % 9), Lr terms apart; Q8_0: chain = row f, 8 terms per unit) in
@@ -820,7 +1055,7 @@ __device__ __forceinline__ void st_u16(uint16_t* p, uint16_t v) {
 
 // Epilogue of one finished pair (every lane holds both row sums; lane 0 writes).
 // (ANY_LANE: the calling lane writes; the batched matvec runs one token per lane)
-template <int EPI, bool WT = false, class MA, bool ANY_LANE = false>
+template <int EPI, bool WT = false, class MA, bool ANY_LANE = false, int X86 = 0>
 __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, PairSum v, int pos,
                                          unsigned long long& best) {
     const int lane = threadIdx.x & 63;
@@ -846,7 +1081,7 @@ __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, P
             best = k > best ? k : best;
         }
     } else if constexpr (EPI == EPI_SWIGLU) {
-        st_f32<WT>(A.y + p, llmi_silu(va) * vb);
+        st_f32<WT>(A.y + p, (X86 ? x86_silu(va) : llmi_silu(va)) * vb);
     } else if constexpr (EPI == EPI_QKV) {
         // sa.row0 tells q (0), k (nq) or v (nq+nk); rows (ra, ra+1) are a RoPE pair
         const int hd = A.head_dim;
@@ -921,21 +1156,25 @@ __device__ __forceinline__ LaneUnit lane_unit(const TaskGeo& g, const Sub& b, co
 
 // After the lanes' unit terms: store, fold, and on the row set's last sub-item the row
 // results and the epilogue (lane r' < R handles row r' of the task).
-template <int ACT, int EPI, class MA>
+// (X86: the lane's terms are already in F, unit_store_x86; tm is unused)
+template <int ACT, int EPI, class MA, int X86 = 0>
 __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo& g, int s, const Sub& b, const Seg& sg,
                                            const float (&tm)[9], const LaneUnit& lu, int r, int ul, float& acc,
                                            float& vg, int pos, unsigned long long& best) {
-    if (lu.valid) store_terms<ACT ? T_Q8_0 : T_Q4_K>(F, r, ul, g.lr, tm);
+    if constexpr (!X86)
+        if (lu.valid) store_terms<ACT ? T_Q8_0 : T_Q4_K>(F, r, ul, g.lr, tm);
     wave_lds_sync();
     const int n = min(g.lr, g.U - g.lr * b.j);
     const bool last = b.j == g.nj - 1;
-    fold_sub<ACT>(F, g.R, g.lr, n, last, acc);
+    if constexpr (X86) fold_sub_x86<ACT>(F, g.R, g.lr, n, last, acc);
+    else fold_sub<ACT>(F, g.R, g.lr, n, last, acc);
+    auto final_of = [&](int rr) { return X86 ? row_final_x86<ACT>(F, rr, sg.type) : row_final<ACT>(F, rr); };
     if (last) {
         wave_lds_sync();
         const int lane = threadIdx.x & 63;
         const int row = b.row0 + lane;
         if (lane < g.R && row < sg.rows) {
-            const float v = row_final<ACT>(F, lane);
+            const float v = final_of(lane);
             PairRef ref;
             ref.sa = ref.sb = sg;
             ref.ra = row;
@@ -944,12 +1183,12 @@ __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo&
             ref.type = sg.type;
             if constexpr (EPI == EPI_SWIGLU) {
                 if (s < g.nj) vg = v;
-                else epilogue<EPI, false, MA, true>(A, ref, row, PairSum{vg, v}, pos, best);
+                else epilogue<EPI, false, MA, true, X86>(A, ref, row, PairSum{vg, v}, pos, best);
             } else if constexpr (EPI == EPI_QKV) {
                 ref.vb = 1;  // RoPE pairs (row, row + 1): R and every segment start are even
-                if ((lane & 1) == 0) epilogue<EPI, false, MA, true>(A, ref, row, PairSum{v, row_final<ACT>(F, lane + 1)}, pos, best);
+                if ((lane & 1) == 0) epilogue<EPI, false, MA, true, X86>(A, ref, row, PairSum{v, final_of(lane + 1)}, pos, best);
             } else {
-                epilogue<EPI, false, MA, true>(A, ref, row, PairSum{v, 0.f}, pos, best);
+                epilogue<EPI, false, MA, true, X86>(A, ref, row, PairSum{v, 0.f}, pos, best);
             }
         }
     }
@@ -958,7 +1197,7 @@ __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo&
 
 // One task of any type, not pipelined (tasks whose type is not the kernel's primary type:
 // the Q6_K attn_v rows of a Q4_K QKV launch, mixed-type gate/up).
-template <int ACT, int EPI, class MA>
+template <int ACT, int EPI, class MA, int X86 = 0>
 __device__ __forceinline__ void task_any(const MA& A, const Lds& L, float* F, const TaskGeo& g, int task, int r, int ul,
                                          int pos, unsigned long long& best) {
     const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
@@ -969,7 +1208,17 @@ __device__ __forceinline__ void task_any(const MA& A, const Lds& L, float* F, co
         const LaneUnit lu = lane_unit(g, b, sg, r, ul);
         const uint8_t* rec = L.act + (size_t)lu.u * kRec;
         float tm[9];
-        if constexpr (ACT == 1) {
+        if constexpr (X86) {
+            if constexpr (ACT == 1) {
+                unit_store_x86<T_Q8_0>(load_unit<T_Q8_0>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid);
+            } else {
+                switch (sg.type) {
+                    case T_Q4_K: unit_store_x86<T_Q4_K>(load_unit<T_Q4_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid); break;
+                    case T_Q5_K: unit_store_x86<T_Q5_K>(load_unit<T_Q5_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid); break;
+                    default: unit_store_x86<T_Q6_K>(load_unit<T_Q6_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid); break;
+                }
+            }
+        } else if constexpr (ACT == 1) {
             unit_terms<T_Q8_0>(load_unit<T_Q8_0>(sg, lu.row, lu.u, g.U), rec, tm);
         } else {
             switch (sg.type) {
@@ -978,7 +1227,7 @@ __device__ __forceinline__ void task_any(const MA& A, const Lds& L, float* F, co
                 default: unit_terms<T_Q6_K>(load_unit<T_Q6_K>(sg, lu.row, lu.u, g.U), rec, tm); break;
             }
         }
-        sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
+        sub_finish<ACT, EPI, MA, X86>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
     }
 }
 
@@ -993,8 +1242,10 @@ __device__ __forceinline__ float dequant_elem(const Seg& w, int row, int e, int 
         case T_Q5_K:
         case T_Q6_K: {
             // residue order (common.h): element 64c + 32hi + l + 8i of the unit sits in
-            // part 2c + l/4, byte 4 (l % 4) + i (low nibble: hi = 0, high nibble: hi = 1)
-            const int t = e & 255, c = t >> 6, hi = (t >> 5) & 1, l = t & 7, i = (t & 31) >> 3, k = l >> 2, m = l & 3;
+            // part 2c + l/4, byte 4 (l % 4) + i (low nibble: hi = 0, high nibble: hi = 1);
+            // x86 order: element 64c + 32hi + 4l + i (l = 4k + m), the same part / byte / bits
+            const int t = e & 255, c = t >> 6, hi = (t >> 5) & 1;
+            const int l = w.x86 ? (t & 31) >> 2 : t & 7, i = w.x86 ? t & 3 : (t & 31) >> 3, k = l >> 2, m = l & 3;
             const uint8_t qb = w.a[piece_off(row, 2 * c + k, u, U, 8, w.rgs) + 4 * m + i];
             int q = hi ? (qb >> 4) : (qb & 0xF);
             if (w.type == T_Q6_K) {  // H part c: dword (2*hi + k), byte i, bits 2m: the 2 high bits XOR 2

@@ -23,9 +23,10 @@ namespace llmi {
 #endif
 constexpr bool kQ6Masked = LLMI_Q6_MASKED != 0;
 // LDS of a k_matvec launch of NW waves whose pipelined types are T / T2
-__host__ inline size_t mv_lds_total(int act, int cols, int nw, int t, int t2) {
-    const size_t base = fold_off(act, cols, nw) + (size_t)nw * kFoldFloats * 4;
-    return base + ((kQ6Masked && (t == T_Q6_K || t2 == T_Q6_K)) ? (size_t)(cols >> 8) * kQ6MaskRec : 0);
+__host__ inline size_t mv_lds_total(int act, int cols, int nw, int t, int t2, int x86 = 0) {
+    const int ff = x86 ? (act ? fold_floats<1, 1>() : fold_floats<0, 1>()) : kFoldFloats;
+    const size_t base = fold_off(act, cols, nw) + (size_t)nw * ff * 4;
+    return base + ((kQ6Masked && !x86 && (t == T_Q6_K || t2 == T_Q6_K)) ? (size_t)(cols >> 8) * kQ6MaskRec : 0);
 }
 
 static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_SPLIT_BY_PAIRS")) : 0;  // A/B only
@@ -47,7 +48,7 @@ static int g_split_by_pairs = getenv("LLMI_SPLIT_BY_PAIRS") ? atoi(getenv("LLMI_
 #define MV_STAMP(I, V)
 #endif
 
-template <int ACT, bool NORM, int EPI, int T, int NP, int NT = kMVThreads>
+template <int ACT, bool NORM, int EPI, int T, int NP, int NT = kMVThreads, int X86 = 0>
 __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds& L, float* F, int t0, int G, int tbeg,
                                                       int tend) {
     int pos = 0;
@@ -81,11 +82,11 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     // measured slower on every shape: gate+up 16.9 -> 21.2 us, 516 -> 433 tok/s)
     UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
     if (img) mv_img_finish<2 * NP + 1, NT>(A, L, RI);
-    else mv_prologue_finish<ACT, NORM, NP, NT>(A, L, R);
+    else mv_prologue_finish<ACT, NORM, NP, NT, X86>(A, L, R);
     __syncthreads();
     // Q6_K: the masked activation copies (mv_device.h q6_masks_build), after the fold buffers
     [[maybe_unused]] uint8_t* q6m = nullptr;
-    if constexpr (T == T_Q6_K && kQ6Masked) {
+    if constexpr (T == T_Q6_K && kQ6Masked && !X86) {
         q6m = (uint8_t*)L.act + fold_off(ACT, A.cols, NT / 64) + (size_t)(NT / 64) * kFoldFloats * 4;
         q6_masks_build<NT>(L, g.U, q6m);
         __syncthreads();
@@ -118,11 +119,13 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             // always issue the prefetch (a valid re-load of the current unit if none)
             nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
             float tm[9];
-            if constexpr (T == T_Q6_K && kQ6Masked)
+            if constexpr (X86)
+                unit_store_x86<T>(cur, L.act + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
+            else if constexpr (T == T_Q6_K && kQ6Masked)
                 unit_terms_q6m(cur, q6m + (size_t)lu.u * kQ6MaskRec, *(const float*)(L.act + (size_t)lu.u * kRec + kRecD), tm);
             else
                 unit_terms<T>(cur, L.act + (size_t)lu.u * kRec, tm);
-            sub_finish<ACT, EPI>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
+            sub_finish<ACT, EPI, MVArgs, X86>(A, F, g, s, b, sg, tm, lu, r, ul, acc, vg, pos, best);
 #if defined(LLMI_EXP_TRACE)
             ++nsub_done;
             if (nsub_done == 1) { MV_STAMP(2, MV_NOW) }
@@ -151,7 +154,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
 #endif
     }
     // remaining tasks of other types (or all tasks if the first was not of type T)
-    for (; task < tend; task += G) task_any<ACT, EPI>(A, L, F, g, task, r, ul, pos, best);
+    for (; task < tend; task += G) task_any<ACT, EPI, MVArgs, X86>(A, L, F, g, task, r, ul, pos, best);
     MV_STAMP(3, MV_NOW)
     MV_STAMP(5, ((unsigned long long)(__builtin_amdgcn_s_getreg(6164) & 15) << 32) | (unsigned)nsub_done)
     return best;
@@ -160,14 +163,14 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
 // A launch whose segments form two type groups (QKV with a Q6_K or Q5_K attn_v) is
 // split by workgroup: workgroups [0, split_wgs) run the tasks of type T, the rest the
 // tasks of type T2, each group pipelined in its own type (no divergence in a workgroup).
-template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T, int NT = kMVThreads>
+template <int ACT, bool NORM, int EPI, int T, int NP, int T2 = T, int NT = kMVThreads, int X86 = 0>
 __global__ __launch_bounds__(NT) void k_matvec(MVArgs A) {
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Lds L = carve(smem, ACT, A.cols);
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
-    float* F = (float*)(smem + fold_off(ACT, A.cols, NW)) + wave * kFoldFloats;
+    float* F = (float*)(smem + fold_off(ACT, A.cols, NW)) + wave * fold_floats<ACT, X86>();
     unsigned long long best;
     if constexpr (T2 == T) {
         // single type: optionally two task ranges, the larger one for the first dispatch
@@ -184,13 +187,13 @@ __global__ __launch_bounds__(NT) void k_matvec(MVArgs A) {
                 tb = A.split_tasks;
             }
         }
-        best = mv_body<ACT, NORM, EPI, T, NP, NT>(A, L, F, t0, G, tb, te);
+        best = mv_body<ACT, NORM, EPI, T, NP, NT, X86>(A, L, F, t0, G, tb, te);
     } else {
         if ((int)blockIdx.x < A.split_wgs)
-            best = mv_body<ACT, NORM, EPI, T, NP, NT>(A, L, F, blockIdx.x * NW + wave, A.split_wgs * NW, 0, A.split_tasks);
+            best = mv_body<ACT, NORM, EPI, T, NP, NT, X86>(A, L, F, blockIdx.x * NW + wave, A.split_wgs * NW, 0, A.split_tasks);
         else
-            best = mv_body<ACT, NORM, EPI, T2, NP, NT>(A, L, F, A.split_tasks + (blockIdx.x - A.split_wgs) * NW + wave,
-                                                       (gridDim.x - A.split_wgs) * NW, A.split_tasks, A.ntasks);
+            best = mv_body<ACT, NORM, EPI, T2, NP, NT, X86>(A, L, F, A.split_tasks + (blockIdx.x - A.split_wgs) * NW + wave,
+                                                            (gridDim.x - A.split_wgs) * NW, A.split_tasks, A.ntasks);
     }
     if constexpr (EPI == EPI_LOGITS) {
         // workgroup max of the lanes' keys, then one atomic into this workgroup's slot
@@ -275,46 +278,41 @@ static inline int wide_epis() {
     return v;
 }
 constexpr int kMVWide = 512;
-template <int ACT, bool NORM, int T, int EPI, int NP>
+template <int ACT, bool NORM, int T, int EPI, int NP, int X86>
 static hipError_t mv_launch_wide(const MVArgs& a, hipStream_t s) {
     constexpr int NW = kMVWide / 64;
-    const size_t lds = mv_lds_total(ACT, a.cols, NW, T, T);
+    const size_t lds = mv_lds_total(ACT, a.cols, NW, T, T, X86);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int blocks = std::max(1, std::min(cu_count(), (a.ntasks + NW - 1) / NW));
-    launch_k(k_matvec<ACT, NORM, EPI, T, NP, T, kMVWide>, dim3(blocks), dim3(kMVWide), lds, s, true, true, a);
+    launch_k(k_matvec<ACT, NORM, EPI, T, NP, T, kMVWide, X86>, dim3(blocks), dim3(kMVWide), lds, s, true, true, a);
     return hipGetLastError();
 }
-template <int ACT, bool NORM, int T, int EPI>
+template <int ACT, bool NORM, int T, int EPI, int X86>
 static bool mv_try_wide(const MVArgs& a, hipStream_t s, hipError_t& e) {
-    if constexpr (EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV || EPI == EPI_LOGITS) {
+    if constexpr ((EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV || EPI == EPI_LOGITS) && !(X86 && ACT)) {
         const int wc = wide_cols();
         if (wc <= 0 || a.cols < wc || cu_count() <= 0 || !(wide_epis() >> EPI & 1)) return false;
         for (int i = 0; i < a.nseg; ++i)
             if (a.seg[i].type != T) return false;  // single-type launches only
         const int per = (a.cols / 16 + kMVWide - 1) / kMVWide;
-        e = per <= 1 ? mv_launch_wide<ACT, NORM, T, EPI, 1>(a, s)
-            : per <= 2 ? mv_launch_wide<ACT, NORM, T, EPI, 2>(a, s) : mv_launch_wide<ACT, NORM, T, EPI, 4>(a, s);
+        e = per <= 1 ? mv_launch_wide<ACT, NORM, T, EPI, 1, X86>(a, s)
+            : per <= 2 ? mv_launch_wide<ACT, NORM, T, EPI, 2, X86>(a, s) : mv_launch_wide<ACT, NORM, T, EPI, 4, X86>(a, s);
         return true;
     } else {
         (void)a; (void)s; (void)e;
         return false;
     }
 }
-template <int ACT, bool NORM, int T, int EPI, int NP>
+template <int ACT, bool NORM, int T, int EPI, int NP, int X86>
 static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds_in, hipStream_t s) {
-    const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T));
+    const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T, X86));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    auto k = k_matvec<ACT, NORM, EPI, T, NP>;
+    auto k = k_matvec<ACT, NORM, EPI, T, NP, T, kMVThreads, X86>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
     a.split_wgs = 0;
     const double sh = old_share();
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
-        return n;
-    }();
+    const int cus = cu_count();
     // long launches only (>= 4 tasks per wave), and only when the grid is exactly two
     // dispatch rounds of one workgroup per CU
     if (sh > 0 && cus > 0 && (int)g.x == 2 * cus && a.ntasks >= 4 * (int)g.x * kMVWaves) {
@@ -339,11 +337,11 @@ static inline int split_groups(int wgs, int p1, int p2, double b1, double b2) {
     }
     return best;
 }
-template <int ACT, bool NORM, int T, int T2, int EPI, int NP>
+template <int ACT, bool NORM, int T, int T2, int EPI, int NP, int X86>
 static hipError_t mv_launch2(const MVArgs& a0, int split_tasks, dim3 grid, size_t lds_in, hipStream_t s) {
-    const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T2));
+    const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T2, X86));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    auto k = k_matvec<ACT, NORM, EPI, T, NP, T2>;
+    auto k = k_matvec<ACT, NORM, EPI, T, NP, T2, kMVThreads, X86>;
     const dim3 g = resident_grid(k, grid, lds);
     MVArgs a = a0;
     a.split_tasks = split_tasks;
@@ -366,31 +364,31 @@ static inline int prologue_np(int cols) {
     return per <= 1 ? 1 : per <= 2 ? 2 : 4;
 }
 
-template <int ACT, bool NORM, int T, int EPI>
+template <int ACT, bool NORM, int T, int EPI, int X86>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     hipError_t e = hipSuccess;
-    if (mv_try_wide<ACT, NORM, T, EPI>(a, s, e)) return e;
+    if (mv_try_wide<ACT, NORM, T, EPI, X86>(a, s, e)) return e;
     switch (prologue_np(a.cols)) {
-        case 1: return mv_launch<ACT, NORM, T, EPI, 1>(a, grid, lds, s);
-        case 2: return mv_launch<ACT, NORM, T, EPI, 2>(a, grid, lds, s);
-        default: return mv_launch<ACT, NORM, T, EPI, 4>(a, grid, lds, s);
+        case 1: return mv_launch<ACT, NORM, T, EPI, 1, X86>(a, grid, lds, s);
+        case 2: return mv_launch<ACT, NORM, T, EPI, 2, X86>(a, grid, lds, s);
+        default: return mv_launch<ACT, NORM, T, EPI, 4, X86>(a, grid, lds, s);
     }
 }
 
 // Instantiated (ACT, NORM, EPI) combinations: STORE and ADD with or without the fused
 // RMSNorm; QKV, SWIGLU and LOGITS always take a normalised input.
-template <int ACT, bool NORM, int T>
+template <int ACT, bool NORM, int T, int X86>
 hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipStream_t s) {
     switch (epi) {
-        case EPI_STORE: return mv_launch_np<ACT, NORM, T, EPI_STORE>(a, grid, lds, s);
-        case EPI_ADD: return mv_launch_np<ACT, NORM, T, EPI_ADD>(a, grid, lds, s);
+        case EPI_STORE: return mv_launch_np<ACT, NORM, T, EPI_STORE, X86>(a, grid, lds, s);
+        case EPI_ADD: return mv_launch_np<ACT, NORM, T, EPI_ADD, X86>(a, grid, lds, s);
         default: break;
     }
     if constexpr (NORM) {
         switch (epi) {
-            case EPI_QKV: return mv_launch_np<ACT, NORM, T, EPI_QKV>(a, grid, lds, s);
-            case EPI_SWIGLU: return mv_launch_np<ACT, NORM, T, EPI_SWIGLU>(a, grid, lds, s);
-            case EPI_LOGITS: return mv_launch_np<ACT, NORM, T, EPI_LOGITS>(a, grid, lds, s);
+            case EPI_QKV: return mv_launch_np<ACT, NORM, T, EPI_QKV, X86>(a, grid, lds, s);
+            case EPI_SWIGLU: return mv_launch_np<ACT, NORM, T, EPI_SWIGLU, X86>(a, grid, lds, s);
+            case EPI_LOGITS: return mv_launch_np<ACT, NORM, T, EPI_LOGITS, X86>(a, grid, lds, s);
             default: break;
         }
     }
@@ -399,9 +397,9 @@ hipError_t mv_dispatch_epi(const MVArgs& a, int epi, dim3 grid, size_t lds, hipS
 
 // QKV whose q/k and v segments are two type groups: workgroup-split launch (k_matvec's
 // T2 path), called from kernels.hip mv_dispatch_qkv2.
-template <bool NORM, int T, int T2>
+template <bool NORM, int T, int T2, int X86>
 hipError_t mv_qkv2_launch(const MVArgs& a, int split_tasks, dim3 grid, size_t lds, hipStream_t s) {
-    return mv_launch2<0, NORM, T, T2, EPI_QKV, 1>(a, split_tasks, grid, lds, s);
+    return mv_launch2<0, NORM, T, T2, EPI_QKV, 1, X86>(a, split_tasks, grid, lds, s);
 }
 
 }  // namespace llmi

@@ -99,8 +99,9 @@ template <int T, int NP>
 struct PfB {
     h8 b[NP];  // Q6_K: b[0] = (q-32)*sl, b[1] = (q-32)*sh
 };
-// B fragments of residue l (K-quants) or 32-block l (Q8_0) for this lane
-template <int T>
+// B fragments of residue l (K-quants) or 32-block l (Q8_0) for this lane (X86: of x86
+// lane l, the weights' x86 byte order: a Q6_K dword = 4 elements of ONE sub-block)
+template <int T, int X86 = 0>
 __device__ __forceinline__ void pf_build_b(const PfW<T>& w, int l, h2 slo, h2 shi, h2 slo_o, h2 shi_o, const h2* s6,
                                            const h2* s6o, h8* out) {
     if constexpr (T == T_Q8_0) {
@@ -143,13 +144,15 @@ __device__ __forceinline__ void pf_build_b(const PfW<T>& w, int l, h2 slo, h2 sh
             hi01 |= (h01 ^ 0x00020002u) << 4;
             hi23 |= (h23 ^ 0x00020002u) << 4;
             // pairs: (lo01) sub-block 4g, (lo23) 4g+1, (hi01) 4g+2, (hi23) 4g+3
+            // (X86: lo01 and lo23 sub-block 4g + l/4, hi01 and hi23 4g + 2 + l/4)
             const uint32_t m[4] = {pf_magic(lo01), pf_magic(lo23), pf_magic(hi01), pf_magic(hi23)};
 #pragma unroll
             for (int part = 0; part < 2; ++part) {
                 h8 r;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const h2 x = as_h2(pf_scale(m[k], s6[2 * k + part], s6o[2 * k + part]));
+                    const int sbk = X86 ? (k >> 1) * 2 + (l >> 2) : k;
+                    const h2 x = as_h2(pf_scale(m[k], s6[2 * sbk + part], s6o[2 * sbk + part]));
                     r[2 * k] = x[0];  // fragment order: j = 4h + i
                     r[2 * k + 1] = x[1];
                 }

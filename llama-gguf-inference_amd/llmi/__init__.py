@@ -17,6 +17,9 @@ from ._lib import LlmiLibraryError, last_error, lib, llama_context_params, llama
 
 # ggml type ids
 F32, F16, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 8, 12, 13, 14, 15
+# model numerics (llama_model_params.numerics): ggml's generic scalar order, or upstream's
+# x86 AVX2 association (the reference's NGL=0 build)
+NUMERICS_GENERIC, NUMERICS_X86 = 0, 1
 PRESETS = (
     "llama3-8b-q4km", "llama3-70b-q4km", "tinyllama-q8_0", "mistral7b-q6k", "mistral7b-q5km",
     "tiny-mixed", "tiny-mixed-d128",
@@ -143,13 +146,14 @@ class Model:
     """llama_model_load_from_file: GGUF -> HBM arena on `main_gpu`."""
 
     def __init__(self, path: str, n_gpu_layers: int = 999, main_gpu: int = 0, vocab_only: bool = False,
-                 no_upload: bool = False):
+                 no_upload: bool = False, numerics: int = NUMERICS_GENERIC):
         L = lib()
         p = L.llama_model_default_params()
         p.n_gpu_layers = n_gpu_layers
         p.main_gpu = main_gpu
         p.vocab_only = vocab_only
         p.no_upload = no_upload
+        p.numerics = numerics
         self._h = L.llama_model_load_from_file(path.encode(), p)
         if not self._h:
             raise LlmiError(last_error())
@@ -169,27 +173,33 @@ class Model:
         buf = C.create_string_buffer(256)
         L.llama_model_desc(self._h, buf, 256)
         self.desc = buf.value.decode()
+        self.numerics = int(L.llmi_model_numerics(self._h))
 
     @classmethod
-    def load_fanout(cls, path: str, main_gpu: int, uid: bytes, nranks: int, rank: int) -> "Model":
+    def load_fanout(cls, path: str, main_gpu: int, uid: bytes, nranks: int, rank: int,
+                    numerics: int = NUMERICS_GENERIC) -> "Model":
         """Load with the replica fan-out pipelined behind the upload (llmi_model_load_fanout,
         SURVEY.md §8e): every rank calls it with the same RCCL unique id; rank 0 uploads the
         GGUF, the others receive the arena in 256 MB pieces over xGMI."""
         L = lib()
         p = L.llama_model_default_params()
         p.main_gpu = main_gpu
+        p.numerics = numerics
         h = L.llmi_model_load_fanout(path.encode(), p, uid, int(nranks), int(rank))
         if not h:
             raise LlmiError(last_error())
         return cls._from_handle(h, path, main_gpu)
 
     @classmethod
-    def load_replicated(cls, path: str, main_gpu: int, devices: Sequence[int]) -> tuple["Model", list["Model"]]:
+    def load_replicated(cls, path: str, main_gpu: int, devices: Sequence[int], n_gpu_layers: int = 999,
+                        numerics: int = NUMERICS_GENERIC) -> tuple["Model", list["Model"]]:
         """One process: the model on main_gpu and a replica on each of `devices`, the RCCL
         broadcast pipelined behind the upload (llmi_model_load_replicated)."""
         L = lib()
         p = L.llama_model_default_params()
         p.main_gpu = main_gpu
+        p.n_gpu_layers = n_gpu_layers
+        p.numerics = numerics
         n = len(devices)
         devs = (C.c_int32 * max(1, n))(*devices)
         out = (C.c_void_p * max(1, n))()
@@ -214,6 +224,7 @@ class Model:
         self.n_ctx_train = L.llama_model_n_ctx_train(h)
         self.size = int(L.llama_model_size(h))
         self.desc = ""
+        self.numerics = int(L.llmi_model_numerics(h))
         return self
 
     @property

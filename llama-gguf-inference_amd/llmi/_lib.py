@@ -25,6 +25,7 @@ class llama_model_params(C.Structure):
         ("vocab_only", C.c_bool),
         ("use_mmap", C.c_bool),
         ("no_upload", C.c_bool),
+        ("numerics", C.c_int32),
     ]
 
 
@@ -90,6 +91,7 @@ SIGNATURES = {
     "llama_n_ctx": (C.c_uint32, [_P]),
     "llama_kv_self_clear": (None, [_P]),
     "llmi_last_error": (C.c_char_p, []),
+    "llmi_model_numerics": (C.c_int32, [_P]),
     "llmi_device_count": (C.c_int32, []),
     "llmi_greedy_ith": (C.c_int32, [_P, C.c_int32]),
     "llmi_generate_greedy": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),

@@ -396,8 +396,9 @@ class Engine:
     ties to the lowest index) and are served there with continuous batching."""
 
     def __init__(self, path: str, n_ctx: int, n_gpu_layers: int, devices: list[int], slots: int = 4,
-                 chunk: int = 8, contexts=None, sampling: Optional[SamplingParams] = None):
+                 chunk: int = 8, contexts=None, sampling: Optional[SamplingParams] = None, numerics: int = 0):
         self.path, self.n_ctx, self.ngl, self.devices = path, n_ctx, n_gpu_layers, devices
+        self.numerics = numerics  # llmi.NUMERICS_GENERIC / NUMERICS_X86 (DESIGN.md §5)
         self.sampling = sampling or SamplingParams()  # server defaults (llama-server's)
         self.slots, self.chunk = max(1, slots), max(1, chunk)
         self.ready = False
@@ -420,9 +421,11 @@ class Engine:
                 from . import tokenizer as T
 
                 if len(self.devices) > 1:  # replicas: RCCL pieces pipelined behind the upload
-                    m0, reps = llmi.Model.load_replicated(self.path, self.devices[0], self.devices[1:])
+                    m0, reps = llmi.Model.load_replicated(self.path, self.devices[0], self.devices[1:],
+                                                          n_gpu_layers=self.ngl, numerics=self.numerics)
                 else:
-                    m0, reps = llmi.Model(self.path, n_gpu_layers=self.ngl, main_gpu=self.devices[0]), []
+                    m0, reps = llmi.Model(self.path, n_gpu_layers=self.ngl, main_gpu=self.devices[0],
+                                          numerics=self.numerics), []
                 models = [m0] + reps
                 self._models = models
                 ctxs = [llmi.Context(m, n_ctx=self.n_ctx, n_seq=self.slots) for m in models]
@@ -686,6 +689,9 @@ def parse_args(argv=None):
     ap.add_argument("-np", "--parallel", type=int, default=int(os.environ.get("LLMI_SLOTS", "4")),
                     help="sequences (slots) per replica decoded together (continuous batching)")
     ap.add_argument("--decode-chunk", type=int, default=8, help="tokens per batched decode call")
+    ap.add_argument("--numerics", choices=("generic", "x86"), default=os.environ.get("LLMI_NUMERICS", "generic"),
+                    help="fp32 association of every kernel: ggml's generic order, or upstream's x86 AVX2 build "
+                         "(the reference's NGL=0 path)")
     # llama-server's sampling flags and defaults (per-request fields override them)
     d = SamplingParams()
     ap.add_argument("--temp", type=float, default=d.temperature)
@@ -718,7 +724,7 @@ def main(argv=None) -> int:
                         repeat_penalty=args.repeat_penalty, repeat_last_n=args.repeat_last_n,
                         presence_penalty=args.presence_penalty, frequency_penalty=args.frequency_penalty, seed=args.seed)
     eng = Engine(args.model, args.ctx_size, args.ngl, list(range(max(1, args.replicas))), slots=args.parallel,
-                 chunk=args.decode_chunk, sampling=sp)
+                 chunk=args.decode_chunk, sampling=sp, numerics=1 if args.numerics == "x86" else 0)
     srv = make_server(eng, args.host, args.port, key)
     threading.Thread(target=eng.load, daemon=True).start()
     print(f"[llmi-server] listening on {args.host}:{args.port}", file=sys.stderr, flush=True)

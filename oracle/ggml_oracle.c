@@ -757,6 +757,14 @@ static void quantize_act(int wtype, const float* x, void* act, int64_t cols) {
     else memcpy(act, x, (size_t)cols * 4);
 }
 
+/* the activation conversion or_matvec applies for weight type wtype (vec_dot_type of
+ * wtype, under the current mode: x86 q8_0 rounding with OR_X86_Q80) */
+int or_quantize_act(int wtype, const float* x, void* out, int64_t cols) {
+    if (or_vec_dot_type(wtype) < 0 || cols % or_block_size(or_vec_dot_type(wtype))) return -1;
+    quantize_act(wtype, x, out, cols);
+    return 0;
+}
+
 /* upstream ggml_compute_forward_mul_mat for one src1 column: src1 is converted to
  * vec_dot_type once, then vec_dot per src0 row. */
 int or_matvec(int wtype, const void* W, int64_t rows, int64_t cols, const float* x, float* y, int nthreads) {

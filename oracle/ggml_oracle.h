@@ -50,6 +50,8 @@ int or_set_fast_dots(int on);
  * dots and exp onto upstream's x86 AVX2 association (flags in ggml_oracle.c: 1 dots, 2 q8_0,
  * 4 f16 dots, 8 ggml_v_expf, 16 libm expf, 32 no FMA contraction).  0 = generic (default). */
 int or_set_x86_mode(int flags);
+/* the activation conversion or_matvec applies to x for weight type wtype (current mode) */
+int or_quantize_act(int wtype, const float* x, void* out, int64_t cols);
 int or_get_x86_mode(void);
 /* y[r] = vec_dot(W[r], quantize(x)) for r < rows (x is f32[cols]); OpenMP over rows */
 int or_matvec(int wtype, const void* W, int64_t rows, int64_t cols, const float* x, float* y, int nthreads);

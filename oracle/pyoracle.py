@@ -87,6 +87,7 @@ def lib() -> C.CDLL:
         "or_bytes_per_token": (C.c_double, [P, C.c_int]),
         "or_set_fast_dots": (C.c_int, [C.c_int]),
         "or_set_x86_mode": (C.c_int, [C.c_int]),
+        "or_quantize_act": (C.c_int, [C.c_int, P, P, C.c_int64]),
         "or_get_x86_mode": (C.c_int, []),
     }
     for k, (r, a) in sig.items():
@@ -149,8 +150,33 @@ def quantize_q8_0(x: np.ndarray) -> np.ndarray:
     return out
 
 
-def quantize_act(wtype: int, x: np.ndarray) -> np.ndarray:
-    return quantize_q8_0(x) if wtype == Q8_0 else quantize_q8_K(x)
+def quantize_act(wtype: int, x: np.ndarray, x86: int | None = None) -> np.ndarray:
+    """The activation conversion of a matvec with weight type wtype; x86: the oracle's
+    association flags for the call (X86_Q80: upstream's x86 round-half-even q8_0; None:
+    the current mode)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n = x.size // 32 * 34 if wtype == Q8_0 else x.size // 256 * 292
+    out = np.zeros(n, dtype=np.uint8)
+    with x86_mode(x86):
+        assert lib().or_quantize_act(wtype, _p(x), _p(out), x.size) == 0
+    return out
+
+
+class x86_mode:
+    """Context manager: the oracle's (process-global) association flags for a block."""
+
+    def __init__(self, flags: int | None):
+        self.flags = flags  # None: leave the current mode
+
+    def __enter__(self):
+        self.old = int(lib().or_get_x86_mode())
+        if self.flags is not None:
+            lib().or_set_x86_mode(int(self.flags))
+        return self
+
+    def __exit__(self, *exc):
+        lib().or_set_x86_mode(self.old)
+        return False
 
 
 def rms_norm_mul(x: np.ndarray, w: np.ndarray, eps: float) -> np.ndarray:
@@ -161,11 +187,13 @@ def rms_norm_mul(x: np.ndarray, w: np.ndarray, eps: float) -> np.ndarray:
     return y
 
 
-def matvec(type_: int, W: np.ndarray, rows: int, cols: int, x: np.ndarray, threads: int = 0) -> np.ndarray:
+def matvec(type_: int, W: np.ndarray, rows: int, cols: int, x: np.ndarray, threads: int = 0,
+           x86: int | None = None) -> np.ndarray:
     W = np.ascontiguousarray(W, dtype=np.uint8)
     x = np.ascontiguousarray(x, dtype=np.float32)
     y = np.empty(rows, dtype=np.float32)
-    assert lib().or_matvec(type_, _p(W), rows, cols, _p(x), _p(y), threads or nthreads()) == 0
+    with x86_mode(x86):
+        assert lib().or_matvec(type_, _p(W), rows, cols, _p(x), _p(y), threads or nthreads()) == 0
     return y
 
 

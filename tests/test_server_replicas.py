@@ -193,7 +193,7 @@ def test_replicas_flag_wires_llmi_replicate(tmp_path, monkeypatch):
             self.n_vocab, self.bos, self.eos = 1000, 1, 2
 
         @classmethod
-        def load_replicated(cls, p, main_gpu, devices):
+        def load_replicated(cls, p, main_gpu, devices, **k):
             log.append(("load_replicated", p, main_gpu, list(devices)))
             m = cls.__new__(cls)
             m.n_vocab, m.bos, m.eos = 1000, 1, 2
