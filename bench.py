@@ -51,7 +51,7 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--model-dir", default=os.environ.get("LLMI_BENCH_DIR", "/tmp/llmi_bench"))
     ap.add_argument("--profile-steps", type=int, default=20)
-    ap.add_argument("--cpu-sample-tokens", type=int, default=48)
+    ap.add_argument("--cpu-sample-tokens", type=int, default=20, help="timed CPU-baseline tokens (at the GPU window)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--batch-seqs", default="2,4,8",
                     help="continuous-batching leg: sequence counts to time (comma list, '' to skip)")
@@ -61,6 +61,11 @@ def parse(argv=None):
     ap.add_argument("--no-c2-full", action="store_true", help="skip the full-trajectory (128 -> 640) timing")
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r04"),
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
+    ap.add_argument("--numerics", choices=("generic", "x86"), default="generic",
+                    help="fp32 association of every kernel (DESIGN.md §5): ggml's generic order, or upstream's "
+                         "x86 AVX2 build (the reference's NGL=0 path)")
+    ap.add_argument("--no-other-numerics", action="store_true",
+                    help="skip the leg that times the same window in the other numerics mode")
     return ap.parse_args(argv)
 
 
@@ -179,8 +184,12 @@ class LlmiEngine:
         self.path = path
         self.gate_type = GATE_TYPE.get(args.preset, "?")
         t = time.perf_counter()
-        self.model, self.fanout_s = load_replica(path, dist, llmi.rccl_unique_id, llmi.Model.load_fanout,
-                                                 lambda p, g: llmi.Model(p, main_gpu=g))
+        self.numerics = llmi.NUMERICS_X86 if args.numerics == "x86" else llmi.NUMERICS_GENERIC
+        num = self.numerics
+        self.model, self.fanout_s = load_replica(
+            path, dist, llmi.rccl_unique_id,
+            lambda p, g, uid, nr, r: llmi.Model.load_fanout(p, g, uid, nr, r, numerics=num),
+            lambda p, g: llmi.Model(p, main_gpu=g, numerics=num))
         self.load_s = time.perf_counter() - t
         last = window_start(args.prompt, args.steps, args.warmup) + args.steps
         n_ctx = ((max(last, args.prompt + C2_DECODE) + args.profile_steps + 2 + 255) // 256) * 256
@@ -234,6 +243,41 @@ class LlmiEngine:
         """Per-class kernel time at the current position (consumes no tokens)."""
         return self.ctx.profile_kernels(self.next, self.pos, n)
 
+    def other_numerics(self, window: tuple[int, int]) -> dict:
+        """The same timed window and the C2 trajectory in the OTHER numerics mode (a second
+        replica of the weights in that mode's byte order on this GPU): reported beside
+        `value`, never as it."""
+        llmi = self.llmi
+        num = llmi.NUMERICS_GENERIC if self.numerics == llmi.NUMERICS_X86 else llmi.NUMERICS_X86
+        m = llmi.Model(self.path, main_gpu=self.dist.local_rank, numerics=num)
+        ctx = llmi.Context(m, n_ctx=self.ctx.n_ctx)
+        assert ctx.decode(self.prompt) == 0
+        first = ctx.greedy(-1)
+        pre = window[0] - len(self.prompt)
+        toks = ctx.generate_greedy(first, len(self.prompt), pre) if pre > 0 else []
+        nxt = toks[-1] if toks else first
+        self.sync()
+        t0 = time.perf_counter()
+        ctx.generate_greedy(nxt, window[0], window[1] - window[0])
+        self.sync()
+        dt = time.perf_counter() - t0
+        k = window[1] - window[0]
+        out = {"numerics": "x86" if num == llmi.NUMERICS_X86 else "generic", "tok_s": round(k / dt, 2),
+               "ms_per_step": round(dt / k * 1e3, 4), "timed_window": list(window),
+               "prefill_path": "mfma" if m.prefill_supported else "decode-steps"}
+        if self.args.prompt == C2_PROMPT and not self.args.no_c2_full:
+            ctx.kv_clear()
+            assert ctx.decode(self.prompt) == 0
+            first = ctx.greedy(-1)
+            self.sync()
+            t0 = time.perf_counter()
+            ctx.generate_greedy(first, len(self.prompt), C2_DECODE)
+            self.sync()
+            out["c2_full_tok_s"] = round(C2_DECODE / (time.perf_counter() - t0), 2)
+        ctx.close()
+        m.close()
+        return out
+
     def batched(self, counts: list[int], steps: int) -> dict:
         """Continuous-batching leg (reported beside `value`, never as it): k sequences of one
         context (the same 128-token prompt length, different prompts) advance together
@@ -276,61 +320,87 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(path: str, n_tokens: int, prompt: list[int]) -> dict:
+def host_cpu() -> dict:
+    """The host's CPU model, the logical CPUs this process may run on and its physical cores."""
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus_granted": len(os.sched_getaffinity(0)), "logical_cpus": os.cpu_count()}
+
+
+def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tuple[int, int], n_tokens: int) -> dict:
     """The reference's CPU path (NGL=0: llama.cpp built for the host, Dockerfile.cpu:84-89)
-    restated — oracle/, test infrastructure — timed on this host: the -O3
-    -march=x86-64-v3 build with its AVX2 dot products (the x86 kernels' maddubs/madd
-    structure and 8-lane fp32 block accumulation; or_set_fast_dots), one OpenMP thread per
-    physical core up to the box's CPU share (16).  Workload: the same 128-token prompt (its
-    KV rows filled by decode steps without logits, untimed), then n_tokens timed greedy
-    decode steps at context 128+ — a bounded sample of the GPU run's decode.  Beside it the
-    host DRAM streaming-read rate and the decode roofline it implies, and the scalar
-    generic-order restatement's rate (the parity checker, 2 steps)."""
+    restated — oracle/, test infrastructure — timed on this host, on the GPU run's own
+    workload: the same prompt and the GPU's generated tokens fill the KV cache up to the
+    GPU's timed window (untimed, decode steps without logits), then n_tokens greedy decode
+    steps at the window's first positions are timed.  The -O3 -march=x86-64-v3 build with
+    its AVX2 dot products (the x86 kernels' maddubs/madd structure and 8-lane fp32 block
+    accumulation; or_set_fast_dots), OpenMP threads = every physical core of the CPUs this
+    process may run on (the reference's THREADS=0, scripts/start.sh:484-486: llama.cpp's
+    own default), and again at 8 threads (its documented CPU config,
+    docs/CONFIGURATION.md:579-587).  Beside it the host DRAM streaming-read rate, the
+    fraction of it the decode reaches, and the decode roofline it implies."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import pyoracle as po
 
     po.prefer_simd()
+    cpu = host_cpu()
     phys = po.physical_cores()
-    threads = max(1, min(phys, 16))
+    threads = max(1, min(phys, cpu["logical_cpus_granted"]))
     fast = po.set_fast_dots(True)
-    om = po.OracleModel(path, n_ctx=len(prompt) + n_tokens + 4, threads=threads)
+    ctx_toks = (prompt + list(generated))[: window[0]]
+    om = po.OracleModel(path, n_ctx=window[0] + n_tokens + 8, threads=threads)
+    res = {}
     try:
         t = time.perf_counter()
-        for i, tk in enumerate(prompt[:-1]):  # KV rows of the prompt (untimed)
+        for i, tk in enumerate(ctx_toks[:-1]):  # KV rows up to the window (untimed)
             om.decode(tk, i, logits=False)
         fill_s = time.perf_counter() - t
-        lg = om.decode(prompt[-1], len(prompt) - 1)  # first step (page-in), untimed
-        tok = int(np.argmax(lg))
-        t0 = time.perf_counter()
-        for k in range(n_tokens):
-            lg = om.decode(tok, len(prompt) + k)
-            tok = int(np.argmax(lg))
-        dt = time.perf_counter() - t0
-        # the scalar generic-order restatement (the parity checker) for comparison
-        po.set_fast_dots(False)
-        t1 = time.perf_counter()
-        for k in range(2):
-            om.decode(tok, len(prompt) + n_tokens + k)
-        generic_tok_s = 2 / (time.perf_counter() - t1)
+        lg = om.decode(ctx_toks[-1], len(ctx_toks) - 1)  # -> the window's first token (untimed)
+        tok0 = int(np.argmax(lg))
+
+        def timed(nth: int) -> float:
+            om.threads = nth
+            tok = tok0
+            t0 = time.perf_counter()
+            for k in range(n_tokens):
+                out = om.decode(tok, window[0] + k)
+                tok = int(np.argmax(out))
+            return n_tokens / (time.perf_counter() - t0)
+
+        res["all"] = timed(threads)
+        res["t8"] = timed(8)
     finally:
         po.set_fast_dots(False)
-    bpt = om.bytes_per_token(len(prompt) + n_tokens // 2)
+    bpt = om.bytes_per_token(window[0] + n_tokens // 2)
     om.close()
     host_gbps = po.host_stream_gbps(1 << 30, 3, threads)
-    tok_s = n_tokens / dt
-    return {"value": round(tok_s, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
-            "physical_cores": phys,
-            "achieved_GBps": round(tok_s * bpt / 1e9, 2),
+    tok_s = res["all"]
+    gbps = tok_s * bpt / 1e9
+    return {"value": round(tok_s, 3), "unit": "tokens/s", "cores": threads, "kind": "port", "threads": threads,
+            "physical_cores": phys, "host_cpu": cpu,
+            "ctx_window": [window[0], window[0] + n_tokens - 1],
+            "achieved_GBps": round(gbps, 2),
+            "stream_frac": round(gbps / host_gbps, 4) if host_gbps > 0 else None,
+            "threads_8": {"value": round(res["t8"], 3), "unit": "tokens/s",
+                          "achieved_GBps": round(res["t8"] * bpt / 1e9, 2)},
             "dots": "avx2 (x86 kernel association)" if fast else "generic scalar (no AVX2 in this build)",
-            "generic_order_tok_s": round(generic_tok_s, 3),
             "host_dram_roofline": {"stream_read_GBps": round(host_gbps, 1),
                                    "decode_tok_s_at_roofline": round(host_gbps * 1e9 / bpt, 2)},
-            "sample": f"{n_tokens} greedy decode steps at ctx {len(prompt)}..{len(prompt) + n_tokens - 1} after the "
-                      f"same {len(prompt)}-token prompt (KV rows filled by decode steps in {fill_s:.1f}s, untimed) "
-                      f"on {os.path.basename(path)}; oracle/ggml_oracle.c -O3 -march=x86-64-v3 with AVX2 dots, "
-                      f"OpenMP {threads} threads ({phys} physical cores on the host; 16 = the box's CPU share per GPU)"}
+            "sample": f"{n_tokens} greedy decode steps at ctx {window[0]}..{window[0] + n_tokens - 1}, the GPU's timed "
+                      f"window, after the same {len(prompt)}-token prompt and the GPU's generated tokens (KV rows "
+                      f"filled by {len(ctx_toks) - 1} decode steps in {fill_s:.1f}s, untimed) on {os.path.basename(path)}; "
+                      f"oracle/ggml_oracle.c -O3 -march=x86-64-v3 with AVX2 dots, OpenMP {threads} threads "
+                      f"(every physical core granted; {cpu['logical_cpus_granted']} logical CPUs, {cpu['model']}) "
+                      f"and 8 threads (the reference's documented CPU config)"}
 
 
 def env_knobs() -> dict:
@@ -390,6 +460,12 @@ def main(argv=None):
     window = (eng.pos - args.steps, eng.pos)
     prof = eng.profile(args.profile_steps) if args.profile_steps > 0 else {}
     c2 = eng.c2_full() if not args.no_c2_full and args.prompt == C2_PROMPT else None
+    other = None
+    if not args.no_other_numerics:
+        try:
+            other = eng.other_numerics(window)
+        except Exception as e:  # reported beside the metric, never required
+            log(f"other-numerics leg failed: {e}")
     counts = [int(x) for x in args.batch_seqs.split(",") if x.strip()]
     batched = None
     if counts:
@@ -406,7 +482,8 @@ def main(argv=None):
         cpu = None
         if n == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(eng.path, args.cpu_sample_tokens, eng.prompt)
+                cpu = cpu_baseline(eng.path, eng.prompt, eng.generated, window,
+                                   min(args.cpu_sample_tokens, window[1] - window[0]))
             except Exception as e:  # the baseline is reported, never required
                 log(f"cpu baseline failed: {e}")
         result = {
@@ -430,6 +507,8 @@ def main(argv=None):
                        "model": args.preset, "prompt_tokens": args.prompt, "timed_window": list(window),
                        "parallelism": f"replicas x{n} (RCCL weight fan-out)", "global_batch": n},
             "c2_full": c2,
+            "numerics": args.numerics,
+            "other_numerics": other,
             "roofline": {"bound": "hbm", "kernel": f"k_matvec (ffn_gate+ffn_up {eng.gate_type} + SwiGLU)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,

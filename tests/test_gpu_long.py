@@ -34,10 +34,10 @@ import pyoracle as po
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_run(path, prompt, n_ctx, n_gen):
+def _oracle_run(path, prompt, n_ctx, n_gen, x86=0):
     """Oracle logits after the prompt (batched or_prefill for all but the last token)
-    and for n_gen greedy steps after it."""
-    om = po.OracleModel(path, n_ctx=n_ctx)
+    and for n_gen greedy steps after it (x86: the oracle's association flags)."""
+    om = po.OracleModel(path, n_ctx=n_ctx, x86=x86)
     if len(prompt) > 1:
         om.prefill(prompt[:-1])
     lo = om.decode(prompt[-1], len(prompt) - 1)
@@ -72,11 +72,13 @@ def _assert_same(got, want):
 
 
 # ---- C1: TinyLlama through the HTTP front end ---------------------------------------
-def test_tinyllama_http_greedy16_vs_oracle(gpu, synth_dir):
+@pytest.mark.parametrize("numerics", ["generic", "x86"])
+def test_tinyllama_http_greedy16_vs_oracle(gpu, synth_dir, numerics):
     """TinyLlama-shaped Q8_0 GGUF (E 2048, 22 layers, V 32000), prompt
     BOS + 16 ids uniform in [3, V) (seed 2), greedy 16 tokens with temperature 0, top_k
     1, repeat_penalty 1.0, ignore_eos, sent as the gateway forwards it (lowercase
-    headers, Bearer key, Connection: close); the ids equal the oracle's greedy ids."""
+    headers, Bearer key, Connection: close); the ids equal the oracle's greedy ids, in
+    both numerics (x86: `llama-server --numerics x86` against the oracle's x86 mode)."""
     from llmi.server import Engine, make_server
 
     path = str(synth_dir / "tinyllama-q8_0-full.gguf")
@@ -84,10 +86,11 @@ def test_tinyllama_http_greedy16_vs_oracle(gpu, synth_dir):
         llmi.write_synthetic_gguf(path, "tinyllama-q8_0", seed=1)
     rng = np.random.default_rng(2)
     prompt = [1] + [int(t) for t in rng.integers(3, 32000, 16)]
-    want_logits = _oracle_run(path, prompt, 64, 15)
+    x86 = numerics == "x86"
+    want_logits = _oracle_run(path, prompt, 64, 15, x86=po.X86_ALL if x86 else 0)
     want = [int(np.argmax(lo)) for lo in want_logits]
 
-    eng = Engine(path, 64, 99, [0])
+    eng = Engine(path, 64, 99, [0], numerics=llmi.NUMERICS_X86 if x86 else llmi.NUMERICS_GENERIC)
     eng.load()
     assert eng.ready, eng.error
     srv = make_server(eng, "127.0.0.1", 0, "k-test")
