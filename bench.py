@@ -61,6 +61,7 @@ def parse(argv=None):
     ap.add_argument("--no-c2-full", action="store_true", help="skip the full-trajectory (128 -> 640) timing")
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r04"),
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
+    ap.add_argument("--experiment", action="store_true", help="allow LLMI_EXP_* knobs (line marked as an experiment)")
     ap.add_argument("--numerics", choices=("generic", "x86"), default="generic",
                     help="fp32 association of every kernel (DESIGN.md §5): ggml's generic order, or upstream's "
                          "x86 AVX2 build (the reference's NGL=0 path)")
@@ -258,13 +259,16 @@ class LlmiEngine:
         nxt = toks[-1] if toks else first
         self.sync()
         t0 = time.perf_counter()
-        ctx.generate_greedy(nxt, window[0], window[1] - window[0])
+        gen = ctx.generate_greedy(nxt, window[0], window[1] - window[0])
         self.sync()
         dt = time.perf_counter() - t0
         k = window[1] - window[0]
         out = {"numerics": "x86" if num == llmi.NUMERICS_X86 else "generic", "tok_s": round(k / dt, 2),
                "ms_per_step": round(dt / k * 1e3, 4), "timed_window": list(window),
                "prefill_path": "mfma" if m.prefill_supported else "decode-steps"}
+        if self.args.profile_steps > 0 and len(gen):
+            prof = ctx.profile_kernels(int(gen[-1]), window[1], self.args.profile_steps)
+            out["kernels"] = {k2: {"us": round(v["us"], 3), "per_step": v["launches_per_step"]} for k2, v in prof.items()}
         if self.args.prompt == C2_PROMPT and not self.args.no_c2_full:
             ctx.kv_clear()
             assert ctx.decode(self.prompt) == 0
@@ -331,7 +335,23 @@ def host_cpu() -> dict:
                     break
     except OSError:
         pass
-    return {"model": model, "logical_cpus_granted": len(os.sched_getaffinity(0)), "logical_cpus": os.cpu_count()}
+    quota = None  # the cgroup's CPU bandwidth limit (cpu.max "quota period"), in CPUs
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as g:
+                q, per = int(f.read()), int(g.read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return {"model": model, "logical_cpus_granted": len(os.sched_getaffinity(0)), "logical_cpus": os.cpu_count(),
+            "cgroup_cpu_quota": quota, "omp_num_threads": int(omp) if omp.isdigit() else None}
 
 
 def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tuple[int, int], n_tokens: int) -> dict:
@@ -354,7 +374,12 @@ def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tup
     po.prefer_simd()
     cpu = host_cpu()
     phys = po.physical_cores()
-    threads = max(1, min(phys, cpu["logical_cpus_granted"]))
+    # every physical core the process may use: the affinity mask, capped by the cgroup's CPU
+    # quota (a GPU box grants a share of a larger host: its mask lists every CPU)
+    # quota (a GPU box grants a share of a larger host: its mask lists every CPU) and by the
+    # OMP_NUM_THREADS the box sets to that share
+    threads = max(1, min(phys, cpu["logical_cpus_granted"], cpu["cgroup_cpu_quota"] or 1 << 30,
+                         cpu["omp_num_threads"] or 1 << 30))
     fast = po.set_fast_dots(True)
     ctx_toks = (prompt + list(generated))[: window[0]]
     om = po.OracleModel(path, n_ctx=window[0] + n_tokens + 8, threads=threads)
@@ -399,16 +424,19 @@ def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tup
                       f"window, after the same {len(prompt)}-token prompt and the GPU's generated tokens (KV rows "
                       f"filled by {len(ctx_toks) - 1} decode steps in {fill_s:.1f}s, untimed) on {os.path.basename(path)}; "
                       f"oracle/ggml_oracle.c -O3 -march=x86-64-v3 with AVX2 dots, OpenMP {threads} threads "
-                      f"(every physical core granted; {cpu['logical_cpus_granted']} logical CPUs, {cpu['model']}) "
+                      f"(every core granted: {cpu['logical_cpus_granted']} logical CPUs in the mask, cgroup quota "
+                      f"{cpu['cgroup_cpu_quota']} CPUs, OMP_NUM_THREADS {cpu['omp_num_threads']}, {phys} physical "
+                      f"cores; {cpu['model']}) "
                       f"and 8 threads (the reference's documented CPU config)"}
 
 
-def env_knobs() -> dict:
+def env_knobs(allow_exp: bool = False) -> dict:
     """Every LLMI_* variable in the environment (recorded in the line); experiment-build
-    knobs are refused: they remove or reorder work inside the timed region."""
+    knobs are refused (they remove or reorder work inside the timed region) unless
+    --experiment marks the line as an experiment's, never a result."""
     knobs = {k: v for k, v in os.environ.items() if k.startswith("LLMI_")}
     bad = [k for k in knobs if k.startswith("LLMI_EXP_")]
-    if bad:
+    if bad and not allow_exp:
         raise SystemExit(f"bench.py: refusing to run with experiment knobs set: {bad}")
     return knobs
 
@@ -443,7 +471,7 @@ def main(argv=None):
         import faulthandler
         faulthandler.enable(all_threads=True)
     args = parse(argv)
-    knobs = env_knobs()
+    knobs = env_knobs(args.experiment)
     dist = Dist(os.environ.get("LLMI_DIST_BACKEND", "nccl"))
     if dist.world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={dist.world}; using WORLD_SIZE")
@@ -542,6 +570,8 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "env": knobs,
             "eager": bool(args.eager),
+            **({"experiment": "LLMI_EXP_* knobs set: timing of an experiment build, not a result"}
+               if args.experiment else {}),
         }
         print(json.dumps(result), flush=True)
     dist.close()

@@ -17,8 +17,11 @@
 // The fp32 chains are exact sequences (one lane per chain); only the double sum of chunk
 // sums is reordered (a lane tree, absorbed by double as on every other path).
 //
-//   decode:  k_a86_scores (KV group x 64-position tile) -> k_a86_softmax (one workgroup
-//            per head, p in place of the scores) -> k_a86_pv (KV group x 16 dims)
+//   decode:  k_a86_d, one launch up to kA86MaxKV positions: (KV group, 16-dim slice) per
+//            workgroup, every workgroup of a group takes the group's scores and softmax
+//            (LDS) and its slice of PV; beyond: k_a86_scores (KV group x 64-position tile)
+//            -> k_a86_softmax (one workgroup per head, p in place of the scores) -> k_a86_pv
+//            (KV group x 16 dims)
 //   prefill: k_pf_a86 (KV group x query token), scores and p in LDS
 #include "kernels.h"
 #include "launch_util.h"
@@ -150,19 +153,139 @@ __global__ __launch_bounds__(512) void k_a86_pv(AttnArgs a) {
     }
 }
 
+// One launch: workgroup (KV group g, slice of DS dims), 1024 threads.  The V slice is
+// loaded first (registers, then LDS: it does not depend on the scores); the scores take
+// one position per 32-lane half-wave, lane c running chain c over elements c, c + 32, ...
+// of the f16 dot (the 4 x 8-lane association; x86_f16dot_reduce_lanes); max, chunk sums
+// and p as k_a86_softmax; PV per (dim, head) job of a half-wave, lane c = chain c over
+// positions c, c + 32, ... < np.  Blocks g + hk * slice: with hk = 8 a group's slices
+// share an XCD (its K read once into that L2).
+constexpr int kA86MaxKV = 2048, kA86Threads = 1024, kA86DS = 16;
+template <int D, int G, int DS>
+__global__ __launch_bounds__(kA86Threads) void k_a86_d(AttnArgs a, int hk, int kvb) {
+    constexpr int NT = kA86Threads, NW = NT / 64, NE = D / 32, VP = DS * kA86MaxKV / 8 / NT;
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    float* qs = (float*)sm;                                   // [G][D]
+    float* wl = qs + G * D;                                   // [G][kvb]: scores, then p
+    uint16_t* vs = (uint16_t*)(wl + (size_t)G * kvb);         // [DS][kvb]
+    __shared__ float redm[NW][G];
+    __shared__ double reds[NW][G];
+    const int g = blockIdx.x % hk, d0 = (blockIdx.x / hk) * DS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane & 31, half = lane >> 5;
+    const int n_kv = a.st->pos + 1, np = (n_kv + 31) & ~31;
+    // V slice rows [d0, d0 + DS) x positions [0, np): 16-B pieces into registers
+    const int prow = np >> 3;
+    const uint16_t* vb = a.vc + ((size_t)g * D + d0) * a.n_ctx;
+    u32x4 vr[VP];
+#pragma unroll
+    for (int k = 0; k < VP; ++k) {
+        const int i = tid + k * NT;
+        if (i < DS * prow) vr[k] = *(const u32x4*)(vb + (size_t)(i / prow) * a.n_ctx + (i % prow) * 8);
+    }
+    for (int i = tid; i < G * D; i += NT) qs[i] = h2f(f2h(a.q[(size_t)g * G * D + i]));
+    __syncthreads();
+    float qv[G][NE];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) qv[hh][e] = qs[hh * D + c + 32 * e];
+    // scores: U position pairs of a wave in flight
+    constexpr int U = 4;
+    const uint16_t* kg = a.kc + (size_t)g * a.n_ctx * D + c;
+    for (int base = 2 * wave; base < n_kv; base += 2 * NW * U) {
+        uint16_t kk[U][NE];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = min(base + 2 * NW * u + half, n_kv - 1);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) kk[u][e] = kg[(size_t)t * D + 32 * e];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = base + 2 * NW * u + half;
+#pragma unroll
+            for (int hh = 0; hh < G; ++hh) {
+                float acc = 0.f;
+#pragma unroll
+                for (int e = 0; e < NE; ++e) acc = __builtin_fmaf(h2f(kk[u][e]), qv[hh][e], acc);
+                const float w = x86_f16dot_reduce_lanes(acc) * a.scale;
+                if (c == 0 && t < n_kv) wl[hh * kvb + t] = w;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < VP; ++k) {
+        const int i = tid + k * NT;
+        if (i < DS * prow) *(u32x4*)(vs + (size_t)(i / prow) * kvb + (i % prow) * 8) = vr[k];
+    }
+    __syncthreads();
+    float mx[G];
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        float m = -INFINITY;
+        for (int t = tid; t < n_kv; t += NT) m = fmaxf(m, wl[hh * kvb + t]);
+        m = wave_max(m);
+        if (lane == 0) redm[wave][hh] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        float m = redm[0][hh];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) m = fmaxf(m, redm[w][hh]);
+        mx[hh] = m;
+        double sum = 0.0;
+        for (int c8 = tid; 8 * c8 < n_kv; c8 += NT) {
+            float e[8];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) e[l] = 8 * c8 + l < n_kv ? x86_v_expf(wl[hh * kvb + 8 * c8 + l] - m) : 0.f;
+            sum += (double)x86_hsum8(e);
+        }
+        sum = wave_sum_d(sum);
+        if (lane == 0) reds[wave][hh] = sum;
+    }
+    __syncthreads();  // also: every score read before any p replaces it
+#pragma unroll
+    for (int hh = 0; hh < G; ++hh) {
+        double sum = 0.0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) sum += reds[w][hh];
+        const float inv = (float)(1.0 / sum);
+        for (int t = tid; t < np; t += NT)
+            wl[hh * kvb + t] = t < n_kv ? h2f(f2h(x86_v_expf(wl[hh * kvb + t] - mx[hh]) * inv)) : 0.f;
+    }
+    __syncthreads();
+    for (int j = tid >> 5; j < DS * G; j += NT / 32) {
+        const int dl = j % DS, hh = j / DS;
+        float acc = 0.f;
+        for (int q = c; q < np; q += 32) {
+            const float v = q < n_kv ? h2f(vs[dl * kvb + q]) : 0.f;
+            acc = __builtin_fmaf(v, wl[hh * kvb + q], acc);
+        }
+        const float r = x86_f16dot_reduce_lanes(acc);
+        if (c == 0) a.out[(size_t)(g * G + hh) * D + d0 + dl] = r;
+    }
+}
+
 template <int D, int G>
-static hipError_t a86_launch(const AttnArgs& a, int n_head, int hk, int kv_bound, hipStream_t s) {
+static hipError_t a86_launch(const AttnArgs& a, int n_head, int hk, int kv_bound, hipStream_t s, int mode) {
+    if (mode != 3 && kv_bound <= kA86MaxKV) {
+        const size_t lds = (size_t)G * D * 4 + (size_t)G * kv_bound * 4 + (size_t)kA86DS * kv_bound * 2;
+        launch_k(k_a86_d<D, G, kA86DS>, dim3(hk * (D / kA86DS)), dim3(kA86Threads), lds, s, true, true, a, hk, kv_bound);
+        return hipGetLastError();
+    }
     launch_k(k_a86_scores<D, G>, dim3(hk, (kv_bound + 63) / 64), dim3(256), 0, s, true, false, a);
     launch_k(k_a86_softmax, dim3(n_head), dim3(256), 0, s, false, false, a);
     launch_k(k_a86_pv<D, G>, dim3(hk, D / 16), dim3(512), 0, s, false, true, a);
     return hipGetLastError();
 }
 
-hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
+hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s,
+                                int mode) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
     const int g = n_head / n_head_kv;
 #define LLMI_A86(D_, G_) \
-    if (head_dim == D_ && g == G_) return a86_launch<D_, G_>(a, n_head, n_head_kv, kv_bound, s);
+    if (head_dim == D_ && g == G_) return a86_launch<D_, G_>(a, n_head, n_head_kv, kv_bound, s, mode);
     LLMI_A86(128, 1) LLMI_A86(128, 2) LLMI_A86(128, 4) LLMI_A86(128, 8)
     LLMI_A86(64, 1) LLMI_A86(64, 2) LLMI_A86(64, 4) LLMI_A86(64, 8)
 #undef LLMI_A86

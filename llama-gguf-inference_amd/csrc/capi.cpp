@@ -1397,11 +1397,9 @@ int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int3
     a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
     a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);
     a.num = t_hook_numerics;
-    set_attn_mode(mode);
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
-    hipError_t e = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, nullptr);
+    hipError_t e = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, nullptr, mode);
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    set_attn_mode(0);
     (void)hipFree(scores);
     (void)hipFree(st);
     if (e != hipSuccess) { set_err(std::string("llmi_attention: ") + hip_err(e)); return -3; }
@@ -1431,18 +1429,13 @@ double llmi_pf_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, in
         if (hipMalloc(&wsc, bytes) != hipSuccess) { set_err("llmi_pf_attention: out of device memory"); return -2; }
         at.wsc = wsc; at.wsc_bytes = bytes;
     }
-    const int fa_old = g_pf_attn_fa, simple_old = g_pf_attn_simple;
-    g_pf_attn_fa = mode == 0;
-    g_pf_attn_simple = mode == 2;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, nullptr);
-    hipError_t e = launch_pf_attn(at, n_head, head_dim, T, nullptr);
+    hipError_t e = launch_pf_attn(at, n_head, head_dim, T, nullptr, mode);
     (void)hipEventRecord(e1, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    g_pf_attn_fa = fa_old;
-    g_pf_attn_simple = simple_old;
     float ms = 0.f;
     if (e == hipSuccess) (void)hipEventElapsedTime(&ms, e0, e1);
     (void)hipEventDestroy(e0);
@@ -1483,7 +1476,6 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     hs.pos = n_kv - 1;
     hs.pos_next = n_kv;
     (void)hipMemcpy(st, &hs, sizeof(hs), hipMemcpyHostToDevice);
-    set_attn_mode(mode);
     hipStream_t s = nullptr;
     (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
@@ -1498,16 +1490,15 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
             a.kc = kc + (size_t)l * kv_layer;
             a.vc = vc + (size_t)l * kv_layer;
             a.layer = l % 255;
-            (void)launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s);
+            (void)launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s, mode);
         }
         a.kc = kc + (size_t)(nl - 1) * kv_layer;
         a.vc = vc + (size_t)(nl - 1) * kv_layer;
         a.layer = (nl - 1) % 255;
         a.trace = (unsigned long long*)trace_dev;
-        const bool okt = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s) == hipSuccess &&
+        const bool okt = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s, mode) == hipSuccess &&
                          hipStreamSynchronize(s) == hipSuccess;
         (void)hipStreamDestroy(s);
-        set_attn_mode(0);
         cleanup();
         return okt ? 0.0 : -1.0;
     }
@@ -1520,7 +1511,7 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
         a.kc = kc + (size_t)l * kv_layer;
         a.vc = vc + (size_t)l * kv_layer;
         a.layer = l % 255;
-        ok = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s) == hipSuccess;
+        ok = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, s, mode) == hipSuccess;
     }
     ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
     double res = -1.0;
@@ -1543,7 +1534,6 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     if (ex) (void)hipGraphExecDestroy(ex);
     if (g) (void)hipGraphDestroy(g);
     (void)hipStreamDestroy(s);
-    set_attn_mode(0);
     cleanup();
     return res;
 }

@@ -551,6 +551,21 @@ Seg seg_of(const Model& m, const DevMat& d, int row0) {
 namespace {
 }  // namespace
 
+#if defined(LLMI_EXPERIMENTS)
+// LLMI_EXP_XQ (step_enqueue): a zero q8 image, allocated before any capture
+static const int exp_xq = [] {
+    const char* e = getenv("LLMI_EXP_XQ");
+    return e ? atoi(e) : 0;
+}();
+static uint8_t* g_exp_img = nullptr;
+static bool exp_prepare(const Model& m) {
+    if (!exp_xq || g_exp_img) return true;
+    const size_t nb = (size_t)(std::max<int64_t>(m.hp.n_ff, m.hp.n_vocab > 0 ? m.hp.n_embd * 2 : 0) / 256 + 1) * 304;
+    return hipMalloc(&g_exp_img, nb) == hipSuccess && hipMemset(g_exp_img, 0, nb) == hipSuccess &&
+           hipDeviceSynchronize() == hipSuccess;
+}
+#endif
+
 bool step_enqueue(Context& c, int kv_bound, std::string& err) {
     const Model& m = *c.m;
     const HParams& hp = m.hp;
@@ -573,8 +588,13 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         const char* e = getenv("LLMI_EXP_XFIRST");
         return e ? atoi(e) : 0;
     }();
+    // LLMI_EXP_XQ = bitmask (1 QKV, 2 attn_output, 4 gate+up, 8 down, 16 output) of launches
+    // fed a zero q8 image instead of their prologue: the upper bound of a free image
+    if (exp_xq && !g_exp_img) { err = "exp_img not allocated"; return false; }
+    auto xq_for = [&](int bit) -> const uint8_t* { return (exp_xq >> bit & 1) ? g_exp_img : nullptr; };
 #else
     constexpr int exp_skip = 0, exp_xfirst = 0;
+    auto xq_for = [](int) -> const uint8_t* { return nullptr; };
 #endif
     auto want = [P](int k) { return !(exp_skip >> k & 1) && (!P || P->want(k)); };
     // a filtered launch, armed with an event pair when the profiler asks for timing
@@ -599,7 +619,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         const Layer& L = m.layers[(size_t)l];
         // --- QKV + RoPE + KV write (grouped by activation kind) ---
         const int num = m.numerics;
-        MVArgs a; a.xfirst = exp_xfirst >> 0 & 1; a.num = num;
+        MVArgs a; a.xfirst = exp_xfirst >> 0 & 1; a.num = num; a.xq = xq_for(0);
         a.cols = E; a.x = c.x; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps; a.y = c.q;
         a.kc = c.kc + l * kv_layer; a.vc = c.vc + l * kv_layer; a.rope = c.rope; a.st = c.st;
         a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = nq; a.nk = nk;
@@ -634,25 +654,25 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         LLMI_RUN(K_ATTN, launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---
-        MVArgs o; o.xfirst = exp_xfirst >> 1 & 1; o.num = num;
+        MVArgs o; o.xfirst = exp_xfirst >> 1 & 1; o.num = num; o.xq = xq_for(1);
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
         LLMI_RUN(K_ATTN_OUT, launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
         if (P) P->add(K_ATTN_OUT, (double)L.wo.bytes + 4.0 * nq + 8.0 * E);
         // --- gate/up + SwiGLU ---
-        MVArgs gu; gu.xfirst = exp_xfirst >> 2 & 1; gu.num = num;
+        MVArgs gu; gu.xfirst = exp_xfirst >> 2 & 1; gu.num = num; gu.xq = xq_for(2);
         gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2;
         gu.cols = E; gu.x = c.x; gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps;
         gu.y = c.h; gu.npairs = hp.n_ff;
         LLMI_RUN(K_FFN_GATE_UP, launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
         if (P) P->add(K_FFN_GATE_UP, (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff);
         // --- down + residual ---
-        MVArgs dn; dn.xfirst = exp_xfirst >> 3 & 1; dn.num = num;
+        MVArgs dn; dn.xfirst = exp_xfirst >> 3 & 1; dn.num = num; dn.xq = xq_for(3);
         dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
         LLMI_RUN(K_FFN_DOWN, launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
         if (P) P->add(K_FFN_DOWN, (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E);
     }
     MVArgs lo;
-    lo.num = m.numerics;
+    lo.num = m.numerics; lo.xq = xq_for(4);
     lo.seg[0] = seg_of(m, m.output, 0); lo.nseg = 1; lo.cols = E; lo.x = c.x;
     lo.nw = (const float*)(m.arena + m.out_norm.off_a); lo.eps = hp.eps; lo.y = c.logits;
     lo.npairs = (hp.n_vocab + 1) / 2; lo.argmax = &c.st->key[0][0]; lo.st = c.st;
@@ -663,6 +683,9 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
 }
 
 bool step_run(Context& c, int pos, std::string& err) {
+#if defined(LLMI_EXPERIMENTS)
+    if (!exp_prepare(*c.m)) { err = "exp_img"; return false; }
+#endif
     const int bucket = pos / 256;
     const int kv_bound = std::min(c.n_ctx, (bucket + 1) * 256);
     if (!c.use_graphs) return step_enqueue(c, kv_bound, err);

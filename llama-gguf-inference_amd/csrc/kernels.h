@@ -192,7 +192,11 @@ hipError_t launch_pf_embed(const Seg& w, int cols, int vocab, const int32_t* tok
 hipError_t launch_pf_quant(const float* x, int ldx, const float* nw, float eps, int cols, int act, int T, void* aq,
                            int16_t* abs, float* ad, void* abf, hipStream_t s, int x86 = 0);
 hipError_t launch_pf_gemm(const PfGemm& g, int epi, hipStream_t s);
-hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipStream_t s);
+// path: -1 the process setting (pf_attn_fa / pf_attn_simple test options), 0 the tiled
+// FP64-MFMA kernel only (hipErrorNotSupported when it does not apply or the scratch is
+// short: never a silent fallback), 1 the LDS kernels (grouped, then one head per
+// workgroup), 2 one head per workgroup
+hipError_t launch_pf_attn(const PfAttn& a, int n_head, int head_dim, int T, hipStream_t s, int path = -1);
 
 // activation kind of a weight type: 0 = block_q8_K (K-quants), 1 = block_q8_0
 __host__ __device__ inline int act_kind(int t) { return t == T_Q8_0 ? 1 : 0; }
@@ -211,12 +215,15 @@ hipError_t launch_matvec(const MVArgs& a, int epi, int max_blocks, hipStream_t s
 // attention path for a KV bound: 1 fused (one WG per head), 2 split (scores + PV over
 // (group, 16-dim slice) workgroups), 3 two-kernel long-context path, 4 one-launch
 // exchange (k_attn_x: scores tiles + granule hand-off + PV, kv_bound <= kXAttnMaxKV)
-int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim);
+// mode: -1 the process setting (set_attn_mode, LLMI_ATTN_MODE at model load), 0 auto,
+// 1..7 one path (A/B and test hooks; a path whose limits the shape passes falls back)
+int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim, int mode = -1);
 int attn_d_slices(int n_head, int head_dim);
 // arm (or with nullptrs disarm) per-op kernel timing events for this thread's launches
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);
-hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream);
+hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream,
+                            int mode = -1);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);
 // the last step's embedding row again (debug tap 0)
 hipError_t launch_embed_row(const EmbArgs& a, const StepState* st, float* out, hipStream_t stream);
@@ -224,7 +231,9 @@ hipError_t launch_repack(int type, const void* raw, uint8_t* a, uint8_t* h, uint
                          int x86, hipStream_t stream);
 // x86 numerics attention (attn86.hip): upstream's non-flash CPU attention in its x86 AVX2
 // association (f16 dots in 4 x 8 fp32 fma lanes, ggml_v_expf softmax with per-8 sums)
-hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s);
+// mode 3: the three-launch path at every context (tests); else one launch up to 2048 positions
+hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s,
+                                int mode = 0);
 hipError_t launch_pf_attn_x86(const PfAttn& a, int n_head, int n_head_kv, int head_dim, int T, hipStream_t s);
 int pf_attn_x86_max_kv(int n_head, int n_head_kv, int head_dim);
 // writes the prologue's quantized activation in ggml block form (test hook)

@@ -1178,18 +1178,19 @@ void set_attn_mode(int mode) {
     const char* r = getenv("LLMI_ATTN_ROT");  // rotated K pass order (bit 1 of the word; default on)
     if (!r || atoi(r)) g_attn_pf |= 2;
 }
-int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
+int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim, int mode) {
     const int g = n_head / n_head_kv;
+    const int m = mode < 0 ? g_attn_mode : mode;
     const bool split_ok = (size_t)g * kv_bound * 4 <= kSplitAttnMaxLds;
     const bool fused_ok = kv_bound <= kFusedAttnMaxKV;
     (void)n_head;
-    if (g_attn_mode == 4 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
-    if (g_attn_mode == 5 && kv_bound <= kRegAttnMaxKV) return 5;
-    if (g_attn_mode == 6 && kv_bound <= kDimAttnMaxKV) return 6;
-    if (g_attn_mode == 7 && g <= 8) return 7;
-    if (g_attn_mode == 1 && fused_ok) return 1;
-    if (g_attn_mode == 2 && split_ok) return 2;
-    if (g_attn_mode == 3) return 3;
+    if (m == 4 && g <= 8 && kv_bound <= kXAttnMaxKV) return 4;
+    if (m == 5 && kv_bound <= kRegAttnMaxKV) return 5;
+    if (m == 6 && kv_bound <= kDimAttnMaxKV) return 6;
+    if (m == 7 && g <= 8) return 7;
+    if (m == 1 && fused_ok) return 1;
+    if (m == 2 && split_ok) return 2;
+    if (m == 3) return 3;
     // auto, from the crossovers measured by tools/attnbench.py (graph-free launches, us;
     // profiles/r01/attn_modes.md):
     //   G=4, D=128 (8B, Mistral): fused <= 256 (8.1 vs 8.4 exchange), exchange <= 512,
@@ -1203,7 +1204,7 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     //   G=4 D=128 128: 5.2 vs 8.1 fused, 512: 7.0 vs 10.0 exchange, 1024: 10.8 vs 12.7 split
     //   long-context four-launch path 7 (profiles/r02/attn_long.md): G=4 D=128 beyond 2048
     //   (4096: 25.4 vs 31.2 split, 16384: 62 vs 628 two-kernel), G=8 beyond 1024
-    if (g_attn_mode == 0) {
+    if (m == 0) {
         if (g <= 8 && kv_bound <= kDimAttnMaxKV && attn_d_slices(n_head, head_dim) >= 2) return 6;
         if (g == 8 && kv_bound > 1024) return 7;
         if (g <= 4 && kv_bound > 2048) return 7;
@@ -1216,16 +1217,17 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim) {
     return split_ok ? 2 : fused_ok ? 1 : 3;
 }
 
-hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
+hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s,
+                            int mode) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
-    if (a0.num) return launch_attention_x86(a0, n_head, n_head_kv, head_dim, kv_bound, s);
+    if (a0.num) return launch_attention_x86(a0, n_head, n_head_kv, head_dim, kv_bound, s, mode < 0 ? g_attn_mode : mode);
     AttnArgs a = a0;
     a.spin_limit = g_xspin_limit;
     a.tag_skew = g_xtag_skew;
     const int g = n_head / n_head_kv;
-    int path = attn_path(n_head, n_head_kv, kv_bound, head_dim);
+    int path = attn_path(n_head, n_head_kv, kv_bound, head_dim, mode);
     if (path == 4 && (!a.gran || !a.fault || a.layer < 0 || a.layer > 254))
-        path = attn_path(n_head, n_head_kv, kXAttnMaxKV + 256, head_dim);
+        path = attn_path(n_head, n_head_kv, kXAttnMaxKV + 256, head_dim, mode);
     if (path == 5) {
         const int p = kv_bound <= 64 ? 1 : kv_bound <= 128 ? 2 : kv_bound <= 256 ? 4 : 8;
 #define LLMI_ATTR(D_, P_) \

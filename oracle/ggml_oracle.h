@@ -46,9 +46,21 @@ float or_vec_dot(int wtype, int n, const void* wrow, const void* act);
 /* CPU baseline timing only: AVX2 dots in the x86 kernels' association (not the
  * generic order; never used by a parity check).  Returns 0 if this build has no AVX2. */
 int or_set_fast_dots(int on);
-/* Parity measurement only (never a check): switch the dots, q8_0 quantization, f16 attention
- * dots and exp onto upstream's x86 AVX2 association (flags in ggml_oracle.c: 1 dots, 2 q8_0,
- * 4 f16 dots, 8 ggml_v_expf, 16 libm expf, 32 no FMA contraction).  0 = generic (default). */
+/* Switch the dots, q8_0 quantization, f16 attention dots and exp onto upstream's x86
+ * association (flags in ggml_oracle.c: 1 dots, 2 q8_0, 4 f16 dots, 8 ggml_v_expf, 16 libm
+ * expf, 32 no FMA contraction).  0 = generic (default).  X86_ALL = 1|2|4|8 is the checker
+ * of the GPU's x86 numerics mode (LLMI_NUMERICS_X86).  Which upstream CPU build it models:
+ *   - the AVX2+FMA+F16C ("haswell") variant of ggml-cpu's x86 kernels (arch/x86/quants.c,
+ *     vec.h/vec.cpp, simd-mappings.h).  A GGML_CPU_ALL_VARIANTS image picks its variant per
+ *     host at run time: on an AVX-512 host the avx512/icelake/sapphirerapids variant runs,
+ *     whose K-quant dots associate in 16-lane registers -- not modelled (unpinned);
+ *   - llm_build_llama's non-flash attention: KQ = mul_mat(K f16, Q -> f16) per head with
+ *     ggml_vec_dot_f16, soft_max_ext, KQV = mul_mat(V^T f16, softmax -> f16).  The
+ *     reference's start.sh passes no --flash-attn flag, so a 2026 llama-server runs its
+ *     default "-fa auto", which on CPU selects ggml_compute_forward_flash_attn_ext (online
+ *     softmax, f16 V accumulation) -- a different association, not modelled (unpinned);
+ *   - plain row-major weight dots: the CPU_REPACK buffer type (q4_K interleaved 8x8 GEMV,
+ *     default on AVX2 builds) associates per 8 rows differently -- not modelled (unpinned). */
 int or_set_x86_mode(int flags);
 /* the activation conversion or_matvec applies to x for weight type wtype (current mode) */
 int or_quantize_act(int wtype, const float* x, void* out, int64_t cols);

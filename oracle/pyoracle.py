@@ -221,8 +221,8 @@ class OracleModel:
     def decode(self, token: int, pos: int, logits: bool = True) -> np.ndarray | None:
         """One decode step; logits=False skips the output head (prompt tokens)."""
         out = np.empty(self.n_vocab, dtype=np.float32) if logits else None
-        lib().or_set_x86_mode(self.x86)
-        rc = lib().or_decode(self._h, int(token), int(pos), _p(out) if logits else None, self.threads)
+        with x86_mode(self.x86):  # the mode is process-global: restored after the call
+            rc = lib().or_decode(self._h, int(token), int(pos), _p(out) if logits else None, self.threads)
         if rc != 0:
             raise RuntimeError(f"or_decode rc={rc}: " + lib().or_last_error().decode())
         return out
@@ -231,8 +231,8 @@ class OracleModel:
         """T decode steps at pos0.. with no logits (or_prefill: the same operations per
         token, loops reordered so each weight row is unpacked once)."""
         toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
-        lib().or_set_x86_mode(self.x86)
-        rc = lib().or_prefill(self._h, _p(toks), int(toks.size), int(pos0), self.threads)
+        with x86_mode(self.x86):
+            rc = lib().or_prefill(self._h, _p(toks), int(toks.size), int(pos0), self.threads)
         if rc != 0:
             raise RuntimeError(f"or_prefill rc={rc}: " + lib().or_last_error().decode())
 

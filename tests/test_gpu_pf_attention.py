@@ -159,6 +159,24 @@ def test_pf_attention_chunked_scratch(gpu):
     _assert_same(whole, want, "one launch")
 
 
+def test_pf_attention_tiled_mode_never_falls_back(gpu):
+    """Mode 0 asks for k_pf_fa alone: a scratch shorter than one query tile is an error,
+    not a silent run of the LDS kernels."""
+    import torch
+
+    H, HK, D, T, pos0 = 32, 8, 128, 48, 900
+    q, K, V, n_ctx, G = _case(H, HK, D, T, pos0, seed=6)
+    ldw = (pos0 + T + 63) // 64 * 64
+    out = torch.zeros(T * H * D, dtype=torch.float32, device="cuda")
+    from helpers import to_dev
+    qd = to_dev(np.ascontiguousarray(q.reshape(-1)))
+    kd = to_dev(K.view(np.uint16).reshape(-1))
+    vd = to_dev(V.view(np.uint16).reshape(-1))
+    rc = llmi.lib().llmi_pf_attention(H, HK, D, T, pos0, n_ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(),
+                                      out.data_ptr(), 0, HK * 64 * ldw * 4 // 2)
+    assert rc < 0 and "not supported" in llmi.last_error().lower()
+
+
 def test_pf_attention_rejects_bad_shapes(gpu):
     L = llmi.lib()
     assert L.llmi_pf_attention(32, 8, 96, 16, 0, 256, 1, 1, 1, 1, 0, 0) < 0   # head_dim

@@ -182,8 +182,10 @@ def _ref_attention_x86(q, K, V, n_kv, G, scale):
 
 
 @pytest.mark.parametrize("H,HK,D,n_kv", [(32, 8, 128, 1), (32, 8, 128, 200), (32, 8, 128, 700),
-                                         (64, 8, 128, 333), (32, 4, 64, 300), (32, 4, 64, 2100)])
-def test_x86_attention_vs_numpy(gpu, H, HK, D, n_kv):
+                                         (64, 8, 128, 333), (32, 4, 64, 300), (32, 4, 64, 2100),
+                                         (32, 8, 128, 2048), (8, 8, 64, 97), (16, 8, 128, 1500)])
+@pytest.mark.parametrize("mode", [0, 3])  # 0: one launch (k_a86_d) up to 2048 positions, 3: three launches
+def test_x86_attention_vs_numpy(gpu, H, HK, D, n_kv, mode):
     import torch
 
     rng = np.random.default_rng(77 + n_kv)
@@ -198,7 +200,7 @@ def test_x86_attention_vs_numpy(gpu, H, HK, D, n_kv):
     qd, kd, vd = to_dev(q.reshape(-1)), to_dev(K.view(np.uint16).reshape(-1)), to_dev(V.view(np.uint16).reshape(-1))
     with numerics():
         rc = llmi.lib().llmi_attention(H, HK, D, n_kv, n_ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(),
-                                       out.data_ptr(), 0)
+                                       out.data_ptr(), mode)
     assert rc == 0, llmi.last_error()
     got = out.cpu().numpy().reshape(H, D)
     want = _ref_attention_x86(q, K, V, n_kv, G, 1.0 / np.sqrt(np.float32(D)))
