@@ -17,8 +17,8 @@
 // The fp32 chains are exact sequences (one lane per chain); only the double sum of chunk
 // sums is reordered (a lane tree, absorbed by double as on every other path).
 //
-//   decode:  k_a86_d, one launch up to kA86MaxKV positions: (KV group, 16-dim slice) per
-//            workgroup, every workgroup of a group takes the group's scores and softmax
+//   decode:  k_a86_h, one launch up to kA86MaxKV positions: (head, 16-dim slice) per
+//            workgroup, every workgroup of a head takes the head's scores and softmax
 //            (LDS) and its slice of PV; beyond: k_a86_scores (KV group x 64-position tile)
 //            -> k_a86_softmax (one workgroup per head, p in place of the scores) -> k_a86_pv
 //            (KV group x 16 dims)
@@ -153,27 +153,44 @@ __global__ __launch_bounds__(512) void k_a86_pv(AttnArgs a) {
     }
 }
 
-// One launch: workgroup (KV group g, slice of DS dims), 1024 threads.  The V slice is
-// loaded first (registers, then LDS: it does not depend on the scores); the scores take
-// one position per 32-lane half-wave, lane c running chain c over elements c, c + 32, ...
-// of the f16 dot (the 4 x 8-lane association; x86_f16dot_reduce_lanes); max, chunk sums
-// and p as k_a86_softmax; PV per (dim, head) job of a half-wave, lane c = chain c over
-// positions c, c + 32, ... < np.  Blocks g + hk * slice: with hk = 8 a group's slices
-// share an XCD (its K read once into that L2).
-constexpr int kA86MaxKV = 2048, kA86Threads = 1024, kA86DS = 16;
-template <int D, int G, int DS>
-__global__ __launch_bounds__(kA86Threads) void k_a86_d(AttnArgs a, int hk, int kvb) {
-    constexpr int NT = kA86Threads, NW = NT / 64, NE = D / 32, VP = DS * kA86MaxKV / 8 / NT;
+// One launch: workgroup (head h, slice of DS dims), 512 threads, H x D/DS workgroups.
+// The V slice is loaded first (registers, then LDS: it does not depend on the scores).
+// Scores: a quad of lanes per position, lane q of the quad running the 8 chains
+// 8q .. 8q+7 of the f16 dot (chain c over elements c, c + 32, ...), its 32 q values in
+// registers; the 4 x 8-lane reduction of x86_f16dot_reduce is two quad DPP steps (xor 2:
+// acc[l] + acc[16 + l], xor 1: + (acc[8 + l] + acc[24 + l]) of the partner) and the
+// t0..t3 tree in the lane.  A wave takes 16 positions per pass (4 rows x 64 B per load:
+// coalesced), U such rows per quad loaded at once (one pass covers 128 U positions: U
+// from the KV bucket, at most 8).  Max, chunk sums and p as
+// k_a86_softmax.  PV: 32 lanes per dim, lane c running chain c over positions c, c + 32,
+// ... < np, reduced by x86_f16dot_reduce_lanes.
+constexpr int kA86MaxKV = 2048, kA86Threads = 512;
+__device__ __forceinline__ float a86_quad_reduce(float (&acc)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += xor_partner<2>(acc[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += xor_partner<1>(acc[j]);
+    const float t0 = acc[0] + acc[4], t1 = acc[1] + acc[5], t2 = acc[2] + acc[6], t3 = acc[3] + acc[7];
+    return (t0 + t1) + (t2 + t3);
+}
+#if defined(LLMI_EXP_TRACE)
+#define A86_STAMP(I) if (threadIdx.x == 0 && a.trace) a.trace[blockIdx.x * 8 + (I)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define A86_STAMP(I)
+#endif
+template <int D, int DS, int U>
+__global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, int gq, int kvb, int stop) {
+    constexpr int NT = kA86Threads, NW = NT / 64, VP = DS * kA86MaxKV / 8 / NT, NE = D / 32;
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-    float* qs = (float*)sm;                                   // [G][D]
-    float* wl = qs + G * D;                                   // [G][kvb]: scores, then p
-    uint16_t* vs = (uint16_t*)(wl + (size_t)G * kvb);         // [DS][kvb]
-    __shared__ float redm[NW][G];
-    __shared__ double reds[NW][G];
-    const int g = blockIdx.x % hk, d0 = (blockIdx.x / hk) * DS;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane & 31, half = lane >> 5;
+    const int vst = kvb + 8;                                  // V row stride (f16): rows off one bank quad
+    float* wl = (float*)sm;                                   // [kvb]: scores, then p
+    uint16_t* vs = (uint16_t*)(wl + kvb);                     // [DS][vst]
+    __shared__ float redm[NW];
+    __shared__ double reds[NW];
+    const int h = blockIdx.x % n_head, d0 = (blockIdx.x / n_head) * DS, g = h / gq;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qg = lane & 3;
+    A86_STAMP(0)
     const int n_kv = a.st->pos + 1, np = (n_kv + 31) & ~31;
-    // V slice rows [d0, d0 + DS) x positions [0, np): 16-B pieces into registers
     const int prow = np >> 3;
     const uint16_t* vb = a.vc + ((size_t)g * D + d0) * a.n_ctx;
     u32x4 vr[VP];
@@ -182,96 +199,111 @@ __global__ __launch_bounds__(kA86Threads) void k_a86_d(AttnArgs a, int hk, int k
         const int i = tid + k * NT;
         if (i < DS * prow) vr[k] = *(const u32x4*)(vb + (size_t)(i / prow) * a.n_ctx + (i % prow) * 8);
     }
-    for (int i = tid; i < G * D; i += NT) qs[i] = h2f(f2h(a.q[(size_t)g * G * D + i]));
-    __syncthreads();
-    float qv[G][NE];
+    // this lane's q values: q[8 qg + 32 e + j], f16-rounded
+    float qv[NE][8];
 #pragma unroll
-    for (int hh = 0; hh < G; ++hh)
+    for (int e = 0; e < NE; ++e) {
+        const float4 qa = *(const float4*)(a.q + (size_t)h * D + 8 * qg + 32 * e);
+        const float4 qb = *(const float4*)(a.q + (size_t)h * D + 8 * qg + 32 * e + 4);
+        const float qf[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
-        for (int e = 0; e < NE; ++e) qv[hh][e] = qs[hh * D + c + 32 * e];
-    // scores: U position pairs of a wave in flight
-    constexpr int U = 4;
-    const uint16_t* kg = a.kc + (size_t)g * a.n_ctx * D + c;
-    for (int base = 2 * wave; base < n_kv; base += 2 * NW * U) {
-        uint16_t kk[U][NE];
+        for (int j = 0; j < 8; ++j) qv[e][j] = h2f(f2h(qf[j]));
+    }
+    const uint16_t* K = a.kc + (size_t)g * a.n_ctx * D + 8 * qg;
+    // a pass: U positions per quad, wave w takes positions pass * 128 U + 128 u + 16 w + lane / 4
+    const int pw = wave * 16 + (lane >> 2);
+    A86_STAMP(1)
+    if (stop == 1) return;
+    float m = -INFINITY;
+    for (int t0 = 0; t0 < n_kv; t0 += NW * 16 * U) {
+        u32x4 kr[U][NE];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int t = min(base + 2 * NW * u + half, n_kv - 1);
+            const int t = min(t0 + NW * 16 * u + pw, n_kv - 1);
 #pragma unroll
-            for (int e = 0; e < NE; ++e) kk[u][e] = kg[(size_t)t * D + 32 * e];
+            for (int e = 0; e < NE; ++e) kr[u][e] = *(const u32x4*)(K + (size_t)t * D + 32 * e);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int t = base + 2 * NW * u + half;
+            const int t = t0 + NW * 16 * u + pw;
+            float acc[8];
 #pragma unroll
-            for (int hh = 0; hh < G; ++hh) {
-                float acc = 0.f;
+            for (int j = 0; j < 8; ++j) acc[j] = 0.f;
 #pragma unroll
-                for (int e = 0; e < NE; ++e) acc = __builtin_fmaf(h2f(kk[u][e]), qv[hh][e], acc);
-                const float w = x86_f16dot_reduce_lanes(acc) * a.scale;
-                if (c == 0 && t < n_kv) wl[hh * kvb + t] = w;
+            for (int e = 0; e < NE; ++e)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    acc[j] = __builtin_fmaf(h2f(kr[u][e][j >> 1] >> (16 * (j & 1))), qv[e][j], acc[j]);
+            const float w = a86_quad_reduce(acc) * a.scale;
+            if (t < n_kv) {
+                if (qg == 0) wl[t] = w;
+                m = fmaxf(m, w);
             }
         }
     }
 #pragma unroll
     for (int k = 0; k < VP; ++k) {
         const int i = tid + k * NT;
-        if (i < DS * prow) *(u32x4*)(vs + (size_t)(i / prow) * kvb + (i % prow) * 8) = vr[k];
+        if (i < DS * prow) *(u32x4*)(vs + (size_t)(i / prow) * vst + (i % prow) * 8) = vr[k];
     }
+    m = wave_max(m);
+    if (lane == 0) redm[wave] = m;
     __syncthreads();
-    float mx[G];
+    A86_STAMP(2)
+    if (stop == 2) return;
+    float mx = redm[0];
 #pragma unroll
-    for (int hh = 0; hh < G; ++hh) {
-        float m = -INFINITY;
-        for (int t = tid; t < n_kv; t += NT) m = fmaxf(m, wl[hh * kvb + t]);
-        m = wave_max(m);
-        if (lane == 0) redm[wave][hh] = m;
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redm[w]);
+    double sum = 0.0;
+    for (int c8 = tid; 8 * c8 < n_kv; c8 += NT) {
+        float e[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) e[l] = 8 * c8 + l < n_kv ? x86_v_expf(wl[8 * c8 + l] - mx) : 0.f;
+        sum += (double)x86_hsum8(e);
     }
-    __syncthreads();
-#pragma unroll
-    for (int hh = 0; hh < G; ++hh) {
-        float m = redm[0][hh];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) m = fmaxf(m, redm[w][hh]);
-        mx[hh] = m;
-        double sum = 0.0;
-        for (int c8 = tid; 8 * c8 < n_kv; c8 += NT) {
-            float e[8];
-#pragma unroll
-            for (int l = 0; l < 8; ++l) e[l] = 8 * c8 + l < n_kv ? x86_v_expf(wl[hh * kvb + 8 * c8 + l] - m) : 0.f;
-            sum += (double)x86_hsum8(e);
-        }
-        sum = wave_sum_d(sum);
-        if (lane == 0) reds[wave][hh] = sum;
-    }
+    sum = wave_sum_d(sum);
+    if (lane == 0) reds[wave] = sum;
     __syncthreads();  // also: every score read before any p replaces it
+    A86_STAMP(3)
+    if (stop == 3) return;
+    double tot = 0.0;
 #pragma unroll
-    for (int hh = 0; hh < G; ++hh) {
-        double sum = 0.0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) sum += reds[w][hh];
-        const float inv = (float)(1.0 / sum);
-        for (int t = tid; t < np; t += NT)
-            wl[hh * kvb + t] = t < n_kv ? h2f(f2h(x86_v_expf(wl[hh * kvb + t] - mx[hh]) * inv)) : 0.f;
-    }
+    for (int w = 0; w < NW; ++w) tot += reds[w];
+    const float inv = (float)(1.0 / tot);
+    for (int t = tid; t < np; t += NT) wl[t] = t < n_kv ? h2f(f2h(x86_v_expf(wl[t] - mx) * inv)) : 0.f;
     __syncthreads();
-    for (int j = tid >> 5; j < DS * G; j += NT / 32) {
-        const int dl = j % DS, hh = j / DS;
+    A86_STAMP(4)
+    if (stop == 4) return;
+    // PV: 32 lanes per dim, lane c = chain c (positions c, c + 32, ...), 16 dims per pass
+    const int c = lane & 31;
+    for (int dl = tid >> 5; dl < DS; dl += NT / 32) {
         float acc = 0.f;
+#pragma unroll 4
         for (int q = c; q < np; q += 32) {
-            const float v = q < n_kv ? h2f(vs[dl * kvb + q]) : 0.f;
-            acc = __builtin_fmaf(v, wl[hh * kvb + q], acc);
+            const float v = q < n_kv ? h2f(vs[dl * vst + q]) : 0.f;
+            acc = __builtin_fmaf(v, wl[q], acc);
         }
         const float r = x86_f16dot_reduce_lanes(acc);
-        if (c == 0) a.out[(size_t)(g * G + hh) * D + d0 + dl] = r;
+        if (c == 0) a.out[(size_t)h * D + d0 + dl] = r;
     }
+    A86_STAMP(5)
 }
 
 template <int D, int G>
 static hipError_t a86_launch(const AttnArgs& a, int n_head, int hk, int kv_bound, hipStream_t s, int mode) {
     if (mode != 3 && kv_bound <= kA86MaxKV) {
-        const size_t lds = (size_t)G * D * 4 + (size_t)G * kv_bound * 4 + (size_t)kA86DS * kv_bound * 2;
-        launch_k(k_a86_d<D, G, kA86DS>, dim3(hk * (D / kA86DS)), dim3(kA86Threads), lds, s, true, true, a, hk, kv_bound);
+#if defined(LLMI_EXPERIMENTS)
+        static const int stop = getenv("LLMI_EXP_A86_STOP") ? atoi(getenv("LLMI_EXP_A86_STOP")) : 0;
+#else
+        constexpr int stop = 0;
+#endif
+        constexpr int DS = 16;
+        const size_t lds = (size_t)kv_bound * 4 + (size_t)DS * (kv_bound + 8) * 2;
+        const dim3 grid(n_head * (D / DS));
+        if (kv_bound <= 128) launch_k(k_a86_h<D, DS, 1>, grid, dim3(kA86Threads), lds, s, true, true, a, n_head, G, kv_bound, stop);
+        else if (kv_bound <= 256) launch_k(k_a86_h<D, DS, 2>, grid, dim3(kA86Threads), lds, s, true, true, a, n_head, G, kv_bound, stop);
+        else if (kv_bound <= 512) launch_k(k_a86_h<D, DS, 4>, grid, dim3(kA86Threads), lds, s, true, true, a, n_head, G, kv_bound, stop);
+        else launch_k(k_a86_h<D, DS, 8>, grid, dim3(kA86Threads), lds, s, true, true, a, n_head, G, kv_bound, stop);
         return hipGetLastError();
     }
     launch_k(k_a86_scores<D, G>, dim3(hk, (kv_bound + 63) / 64), dim3(256), 0, s, true, false, a);

@@ -1481,6 +1481,7 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
     AttnArgs a;
     a.q = q; a.scores = scores; a.out = out; a.st = st; a.n_ctx = n_ctx; a.scale = 1.0f / sqrtf((float)head_dim);
+    a.num = t_hook_numerics;
     a.tmax = scores + (size_t)n_head * n_ctx;
     a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
     a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);

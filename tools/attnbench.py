@@ -1,6 +1,6 @@
 """Attention microbenchmark over KV lengths and paths (llmi_bench_attention).
 Env: ATT_SHAPE="32,8,128" (n_head, n_head_kv, head_dim), ATT_KV="128,640,2048,4096,8000",
-ATT_MODES="1,2,3,4", ATT_REPS=20."""
+ATT_MODES="1,2,3,4", ATT_REPS=20, ATT_NUMERICS=1 (the x86 numerics mode's kernels)."""
 import json
 import os
 import sys
@@ -12,6 +12,8 @@ import torch  # noqa: F401,E402
 from llmi._lib import lib  # noqa: E402
 
 L = lib()
+if os.environ.get("ATT_NUMERICS"):
+    L.llmi_test_option(b"numerics", int(os.environ["ATT_NUMERICS"]))
 H, HK, D = (int(v) for v in os.environ.get("ATT_SHAPE", "32,8,128").split(","))
 kvs = [int(v) for v in os.environ.get("ATT_KV", "128,640,2048,4096,8000").split(",")]
 modes = [int(v) for v in os.environ.get("ATT_MODES", "1,2,3,4").split(",")]
