@@ -1283,7 +1283,7 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     }
     MVArgs a;
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
-    a.nw = nw; a.eps = 1e-5f; a.xfirst = (mode & 4) ? 1 : 0;  // mode bit 2: weights issued after x arrives
+    a.nw = nw; a.eps = 1e-5f; a.xfirst = (mode & 4) ? 1 : (mode & 256) ? -1 : 0;  // mode bit 2: weights after x, bit 8: never
     if (mode & 16) a.prio_alt = prop.multiProcessorCount;  // mode bit 4 (experiment builds): alternating priority
     if (logits) { a.st = st; a.argmax = &st->key[0][0]; }
     uint8_t* xq = nullptr;  // mode bit 3: timing with a pre-quantized activation image (zeros)
@@ -1300,13 +1300,15 @@ double llmi_bench_matvec_ex(int32_t type, const void* w, int32_t n_mats, int64_t
     hipGraph_t g = nullptr;
     hipGraphExec_t ex = nullptr;
     bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    // mode bit 7: every launch reads copy 0 (its weights L2/MALL-hot from the launch before)
+    const size_t wstride = (mode & 128) ? 0 : stride;
     for (int k = 0; ok && k < n_mats; ++k) {
         if (swiglu) {
             a.nseg = 2;
-            a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows / 2, cols);
-            a.seg[1] = seg_at(type, (const uint8_t*)w + stride * k + half, rows / 2, cols);
+            a.seg[0] = seg_at(type, (const uint8_t*)w + wstride * k, rows / 2, cols);
+            a.seg[1] = seg_at(type, (const uint8_t*)w + wstride * k + half, rows / 2, cols);
         } else {
-            a.seg[0] = seg_at(type, (const uint8_t*)w + stride * k, rows, cols);
+            a.seg[0] = seg_at(type, (const uint8_t*)w + wstride * k, rows, cols);
         }
         ok = launch_matvec(a, epi, mb, s) == hipSuccess;
     }

@@ -79,7 +79,7 @@ struct MVArgs {
     int ntasks = 0;
     int split_tasks = 0;                   // two-type launches: tasks of the first type group ...
     int split_wgs = 0;                     // ... and the workgroups that run them
-    int xfirst = 0;                        // experiment: multi-round launches also wait for x before weights
+    int xfirst = 0;                        // experiment: 1 multi-round launches also wait for x before weights, -1 none does
     int prio_alt = 0;                      // experiment builds: alternate s_setprio per sub-item (blocks >= prio_alt: other phase)
     // batched decode (batch.hip, k_mvn): token t of the batch is one decode step of
     // sequence tseq[t] at position tpos[t]; x / y rows are x_stride / y_stride floats

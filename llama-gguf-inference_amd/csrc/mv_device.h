@@ -527,6 +527,19 @@ __host__ __device__ constexpr int row_chains() { return ACT ? 1 : 9; }          
 // chain and sumf starts at 0); Q8_0 tm[b] = (float)sumi_b * (d_w * d_a), b < 8.
 template <int T>
 __device__ __forceinline__ void unit_terms(const UnitW<T>& w, const uint8_t* rec, float (&tm)[9]) {
+#if defined(LLMI_EXP_NOVALU)
+    // experiment builds only: the unit's integer work replaced by an XOR of its words (loads
+    // kept live, results garbage) -- what the launch costs without the per-weight VALU
+    if constexpr (T == T_Q4_K) {
+        uint32_t x = w.s.x ^ w.s.y ^ w.s.z ^ w.s.w;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) x ^= w.q[p][0] ^ w.q[p][1] ^ w.q[p][2] ^ w.q[p][3];
+        const float da = *(const float*)(rec + kRecD);
+#pragma unroll
+        for (int l = 0; l < 9; ++l) tm[l] = da * (float)(int)(x >> l);
+        return;
+    }
+#endif
     if constexpr (T == T_Q4_K || T == T_Q5_K) {
         u32x2 sc, mn;
         scales_mins(w.s.y, w.s.z, w.s.w, sc, mn);

@@ -71,7 +71,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     // their weights only once the activation has arrived: the activation loads then do
     // not queue behind the chip-wide weight burst, and the weight latency overlaps the
     // quantization instead.  Multi-round launches keep the weights in flight from the start.
-    if (tend - tbeg <= G || A.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((tend - tbeg <= G && A.xfirst >= 0) || A.xfirst > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool pipe = task < tend && task_is<EPI, T>(A, g, task);
     Sub b = sub_of<EPI>(A, g, task < tend ? task : tend - 1, 0);
     Seg sg = pick(A, b.si);
