@@ -241,7 +241,7 @@ def test_x86_tiny_decode_vs_oracle(gpu, tiny_models, preset):
 def test_x86_order_trajectory(gpu, synth_dir, preset, n_vocab, n_prompt, n_gen):
     """The configs' real trajectories (2 layers at the preset's exact widths) in x86
     numerics, in lockstep with the oracle's x86 mode: logits bit-identical at every step,
-    the same greedy ids.  Reported into $LLMI_REPORT_DIR/parity_x86_gpu.jsonl."""
+    the same greedy ids.  Reported into $LLMI_REPORT_DIR/parity_x86.jsonl."""
     path = str(synth_dir / f"{preset}-L2-v{n_vocab}.gguf")
     if not os.path.exists(path):
         llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=2, n_vocab=n_vocab)
@@ -279,7 +279,7 @@ def test_x86_order_trajectory(gpu, synth_dir, preset, n_vocab, n_prompt, n_gen):
     out_dir = os.environ.get("LLMI_REPORT_DIR")
     if out_dir:
         os.makedirs(out_dir, exist_ok=True)
-        with open(os.path.join(out_dir, "parity_x86_gpu.jsonl"), "a") as f:
+        with open(os.path.join(out_dir, "parity_x86.jsonl"), "a") as f:
             f.write(json.dumps(rep) + "\n")
 
 
