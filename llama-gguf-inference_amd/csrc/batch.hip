@@ -170,7 +170,8 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
                 sgn = pick(A, bn.si);
             }
             const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
-            const UnitW<T> nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
+            // past the last sub-item: one shared line per part (k_matvec's mv_body)
+            const UnitW<T> nxt = load_unit<T>(sgn, has_next ? lun.row : 0u, has_next ? lun.u : 0u, g.U);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 float tm[9];

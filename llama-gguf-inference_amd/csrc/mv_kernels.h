@@ -77,10 +77,10 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     Seg sg = pick(A, b.si);
     LaneUnit lu = lane_unit(g, b, sg, r, ul);
     // ... then the first units, in flight during the prologue (issued on every path: an
-    // idle wave re-reads row 0, so the prologue's first wait counts only the activation)
+    // idle wave reads unit 0 of row 0, so the prologue's first wait counts only the activation)
     // (prefetch distance 2 -- three rotating register buffers in a 3x unrolled loop --
     // measured slower on every shape: gate+up 16.9 -> 21.2 us, 516 -> 433 tok/s)
-    UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, lu.u, g.U);
+    UnitW<T> cur = load_unit<T>(sg, pipe ? lu.row : 0u, pipe ? lu.u : 0u, g.U);
     if (img) mv_img_finish<2 * NP + 1, NT>(A, L, RI);
     else mv_prologue_finish<ACT, NORM, NP, NT, X86>(A, L, R);
     __syncthreads();
@@ -116,8 +116,10 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
                 sgn = pick(A, bn.si);
             }
             const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
-            // always issue the prefetch (a valid re-load of the current unit if none)
-            nxt = load_unit<T>(sgn, lun.row, lun.u, g.U);
+            // always issue the prefetch (straight-line vmcnt counting); past the wave's last
+            // sub-item every lane reads unit 0 of row 0 -- one line per part per wave instead
+            // of a nontemporal re-read of the wave's 9-14 KB (FETCH_SIZE: +14 MB per gate+up)
+            nxt = load_unit<T>(sgn, has_next ? lun.row : 0u, has_next ? lun.u : 0u, g.U);
             float tm[9];
             if constexpr (X86)
                 unit_store_x86<T>(cur, L.act + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
