@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn tools/bench_profile.sh's two rocprofv3 passes into the committed roofline evidence:
+"""Turn tools/evidence.sh config's two rocprofv3 passes into the committed roofline evidence:
 <out>/traffic_<preset>.json (dominant kernel: FETCH_SIZE bytes per launch, corrected x2
 on gfx950 per MI355X_MICROARCH.md §HBM; rocprof average duration) and
 <out>/kernel_stats.csv (the --stats summary)."""
@@ -34,7 +34,7 @@ res = {
     "hbm_bytes_per_launch": round(fetch_kib * 1024 * 2),
     "launches_counted": len(vals),
     "correction": "bytes = 2 * 1024 * FETCH_SIZE (gfx950 counts wide streaming reads at half, MI355X_MICROARCH.md §HBM)",
-    "source": f"rocprofv3 --pmc FETCH_SIZE over bench.py --preset {preset} (tools/bench_profile.sh); "
+    "source": f"rocprofv3 --pmc FETCH_SIZE over bench.py --preset {preset} (tools/evidence.sh config); "
               "duration from the separate --kernel-trace --stats pass",
 }
 json.dump(res, open(os.path.join(out, f"traffic_{preset}.json"), "w"), indent=1)
