@@ -292,7 +292,7 @@ class LlmiEngine:
         llmi = self.llmi
         kmax = max(counts)
         n_ctx = ((self.args.prompt + steps + 8 + 2 + 255) // 256) * 256
-        ctx = llmi.Context(self.model, n_ctx=n_ctx, n_seq=kmax)
+        ctx = llmi.Context(self.model, n_ctx=n_ctx, n_seq=kmax, use_graphs=not self.args.eager)
         rng = np.random.default_rng(40)
         bos = self.model.bos if self.model.bos >= 0 else 1
         prompts = [[bos] + [int(t) for t in rng.integers(0, min(128000, self.model.n_vocab), self.args.prompt - 1)]
