@@ -280,10 +280,12 @@ struct BmStage {
 
 template <int T, int NW>
 __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[NW], const uint8_t* aq,
-                                        const uint8_t* abf, const float* ad, int s, int S, int nt, int exp = 0) {
+                                        const uint8_t* abf, const float* ad, int s, int S, int nt, int exp = 0,
+                                        bool weights = true) {
     const int lane = threadIdx.x & 63, n = lane & 15, grp = lane >> 4;
+    if (weights)
 #pragma unroll
-    for (int wi = 0; wi < NW; ++wi) st.w[wi] = pf_w_load<T>(rp[wi], s, S);
+        for (int wi = 0; wi < NW; ++wi) st.w[wi] = pf_w_load<T>(rp[wi], s, S);
     // only the lanes of real tokens load (the padding rows' loads would repeat token 0's
     // fragments through the TA); the others keep zeros
     int ntl = nt;
@@ -396,6 +398,58 @@ __device__ __forceinline__ void bm_tile(const MVArgs& A, int tile, int& si, int&
 #endif
 }
 
+// wave 0 of a k_bmm / k_bmd workgroup: the tile's row values from its chain results G and the
+// epilogue per token
+template <int T, int EPI, int NW, int NC>
+__device__ __forceinline__ void bm_epilogue(const MVArgs& A, const float4* G, int nt, int tile, int si, int row0) {
+    const int t = threadIdx.x >> 3, n0 = 2 * (threadIdx.x & 7);
+    unsigned long long best = 0;
+    int seq = 0, pos = 0;
+    if (t < nt) {
+        seq = A.tseq ? A.tseq[t] : 0;
+        pos = A.tpos ? A.tpos[t] : 0;
+        const float* Gf = (const float*)G;
+        float v[NW][2];
+#pragma unroll
+        for (int wi = 0; wi < NW; ++wi)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int L = n0 + h + 16 * (t >> 2), i = t & 3;
+                float x = NC == 9 ? Gf[((wi * 9 + 8) * 32 + L) * 4 + i] : 0.f;  // sumf, then + sums[0..7]
+#pragma unroll
+                for (int l = 0; l < 8; ++l) x += Gf[((wi * 9 + l) * 32 + L) * 4 + i];
+                v[wi][h] = x;
+            }
+        const MVArgs B = token_view(A, t, seq);
+        PairRef ref;
+        ref.sa = ref.sb = pick(A, si);
+        ref.ra = row0 + n0;
+        ref.rb = ref.ra + 1;
+        ref.vb = 1;
+        ref.type = T;
+        if constexpr (EPI == EPI_SWIGLU) {
+            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
+            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
+        } else {
+            epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
+        }
+    }
+    if constexpr (EPI == EPI_LOGITS) {
+        // per token: the max over its 8 threads (consecutive lanes), one atomic
+        // into the slot of its sequence's StepState; tile 0 advances the position
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const unsigned long long bo = __shfl_xor(best, o);
+            best = bo > best ? bo : best;
+        }
+        if ((threadIdx.x & 7) == 0 && t < nt) {
+            StepState* st = A.st + seq;
+            if (best) atomicMax(&st->key[pos & 1][tile % kArgSlots], best);
+            if (tile == 0) st->pos_next = pos + 1;
+        }
+    }
+}
+
 // Persistent: workgroup b runs tiles b, b + grid, ...; one ITERATION = one round of kBmW
 // stages of one tile, the next iteration's loads (next round, or the next tile's first
 // round) issued before this one's terms, so the next tile's weights are in flight during
@@ -486,54 +540,7 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
         }
         if (last) {
             __syncthreads();
-            if (threadIdx.x < 64) {  // wave 0: the row values and the epilogue of the tile
-                const int t = threadIdx.x >> 3, n0 = 2 * (threadIdx.x & 7);
-                unsigned long long best = 0;
-                int seq = 0, pos = 0;
-                if (t < nt) {
-                    seq = A.tseq ? A.tseq[t] : 0;
-                    pos = A.tpos ? A.tpos[t] : 0;
-                    const float* Gf = (const float*)G;
-                    float v[NW][2];
-#pragma unroll
-                    for (int wi = 0; wi < NW; ++wi)
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int L = n0 + h + 16 * (t >> 2), i = t & 3;
-                            float x = NC == 9 ? Gf[((wi * 9 + 8) * 32 + L) * 4 + i] : 0.f;  // sumf, then + sums[0..7]
-#pragma unroll
-                            for (int l = 0; l < 8; ++l) x += Gf[((wi * 9 + l) * 32 + L) * 4 + i];
-                            v[wi][h] = x;
-                        }
-                    const MVArgs B = token_view(A, t, seq);
-                    PairRef ref;
-                    ref.sa = ref.sb = pick(A, si);
-                    ref.ra = row0 + n0;
-                    ref.rb = ref.ra + 1;
-                    ref.vb = 1;
-                    ref.type = T;
-                    if constexpr (EPI == EPI_SWIGLU) {
-                        epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
-                        epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
-                    } else {
-                        epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
-                    }
-                }
-                if constexpr (EPI == EPI_LOGITS) {
-                    // per token: the max over its 8 threads (consecutive lanes), one atomic
-                    // into the slot of its sequence's StepState; tile 0 advances the position
-#pragma unroll
-                    for (int o = 1; o < 8; o <<= 1) {
-                        const unsigned long long bo = __shfl_xor(best, o);
-                        best = bo > best ? bo : best;
-                    }
-                    if ((threadIdx.x & 7) == 0 && t < nt) {
-                        StepState* st = A.st + seq;
-                        if (best) atomicMax(&st->key[pos & 1][tile % kArgSlots], best);
-                        if (tile == 0) st->pos_next = pos + 1;
-                    }
-                }
-            }
+            if (threadIdx.x < 64) bm_epilogue<T, EPI, NW, NC>(A, G, nt, tile, si, row0);
         }
         if (!has_next) break;
         cur = nxt;
@@ -544,6 +551,163 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
 #pragma unroll
         for (int wi = 0; wi < NW; ++wi) rp[wi] = rpn[wi];
         ++it;
+    }
+}
+
+// ---- k_bmd: k_bmm with the weights staged through LDS by DMA -----------------------------
+// k_bmm's lanes read 16 B of 16 different rows per load (the MFMA's B layout), so every
+// load touches 64 lines; at 8 sequences that access pattern, not the MFMA or the VALU, is
+// what bounds it (LLMI_BMM_EXP=1, every lane reading row 0: 1272 -> 2030 tok/s).  k_bmd
+// moves a whole round -- the kBmW consecutive units of every (matrix, row, plane part) of
+// the tile, 128 contiguous bytes each -- with global_load_lds (1 KiB per wave instruction,
+// no VGPRs) into one LDS buffer, and each wave takes its stage's parts from there.  Per
+// round: weights out of LDS, barrier, next round's DMA + activations, terms, barrier
+// (retires the DMA), fold.  The 16-B pieces of a segment are stored XOR-swizzled by row
+// (slot = stage ^ (row & 7)) so the 16 rows of a read spread over the banks.  Same terms,
+// same fold: bit-identical to k_bmm.
+typedef __attribute__((address_space(3))) void* bmd_lds_vp;
+typedef __attribute__((address_space(1))) void* bmd_glb_vp;
+template <int T>
+__host__ __device__ constexpr int bmd_nseg() { return T == T_Q4_K ? 9 : T == T_Q5_K ? 11 : 13; }
+// bytes of a round's weight buffer
+template <int T, int NW>
+__host__ __device__ constexpr size_t bmd_wbytes() { return (size_t)NW * 16 * bmd_nseg<T>() * kBmW * 16; }
+// plane base of segment `seg` of a row (unit u at + 16 u): A parts 0..7, then Q4_K the
+// header; Q5_K the header and the two fifth-bit parts; Q6_K the four high-bit parts and the scales
+template <int T>
+__device__ __forceinline__ const uint8_t* bmd_seg_base(const RowPtr& rp, int seg) {
+    if (seg < 8) return rp.qa + (uint32_t)seg * rp.ps;
+    if constexpr (T == T_Q4_K) return rp.sb;
+    else if constexpr (T == T_Q5_K) return seg == 8 ? rp.sb : rp.hb + (uint32_t)(seg - 9) * rp.ps;
+    else return seg < 12 ? rp.hb + (uint32_t)(seg - 8) * rp.ps : rp.sb;
+}
+template <int T, int EPI, int NW>
+__device__ __forceinline__ void bmd_dma(const MVArgs& A, int si, int row0, int rho, uint8_t* wb) {
+    constexpr int NSEG = bmd_nseg<T>(), NPC = NW * 16 * NSEG * kBmW;  // 16-B pieces per round
+    static_assert(NPC % 64 == 0, "whole DMA instructions");
+    const int lane = threadIdx.x & 63, wave = uniform((int)(threadIdx.x >> 6));
+    const int U = A.cols >> 8;
+    for (int i = wave; i < NPC / 64; i += kBmW) {
+        const int f = i * 64 + lane, q = f / kBmW, slot = f % kBmW;
+        const int seg = q % NSEG, rr = q / NSEG, row = rr % 16, mat = rr / 16;
+        const int u = min(rho * kBmW + (slot ^ (row & 7)), U - 1);
+        const RowPtr rp = row_ptr<T>(pick(A, EPI == EPI_SWIGLU ? mat : si), row0 + row, A.cols);
+        __builtin_amdgcn_global_load_lds((bmd_glb_vp)(bmd_seg_base<T>(rp, seg) + (uint32_t)u * 16),
+                                         (bmd_lds_vp)(wb + (size_t)i * 1024), 16, 0, 0);
+    }
+}
+// this wave's stage (slot `stg` of the round) of every matrix out of the round buffer (Q6_K's
+// fp16 d, 2 B per unit, still from global memory)
+template <int T, int NW>
+__device__ __forceinline__ void bmd_w(BmStage<T, NW>& st, const uint8_t* wb, int stg, const RowPtr (&rp)[NW], int s) {
+    constexpr int NSEG = bmd_nseg<T>();
+    const int lane = threadIdx.x & 63, row = lane & 15, g = lane >> 4;
+    const int slot = stg ^ (row & 7);
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) {
+        auto piece = [&](int seg) { return wb + ((((size_t)(wi * 16 + row) * NSEG + seg) * kBmW + slot) * 16); };
+        PfW<T>& w = st.w[wi];
+        w.q0 = *(const u32x4*)piece(2 * g);
+        w.q1 = *(const u32x4*)piece(2 * g + 1);
+        if constexpr (T == T_Q4_K || T == T_Q5_K) {
+            w.hdr = *(const u32x4*)piece(8);
+            if constexpr (T == T_Q5_K) w.qh = *(const u32x2*)(piece(9 + (g >> 1)) + 8 * (g & 1));
+        } else {
+            w.hdr = *(const u32x4*)piece(8 + g);
+            w.sc = *(const uint32_t*)(piece(12) + 4 * g);
+            w.d = *(const uint16_t*)(rp[wi].db + (uint32_t)s * 2);
+        }
+    }
+}
+
+template <int T, int EPI>
+__global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
+                                              int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
+    constexpr int NC = T == T_Q6_K ? 8 : 9;
+    constexpr int kBuf = kBmW * NW * 9 * 32;        // float4 of a round's terms
+    float4* Tm = (float4*)smem;
+    float4* G = Tm + kBuf;
+    uint8_t* Wb = (uint8_t*)(G + NW * 9 * 32);
+    const int wave = uniform((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const int S = A.cols >> 8, R = (S + kBmW - 1) / kBmW;
+    int tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    int si, row0;
+    RowPtr rp[NW];
+    bm_tile<T, EPI, NW>(A, tile, si, row0, rp);
+    constexpr int NI = NW * NC * 32;
+    float4 fs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    BmStage<T, NW> cur;
+    bm_load<T, NW>(cur, rp, aq, abf, ad, wave < S ? wave : S - 1, S, nt, 0, false);
+    bmd_dma<T, EPI, NW>(A, si, row0, 0, Wb);
+    __syncthreads();  // vmcnt(0): round 0 in LDS
+    int rho = 0;
+    for (;;) {
+        const int s = rho * kBmW + wave;
+        bmd_w<T, NW>(cur, Wb, wave, rp, s < S ? s : S - 1);
+        int tn = tile, rn = rho + 1;
+        if (rn == R) {
+            rn = 0;
+            tn = tile + gridDim.x;
+        }
+        const bool has_next = tn < ntiles;
+        int sin, row0n;
+        RowPtr rpn[NW];
+        bm_tile<T, EPI, NW>(A, has_next ? tn : tile, sin, row0n, rpn);
+        __syncthreads();  // every wave has its stage out of the round buffer
+        if (has_next) bmd_dma<T, EPI, NW>(A, sin, row0n, rn, Wb);
+        const int sn = rn * kBmW + wave;
+        BmStage<T, NW> nxt;
+        bm_load<T, NW>(nxt, rpn, aq, abf, ad, sn < S ? sn : S - 1, S, nt, 0, false);
+        if (s < S) {
+            float tm[NW][9][4];
+            bm_terms<T, NW>(cur, tm);
+            if (lane < 32) {
+#pragma unroll
+                for (int wi = 0; wi < NW; ++wi)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c)
+                        Tm[((wave * NW + wi) * 9 + c) * 32 + lane] =
+                            make_float4(tm[wi][c][0], tm[wi][c][1], tm[wi][c][2], tm[wi][c][3]);
+            }
+        }
+        __syncthreads();  // the terms in LDS; vmcnt(0) retires the next round's DMA
+        const int nv = S - rho * kBmW < kBmW ? S - rho * kBmW : kBmW;
+        const bool last = rho == R - 1;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int f = threadIdx.x + k * kBmT;
+            if (f < NI) {
+                const int wi = f / (NC * 32), c = (f / 32) % NC, L = f & 31;
+                float4 a = fs[k];
+                for (int w = 0; w < nv; ++w) {
+                    const float4 v = Tm[((w * NW + wi) * 9 + c) * 32 + L];
+                    a.x += v.x;
+                    a.y += v.y;
+                    a.z += v.z;
+                    a.w += v.w;
+                }
+                if (last) {
+                    G[(wi * 9 + c) * 32 + L] = a;
+                    a = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                fs[k] = a;
+            }
+        }
+        if (last) {
+            __syncthreads();
+            if (threadIdx.x < 64) bm_epilogue<T, EPI, NW, NC>(A, G, nt, tile, si, row0);
+        }
+        if (!has_next) break;
+        cur = nxt;
+        tile = tn;
+        rho = rn;
+        si = sin;
+        row0 = row0n;
+#pragma unroll
+        for (int wi = 0; wi < NW; ++wi) rp[wi] = rpn[wi];
     }
 }
 
@@ -655,13 +819,13 @@ hipError_t launch_mvn(const MVArgs& a0, int epi, int nt, int max_blocks, hipStre
 // ---- k_bmm launchers -------------------------------------------------------------------
 static int g_bmm_env = getenv("LLMI_BMM") ? atoi(getenv("LLMI_BMM")) : 1;  // 0: k_mvn everywhere (A/B)
 
-// fewest tokens for which the step takes k_bmm (its cost is nearly flat in nt; k_mvn's
-// grows with nt and pads 5..7 tokens to 8: 8B bench, 2 / 4 / 8 sequences: k_bmm (first
-// form) 6.51 / 6.62 / 6.77 ms per step, persistent 6.27 at 8; k_mvn 2.96 / 4.73 / 8.02
-// ms); LLMI_BMM_MIN overrides (A/B)
+// fewest tokens for which the step takes the matrix-core kernel (its cost is nearly flat in
+// nt; k_mvn's grows with nt and pads 3 to 4 and 5..7 tokens to 8).  8B bench, tok/s at
+// 2 / 3 / 4 / 6 / 8 sequences: k_bmd from 2: 501 / 732 / 959 / 1410 / 1875; k_mvn below 5:
+// 680 / 651 / 851 (profiles/r05/batch/).  LLMI_BMM_MIN overrides (A/B)
 int bmm_min_tokens() {
     const char* e = getenv("LLMI_BMM_MIN");  // read per call (step capture): tests switch it
-    return e ? atoi(e) : 5;
+    return e ? atoi(e) : 3;
 }
 
 bool bmm_ok(const MVArgs& a, int epi) {
@@ -697,11 +861,21 @@ static int bmm_cap(const void* k, size_t lds) {
     return cap;
 }
 
+// LLMI_BMM_DMA (A/B): 1 k_bmd (weights through LDS by DMA, default), 0 k_bmm; read per
+// launch (step capture), so tests can run both
+static int bmm_dma() {
+    const char* e = getenv("LLMI_BMM_DMA");
+    return e ? atoi(e) : 1;
+}
+
 template <int T, int EPI>
 static hipError_t bmm_launch(const MVArgs& a, const void* aq, const void* abf, const float* ad, int nt, hipStream_t s) {
-    auto k = k_bmm<T, EPI>;
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
-    const size_t lds = (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
+    const bool dma = bmm_dma() != 0;
+    auto k = dma ? k_bmd<T, EPI> : k_bmm<T, EPI>;
+    const size_t lds = dma ? (size_t)(kBmW + 1) * NW * 9 * 32 * 16 + bmd_wbytes<T, NW>()
+                           : (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int cap = bmm_cap((const void*)k, lds);
     int rows = 0;
     if (EPI == EPI_SWIGLU) rows = a.seg[0].rows;

@@ -180,11 +180,14 @@ def test_batched_real_widths(gpu, synth_dir, preset, n_vocab):
 
 @pytest.mark.parametrize("preset,k", [("llama3-8b-q4km", 2), ("llama3-8b-q4km", 5), ("mistral7b-q5km", 3),
                                        ("mistral7b-q6k", 8)])
-def test_bmm_any_batch_size(gpu, synth_dir, monkeypatch, preset, k):
-    """The matrix-core batched matvec (batch.hip k_bmm) forced for every batch size
-    (LLMI_BMM_MIN=1; by default it takes steps of 5 or more tokens): each sequence's tokens and
-    logits equal its single-sequence decode at real widths, Q4_K / Q5_K / Q6_K."""
+@pytest.mark.parametrize("dma", ["1", "0"])  # k_bmd (weights staged through LDS by DMA) / k_bmm
+def test_bmm_any_batch_size(gpu, synth_dir, monkeypatch, preset, k, dma):
+    """The matrix-core batched matvec (batch.hip k_bmd, and k_bmm with LLMI_BMM_DMA=0) forced
+    for every batch size (LLMI_BMM_MIN=1; by default it takes steps of 3 or more tokens): each
+    sequence's tokens and logits equal its single-sequence decode at real widths, Q4_K / Q5_K /
+    Q6_K."""
     monkeypatch.setenv("LLMI_BMM_MIN", "1")
+    monkeypatch.setenv("LLMI_BMM_DMA", dma)
     path = str(synth_dir / f"{preset}-batch-L2.gguf")
     llmi.write_synthetic_gguf(path, preset, seed=11, n_layer=2)
     rng = np.random.default_rng(5 + k)
