@@ -563,8 +563,9 @@ def main(argv=None):
                                     "note": "k sequences per replica in batched steps (one weight stream per step), "
                                             f"{args.prompt}-token prompts, {args.batch_steps} timed steps; "
                                             "aggregate tokens/s of this rank; not the metric's value",
-                                    "matvec": "k_bmm (f16 MFMA, batch.hip) from "
-                                              f"{os.environ.get('LLMI_BMM_MIN', '5')} sequences on K-quant "
+                                    "matvec": "k_bmd (f16 MFMA, weights staged by LDS-DMA, batch.hip; k_bmm "
+                                              "with LLMI_BMM_DMA=0) from "
+                                              f"{os.environ.get('LLMI_BMM_MIN', '3')} sequences on K-quant "
                                               "segments, else k_mvn (VALU)"}
             if batched else None,
             "cpu_baseline": cpu,

@@ -170,6 +170,7 @@ struct PfGemm {
     uint16_t* vc = nullptr;    // layer V cache [HK][D][n_ctx]
     const float* rope = nullptr;
     int pos0 = 0, head_dim = 0, n_rot = 0, n_ctx = 0;
+    int exp = 0;               // experiment builds (LLMI_PF_EXP): 1 every lane reads its wave's first row
 };
 struct PfAttn {
     const float* q = nullptr;  // [T][ldq] roped q

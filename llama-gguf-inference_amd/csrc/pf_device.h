@@ -58,6 +58,24 @@ __device__ __forceinline__ RowPtr row_ptr(const Seg& s, int row, int cols) {
     r.db = s.d + ru * (T == T_Q8_0 ? 16 : 2);
     return r;
 }
+// plain (temporal) loads: a lane reads 16 B of a 128-B line whose other 112 B the next 7
+// stages read, so the line should stay in L2 (the decode matvec's nontemporal weights are
+// read once)
+#ifndef LLMI_PF_NT
+#define LLMI_PF_NT 0
+#endif
+__device__ __forceinline__ u32x4 pf_ld16(const uint8_t* p) {
+    if constexpr (LLMI_PF_NT) return ldw(p);
+    else return *(const u32x4*)p;
+}
+__device__ __forceinline__ u32x2 pf_ld8(const uint8_t* p) {
+    if constexpr (LLMI_PF_NT) return ldw8(p);
+    else return *(const u32x2*)p;
+}
+__device__ __forceinline__ uint32_t pf_ld4(const uint8_t* p) {
+    if constexpr (LLMI_PF_NT) return ldw4(p);
+    else return *(const uint32_t*)p;
+}
 template <int T>
 __device__ __forceinline__ PfW<T> pf_w_load(const RowPtr& rp, int stage, int) {
     PfW<T> w;
@@ -70,14 +88,14 @@ __device__ __forceinline__ PfW<T> pf_w_load(const RowPtr& rp, int stage, int) {
             w.q8[l] = *(const u32x2*)(rp.qa + (2 * l + (g >> 1)) * rp.ps + st * 16 + 8 * (g & 1));
         w.dd = *(const u32x4*)(rp.db + st * 16);
     } else {
-        w.q0 = ldw(rp.qa + (2 * g) * rp.ps + st * 16);
-        w.q1 = ldw(rp.qa + (2 * g + 1) * rp.ps + st * 16);
+        w.q0 = pf_ld16(rp.qa + (2 * g) * rp.ps + st * 16);
+        w.q1 = pf_ld16(rp.qa + (2 * g + 1) * rp.ps + st * 16);
         if constexpr (T == T_Q4_K || T == T_Q5_K) {
             w.hdr = *(const u32x4*)(rp.sb + st * 16);
-            if constexpr (T == T_Q5_K) w.qh = ldw8(rp.hb + (g >> 1) * rp.ps + st * 16 + 8 * (g & 1));
+            if constexpr (T == T_Q5_K) w.qh = pf_ld8(rp.hb + (g >> 1) * rp.ps + st * 16 + 8 * (g & 1));
         } else {
-            w.hdr = ldw(rp.hb + g * rp.ps + st * 16);
-            w.sc = ldw4(rp.sb + st * 16 + 4 * g);
+            w.hdr = pf_ld16(rp.hb + g * rp.ps + st * 16);
+            w.sc = pf_ld4(rp.sb + st * 16 + 4 * g);
             w.d = *(const uint16_t*)(rp.db + st * 2);
         }
     }
