@@ -837,6 +837,66 @@ __device__ __forceinline__ void unit_store_x86(const UnitW<T>& w, const uint8_t*
     }
 }
 
+// The fold's chains in order with their LDS reads batched: 16 terms per batch, the next
+// batch's four ds_read_b128 issued before the current batch's adds, so a chain waits one
+// LDS latency per 16 terms instead of one per 4 (the per-4 loop waited on every read:
+// 44 waits for a Q8_0 row of 5632 columns).  Reads run up to 15 floats past the chain's
+// last term -- inside the wave's fold buffer (kFoldFloats >= 9 R Lr + 16) -- and those
+// values are never added.  `a` sees exactly the adds / fmas of the plain loop.
+template <class OP>
+__device__ __forceinline__ float chain_batched(int len, float a, OP&& term) {
+    constexpr int TB = OP::TB;  // terms per batch (16 floats of registers)
+    float c[16], nx[16];
+    term.load(0, c);
+    int b = 0;
+    for (; b + TB <= len; b += TB) {
+        term.load(b + TB, nx);
+#pragma unroll
+        for (int k = 0; k < TB; ++k) a = term.apply(a, c, k);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c[k] = nx[k];
+    }
+#pragma unroll
+    for (int k = 0; k < TB - 1; ++k)
+        if (b + k < len) a = term.apply(a, c, k);
+    return a;
+}
+struct ChainAdd {  // a += q[i]
+    static constexpr int TB = 16;
+    const float* q;
+    __device__ __forceinline__ void load(int b, float* v) const {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 x = *(const float4*)(q + b + 4 * k);
+            v[4 * k] = x.x;
+            v[4 * k + 1] = x.y;
+            v[4 * k + 2] = x.z;
+            v[4 * k + 3] = x.w;
+        }
+    }
+    __device__ __forceinline__ float apply(float a, const float* v, int k) const { return a + v[k]; }
+};
+struct ChainFma {  // a = fma(d[i], s[i], a); v holds the batch's 8 (d, s) pairs
+    static constexpr int TB = 8;
+    const float* d;
+    const float* s;
+    __device__ __forceinline__ void load(int b, float* v) const {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const float4 x = *(const float4*)(d + b + 4 * k), y = *(const float4*)(s + b + 4 * k);
+            v[8 * k] = x.x;
+            v[8 * k + 1] = y.x;
+            v[8 * k + 2] = x.y;
+            v[8 * k + 3] = y.y;
+            v[8 * k + 4] = x.z;
+            v[8 * k + 5] = y.z;
+            v[8 * k + 6] = x.w;
+            v[8 * k + 7] = y.w;
+        }
+    }
+    __device__ __forceinline__ float apply(float a, const float* v, int k) const { return __builtin_fmaf(v[2 * k], v[2 * k + 1], a); }
+};
+
 // Fold lane f = (row f / NC, chain f % NC) runs its fma chain over the sub-item's n units
 // (Q8_0: 8 n blocks) in order; chains 0..7 take d, chains 8..11 (the min lanes) -dmin.
 template <int ACT>
@@ -845,22 +905,16 @@ __device__ __forceinline__ void fold_sub_x86(float* F, int R, int lr, int n, boo
     const int lane = threadIdx.x & 63, nf = R * NC;
     for (int f = lane; f < nf; f += 64) {
         const int r = f / NC, c = f - r * NC;
-        float a = acc;
+        float a;
         if constexpr (ACT) {
             const float* s = F + (size_t)(r * 8 + c) * 8 * lr;
             const float* d = F + kX86QD + (size_t)r * 8 * lr;
-            for (int i = 0; i < 8 * n; i += 4) {
-                const float4 sv = *(const float4*)(s + i), dv = *(const float4*)(d + i);
-                a = __builtin_fmaf(dv.x, sv.x, a);
-                a = __builtin_fmaf(dv.y, sv.y, a);
-                a = __builtin_fmaf(dv.z, sv.z, a);
-                a = __builtin_fmaf(dv.w, sv.w, a);
-            }
+            a = chain_batched(8 * n, acc, ChainFma{d, s});
             if (last) F[kX86QG + f] = a;
         } else {
             const float* s = F + (size_t)(r * 12 + c) * lr;
             const float* d = F + kX86KD + (size_t)(r * 2 + (c >= 8 ? 1 : 0)) * lr;
-            for (int u = 0; u < n; ++u) a = __builtin_fmaf(d[u], s[u], a);
+            a = chain_batched(n, acc, ChainFma{d, s});
             if (last) F[kX86KG + f] = a;
         }
         if (last) a = 0.f;
@@ -936,15 +990,7 @@ __device__ __forceinline__ void fold_sub(float* F, int R, int lr, int n, bool la
     const int lane = threadIdx.x & 63, nf = R * NC;
     const int len = ACT ? 8 * n : n, stride = ACT ? 8 * lr : lr;
     for (int f = lane; f < nf; f += 64) {
-        float a = acc;
-        const float* q = F + f * stride;
-        for (int b = 0; b < len; b += 4) {
-            const float4 v = *(const float4*)(q + b);
-            a += v.x;
-            if (b + 1 < len) a += v.y;
-            if (b + 2 < len) a += v.z;
-            if (b + 3 < len) a += v.w;
-        }
+        float a = chain_batched(len, acc, ChainAdd{F + f * stride});
         if (last) {
             F[kFoldF + f] = a;
             a = 0.f;
