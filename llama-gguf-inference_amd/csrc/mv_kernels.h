@@ -305,6 +305,42 @@ static bool mv_try_wide(const MVArgs& a, hipStream_t s, hipError_t& e) {
         return false;
     }
 }
+// Narrow launches: fewer tasks than the waves of one 4-wave workgroup per CU (TinyLlama's
+// 2048-column QKV, O and gate+up: 256-704 tasks of 8 rows) run as one-wave workgroups, one
+// task each, so they spread over up to ntasks CUs instead of ntasks / 4 (each workgroup
+// still builds the whole activation image).  LLMI_MV_NARROW = 0 turns it off (A/B); which
+// wave reduces a row never changes a result.
+constexpr int kMVNarrow = 64;
+static inline int narrow_on() {
+    static const int v = getenv("LLMI_MV_NARROW") ? atoi(getenv("LLMI_MV_NARROW")) : 1;
+    return v;
+}
+template <int ACT, bool NORM, int T, int EPI, int NP, int X86>
+static hipError_t mv_launch_narrow(const MVArgs& a0, hipStream_t s) {
+    const size_t lds = mv_lds_total(ACT, a0.cols, 1, T, T, X86);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    auto k = k_matvec<ACT, NORM, EPI, T, NP, T, kMVNarrow, X86>;
+    const dim3 g = resident_grid(k, dim3(a0.ntasks), lds, kMVNarrow);
+    MVArgs a = a0;
+    a.split_wgs = 0;
+    launch_k(k, g, dim3(kMVNarrow), lds, s, true, true, a);
+    return hipGetLastError();
+}
+template <int ACT, bool NORM, int T, int EPI, int X86>
+static bool mv_try_narrow(const MVArgs& a, hipStream_t s, hipError_t& e) {
+    if constexpr (EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV || EPI == EPI_STORE) {
+        const int cus = cu_count();
+        if (!narrow_on() || cus <= 0 || a.ntasks >= cus * kMVWaves) return false;
+        for (int i = 0; i < a.nseg; ++i)
+            if (a.seg[i].type != T) return false;  // single-type launches only
+        const int per = (a.cols / 16 + kMVNarrow - 1) / kMVNarrow;
+        e = per <= 2 ? mv_launch_narrow<ACT, NORM, T, EPI, 2, X86>(a, s) : mv_launch_narrow<ACT, NORM, T, EPI, 4, X86>(a, s);
+        return true;
+    } else {
+        (void)a; (void)s; (void)e;
+        return false;
+    }
+}
 template <int ACT, bool NORM, int T, int EPI, int NP, int X86>
 static hipError_t mv_launch(const MVArgs& a0, dim3 grid, size_t lds_in, hipStream_t s) {
     const size_t lds = std::max(lds_in, mv_lds_total(ACT, a0.cols, kMVWaves, T, T, X86));
@@ -370,6 +406,7 @@ template <int ACT, bool NORM, int T, int EPI, int X86>
 static hipError_t mv_launch_np(const MVArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     hipError_t e = hipSuccess;
     if (mv_try_wide<ACT, NORM, T, EPI, X86>(a, s, e)) return e;
+    if (mv_try_narrow<ACT, NORM, T, EPI, X86>(a, s, e)) return e;
     switch (prologue_np(a.cols)) {
         case 1: return mv_launch<ACT, NORM, T, EPI, 1, X86>(a, grid, lds, s);
         case 2: return mv_launch<ACT, NORM, T, EPI, 2, X86>(a, grid, lds, s);
