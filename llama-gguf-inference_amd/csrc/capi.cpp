@@ -1555,6 +1555,7 @@ int32_t llmi_trace_matvec(int32_t type, const void* w, int64_t rows, int64_t col
     a.nseg = 1; a.cols = (int)cols; a.npairs = (int)((rows + 1) / 2); a.x = x; a.y = y;
     a.seg[0] = seg_at(type, w, rows, cols);
     a.trace = (unsigned long long*)trace_dev;
+    if (mode & 256) a.xfirst = -1;  // mode bit 8: weights issued before the activation arrives
     uint8_t* xq = nullptr;  // mode bit 3: pre-quantized activation image (zeros)
     if ((mode & 8) && hipMalloc(&xq, (size_t)(cols / 256) * 304) == hipSuccess) {
         (void)hipMemset(xq, 0, (size_t)(cols / 256) * 304);

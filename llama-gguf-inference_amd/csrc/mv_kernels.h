@@ -315,6 +315,12 @@ static inline int narrow_on() {
     static const int v = getenv("LLMI_MV_NARROW") ? atoi(getenv("LLMI_MV_NARROW")) : 1;
     return v;
 }
+// tasks per CU below which a launch goes narrow (LLMI_MV_NARROW_TPC, A/B; default 4 = the
+// waves of one 4-wave workgroup)
+static inline int narrow_tpc() {
+    static const int v = getenv("LLMI_MV_NARROW_TPC") ? atoi(getenv("LLMI_MV_NARROW_TPC")) : kMVWaves;
+    return v;
+}
 template <int ACT, bool NORM, int T, int EPI, int NP, int X86>
 static hipError_t mv_launch_narrow(const MVArgs& a0, hipStream_t s) {
     const size_t lds = mv_lds_total(ACT, a0.cols, 1, T, T, X86);
@@ -330,7 +336,7 @@ template <int ACT, bool NORM, int T, int EPI, int X86>
 static bool mv_try_narrow(const MVArgs& a, hipStream_t s, hipError_t& e) {
     if constexpr (EPI == EPI_ADD || EPI == EPI_SWIGLU || EPI == EPI_QKV || EPI == EPI_STORE) {
         const int cus = cu_count();
-        if (!narrow_on() || cus <= 0 || a.ntasks >= cus * kMVWaves) return false;
+        if (!narrow_on() || cus <= 0 || a.ntasks >= cus * narrow_tpc()) return false;
         for (int i = 0; i < a.nseg; ++i)
             if (a.seg[i].type != T) return false;  // single-type launches only
         const int per = (a.cols / 16 + kMVNarrow - 1) / kMVNarrow;
