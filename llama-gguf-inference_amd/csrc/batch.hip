@@ -936,10 +936,24 @@ template <int D>
 __global__ __launch_bounds__(D) void k_battl_sum(BAttnArgs b, int n_head) { attl_sum_body<D>(b.a[blockIdx.z], n_head); }
 
 // batched attention path: dim split up to 1024 positions for up to 3 slots (8B bench:
-// 2 slots 940 vs 897 tok/s split, 4: 1335 vs 1341, 8: 1746 vs 1823 — at 8 slots its
-// redundant K reads cost more than the split path's second launch), split while its LDS
-// fits up to 2048 (G <= 4) / 1024 positions, long-context beyond; LLMI_BATTN_MODE (A/B
-// only) forces 2 split, 6 dim split or 7 long-context
+// 2 slots 940 vs 897 tok/s split, 4: 1335 vs 1341, 8: 1746 vs 1823 with 8 dim slices —
+// at 8 slots its redundant K reads cost more than the split path's second launch), and
+// for any slot count up to 512 positions with 1-2 slices (battn_slices), split while its
+// LDS fits up to 2048 (G <= 4) / 1024 positions, long-context beyond; LLMI_BATTN_MODE
+// (A/B only) forces 2 split, 6 dim split or 7 long-context
+// dim slices of the batched dim-split attention: the single-sequence choice (about 256
+// workgroups) is H * S * slots workgroups here, each re-reading its head's K rows; up to
+// 512 positions 2 slices for <= 4 slots and 1 beyond (8B, ~200 positions, 2/4/8 slots:
+// 721/960/1878 tok/s split or 8 slices -> 731/992/1945 with 2, 727/987/1963 with 1,
+// profiles/r05/batch/battn_slices.txt); LLMI_BATTN_S (A/B) forces 1, 2, 4 or 8
+static int battn_slices(int n_head, int head_dim, int kv_bound, int nt) {
+    if (const char* es = getenv("LLMI_BATTN_S")) {
+        const int v = atoi(es);
+        if ((v == 1 || v == 2 || v == 4 || v == 8) && head_dim / v >= 8) return v;
+    }
+    if (kv_bound <= 512 && nt >= 2) return nt > 4 ? 1 : 2;
+    return attn_d_slices(n_head, head_dim);
+}
 static int battn_path(int g, int n_head, int head_dim, int kv_bound, int nt) {
     const char* e = getenv("LLMI_BATTN_MODE");
     const int forced = e ? atoi(e) : 0;
@@ -948,7 +962,7 @@ static int battn_path(int g, int n_head, int head_dim, int kv_bound, int nt) {
     if (forced == 2 && split_ok) return 2;
     if (forced == 6 && dim_ok) return 6;
     if (forced == 7 && g <= 8) return 7;
-    if (dim_ok && nt <= 3) return 6;
+    if (dim_ok && (nt <= 3 || kv_bound <= 512)) return 6;
     if (split_ok && (g <= 4 ? kv_bound <= 2048 : kv_bound <= 1024)) return 2;
     if (dim_ok) return 6;
     return g <= 8 ? 7 : (split_ok ? 2 : 0);
@@ -962,11 +976,12 @@ hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_
     if (path == 6) {
         const int p = kv_bound <= 64 ? 1 : kv_bound <= 128 ? 2 : kv_bound <= 256 ? 4 : kv_bound <= 512 ? 8
                     : kv_bound <= 768 ? 12 : 16;
-        const int sd = attn_d_slices(n_head, head_dim);
+        const int sd = battn_slices(n_head, head_dim, kv_bound, nt);
 #define LLMI_BATTD(D_, P_, S_) \
         if (head_dim == D_ && p == P_ && sd == S_) { hipLaunchKernelGGL((k_battn_d<D_, P_, S_>), dim3(n_head * S_, nt), dim3(512), 0, s, b, g, n_head_kv, kv_bound); return hipGetLastError(); }
 #define LLMI_BATTD_P(D_, S_) LLMI_BATTD(D_, 1, S_) LLMI_BATTD(D_, 2, S_) LLMI_BATTD(D_, 4, S_) LLMI_BATTD(D_, 8, S_) LLMI_BATTD(D_, 12, S_) LLMI_BATTD(D_, 16, S_)
-        LLMI_BATTD_P(128, 2) LLMI_BATTD_P(128, 4) LLMI_BATTD_P(128, 8) LLMI_BATTD_P(64, 2) LLMI_BATTD_P(64, 4) LLMI_BATTD_P(64, 8)
+        LLMI_BATTD_P(128, 1) LLMI_BATTD_P(128, 2) LLMI_BATTD_P(128, 4) LLMI_BATTD_P(128, 8)
+        LLMI_BATTD_P(64, 1) LLMI_BATTD_P(64, 2) LLMI_BATTD_P(64, 4) LLMI_BATTD_P(64, 8)
 #undef LLMI_BATTD_P
 #undef LLMI_BATTD
         return hipErrorInvalidValue;
