@@ -620,10 +620,10 @@ __device__ __forceinline__ void bmd_w(BmStage<T, NW>& st, const uint8_t* wb, int
     }
 }
 
+// the persistent tile loop of one k_bmd workgroup: tiles tile0, tile0 + stride, ... < ntiles
 template <int T, int EPI>
-__global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
-                                              int ntiles) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
+                                         int ntiles, int tile0, int stride, uint8_t* smem) {
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
     constexpr int NC = T == T_Q6_K ? 8 : 9;
     constexpr int kBuf = kBmW * NW * 9 * 32;        // float4 of a round's terms
@@ -632,7 +632,7 @@ __global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const
     uint8_t* Wb = (uint8_t*)(G + NW * 9 * 32);
     const int wave = uniform((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const int S = A.cols >> 8, R = (S + kBmW - 1) / kBmW;
-    int tile = blockIdx.x;
+    int tile = tile0;
     if (tile >= ntiles) return;
     int si, row0;
     RowPtr rp[NW];
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const
         int tn = tile, rn = rho + 1;
         if (rn == R) {
             rn = 0;
-            tn = tile + gridDim.x;
+            tn = tile + stride;
         }
         const bool has_next = tn < ntiles;
         int sin, row0n;
@@ -709,6 +709,22 @@ __global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const
 #pragma unroll
         for (int wi = 0; wi < NW; ++wi) rp[wi] = rpn[wi];
     }
+}
+template <int T, int EPI>
+__global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
+                                              int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    bmd_body<T, EPI>(A, aq, abf, ad, nt, ntiles, blockIdx.x, gridDim.x, smem);
+}
+// A QKV whose attn_v rows have another type (Llama-3 Q4_K_M: Q6_K in half the layers): both
+// type groups in ONE launch, workgroups [0, w1) on the A1 tiles (type T), the rest on A2's
+// (type T2) -- one launch instead of two, no second resident grid competing for the CUs
+template <int T, int T2>
+__global__ __launch_bounds__(kBmT) void k_bmd2(MVArgs A1, MVArgs A2, const uint8_t* aq, const uint8_t* abf, const float* ad,
+                                               int nt, int ntiles1, int ntiles2, int w1) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if ((int)blockIdx.x < w1) bmd_body<T, EPI_QKV>(A1, aq, abf, ad, nt, ntiles1, blockIdx.x, w1, smem);
+    else bmd_body<T2, EPI_QKV>(A2, aq, abf, ad, nt, ntiles2, blockIdx.x - w1, gridDim.x - w1, smem);
 }
 
 // ---- launchers -----------------------------------------------------------------------------
@@ -891,6 +907,43 @@ static hipError_t bmm_launch(const MVArgs& a, const void* aq, const void* abf, c
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBmT), lds, s, a, (const uint8_t*)aq, (const uint8_t*)abf, ad, nt, ntiles);
 #endif
     return hipGetLastError();
+}
+
+template <int T, int T2>
+static hipError_t bmm2_launch(const MVArgs& a1, const MVArgs& a2, const void* aq, const void* abf, const float* ad, int nt,
+                              hipStream_t s) {
+    auto k = k_bmd2<T, T2>;
+    const size_t lds = (size_t)(kBmW + 1) * 9 * 32 * 16 + std::max(bmd_wbytes<T, 1>(), bmd_wbytes<T2, 1>());
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int cap = bmm_cap((const void*)k, lds);
+    int r1 = 0, r2 = 0;
+    for (int i = 0; i < a1.nseg; ++i) r1 += a1.seg[i].rows;
+    for (int i = 0; i < a2.nseg; ++i) r2 += a2.seg[i].rows;
+    const int nt1 = r1 / 16, nt2 = r2 / 16;
+    if (nt1 < 1 || nt2 < 1 || cap < 2) return hipErrorInvalidValue;
+    // workgroups dealt by weight bytes, each group no more than its tiles
+    const double b1 = (double)nt1 * block_bytes(T), b2 = (double)nt2 * block_bytes(T2);
+    int w1 = (int)(cap * b1 / (b1 + b2) + 0.5);
+    w1 = std::max(1, std::min(std::min(w1, cap - 1), nt1));
+    const int w2 = std::max(1, std::min(cap - w1, nt2));
+    hipLaunchKernelGGL(k, dim3(w1 + w2), dim3(kBmT), lds, s, a1, a2, (const uint8_t*)aq, (const uint8_t*)abf, ad, nt, nt1, nt2, w1);
+    return hipGetLastError();
+}
+// LLMI_BMM2 (A/B): 1 mixed-type QKV in one k_bmd2 launch (default), 0 two launches
+static int bmm2_on() {
+    const char* e = getenv("LLMI_BMM2");
+    return e ? atoi(e) : 1;
+}
+hipError_t launch_bmm_qkv2(const MVArgs& a1, const MVArgs& a2, int nt, const void* aq, const void* abf, const float* ad,
+                           hipStream_t s) {
+    if (nt < 1 || nt > kMaxBatch || !bmm2_on() || !bmm_dma() || !bmm_ok(a1, EPI_QKV) || !bmm_ok(a2, EPI_QKV) ||
+        a1.cols != a2.cols)
+        return hipErrorNotSupported;
+    const int t1 = a1.seg[0].type, t2 = a2.seg[0].type;
+    if (t1 == T_Q4_K && t2 == T_Q6_K) return bmm2_launch<T_Q4_K, T_Q6_K>(a1, a2, aq, abf, ad, nt, s);
+    if (t1 == T_Q4_K && t2 == T_Q5_K) return bmm2_launch<T_Q4_K, T_Q5_K>(a1, a2, aq, abf, ad, nt, s);
+    if (t1 == T_Q5_K && t2 == T_Q6_K) return bmm2_launch<T_Q5_K, T_Q6_K>(a1, a2, aq, abf, ad, nt, s);
+    return hipErrorNotSupported;
 }
 
 template <int T>

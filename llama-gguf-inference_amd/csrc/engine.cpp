@@ -779,8 +779,11 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m.layers[(size_t)l];
         qkv_quant = false;
-        // QKV + RoPE + f16 KV write, one launch per run of same-type segments
+        // QKV + RoPE + f16 KV write: one launch per run of same-type segments, or both type
+        // groups in one k_bmd2 launch (launch_bmm_qkv2) on the matrix cores
         const Seg qkv[3] = {seg_of(m, L.wq, 0), seg_of(m, L.wk, QD), seg_of(m, L.wv, QD + nk)};
+        MVArgs grp[3];
+        int ng = 0;
         for (int i = 0; i < 3;) {
             int j = i;
             MVArgs a = base;
@@ -790,9 +793,21 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
             a.cols = E; a.x = c.bx; a.x_stride = E; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps;
             a.y = c.bq; a.y_stride = QD; a.kc = c.kc0 + l * kv_layer; a.vc = c.vc0 + l * kv_layer; a.rope = c.rope;
             a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = QD; a.nk = nk; a.npairs = rows / 2;
-            BC(bmv(a, EPI_QKV, qkv_quant));
+            grp[ng++] = a;
             i = j;
         }
+        bool done = false;
+        if (ng == 2 && nt >= bmm_min_tokens() && bmm_ok(grp[0], EPI_QKV) && bmm_ok(grp[1], EPI_QKV)) {
+            BC(launch_pf_quant(c.bx, E, grp[0].nw, hp.eps, E, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream));
+            qkv_quant = true;
+            const hipError_t e2 = launch_bmm_qkv2(grp[0], grp[1], nt, c.baq, c.babf, c.bad, c.stream);
+            if (e2 != hipErrorNotSupported) {
+                BC(e2);
+                done = true;
+            }
+        }
+        if (!done)
+            for (int gi = 0; gi < ng; ++gi) BC(bmv(grp[gi], EPI_QKV, qkv_quant));
         BAttnArgs ba;
         const size_t scr = attn_scratch_floats(hp.n_head, c.n_ctx);
         for (int s = 0; s < nt; ++s) {

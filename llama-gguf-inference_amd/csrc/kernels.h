@@ -134,6 +134,10 @@ bool bmm_ok(const MVArgs& a, int epi);
 int bmm_min_tokens();
 // (abf: k_pf_quant's bsum fragments; the dmin chain's sumi runs on the MFMA)
 hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const void* abf, const float* ad, hipStream_t s);
+// a QKV of two type groups (a1: q/k rows, a2: the attn_v rows) in one k_bmd2 launch over the
+// same quantized activations; hipErrorNotSupported when the pair does not qualify
+hipError_t launch_bmm_qkv2(const MVArgs& a1, const MVArgs& a2, int nt, const void* aq, const void* abf, const float* ad,
+                           hipStream_t s);
 hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
                              hipStream_t s);
 size_t mvn_lds_bytes(int act, int cols, int nt);
