@@ -1141,7 +1141,8 @@ int g_pf_fa_noalloc = 0;               // prefill: never allocate k_pf_fa's scor
 #ifndef LLMI_PF_QUANT_BPC
 #define LLMI_PF_QUANT_BPC 2
 #endif
-int g_pf_quant_bpc = LLMI_PF_QUANT_BPC;  // k_pf_quant: 256-element blocks per workgroup when rows are split (0: never)
+// k_pf_quant: 256-element blocks per workgroup when rows are split (0: never); LLMI_PF_QUANT_BPC (A/B)
+int g_pf_quant_bpc = getenv("LLMI_PF_QUANT_BPC") ? atoi(getenv("LLMI_PF_QUANT_BPC")) : LLMI_PF_QUANT_BPC;
 int g_pf_quant_split_below = 64;  // ... i.e. below this many rows (batched decode)
 #ifndef LLMI_PF_XCD_MAP
 #define LLMI_PF_XCD_MAP 1
