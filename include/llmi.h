@@ -190,9 +190,23 @@ void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec
  * after its real predecessor: us[k] = mean device microseconds per launch of class k
  * (execution only, no launch gaps), bytes[k] = mean algorithmic HBM bytes per launch,
  * launches[k] = launches per step.  Consumes no tokens: the context is left ready to
- * decode `first` at pos0.  Classes: 0 embed, 1 qkv(+RoPE, KV write), 2 attention (1-4
- * kernels, timed as one), 3 attn_output(+residual), 4 ffn_gate_up(+SwiGLU), 5
- * ffn_down(+residual), 6 output(+argmax).  0 on success. */
+ * decode `first` at pos0.  Classes (arrays of LLMI_KERNEL_CLASSES): 0 embed, 1 qkv(+RoPE,
+ * KV write), 2 attention (1-4 kernels, timed as one), 3 attn_output(+residual), 4
+ * ffn_gate_up(+SwiGLU), 5 ffn_down(+residual), 6 output(+argmax), 7 layer engine (one
+ * persistent launch = attn_output + ffn_gate_up + ffn_down + the next layer's qkv; when it
+ * runs, classes 3-5 and all but layer 0's qkv have no launches).  0 on success. */
+#define LLMI_KERNEL_CLASSES 8
+/* Microbenchmark of the layer engine's weight stream (tools/lestream.py): GB/s of `iters`
+ * launches in which every CU streams its share of `bytes` at device pointer src (mode 0
+ * one LDS-DMA loader wave, asm; 1 the same by the compiler builtin; 2 / 3 two / four
+ * loader waves; 4 eight waves of plain 16-B loads).  < 0 on error. */
+double llmi_le_stream_bench(const void* src, int64_t bytes, int32_t mode, int32_t iters, int32_t nt);
+/* Timeline of one layer-engine launch (leng.hip): one eager step at (first, pos0) with
+ * layer `layer`'s launch writing s_memrealtime stamps (100 MHz) to out[block][wave][32]
+ * (n_out >= CUs * 256); the state is left ready to decode `first` at pos0.  Returns the
+ * grid size (CUs), < 0 on error.  Stamp layout: tools/letrace.py. */
+int32_t llmi_engine_trace(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t layer, uint64_t* out,
+                          int64_t n_out);
 int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t n_steps,
                              double* us, double* bytes, int32_t* launches);
 /* Test options (tests only; no environment variable reaches these): sets `name` to

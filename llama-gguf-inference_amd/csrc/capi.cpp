@@ -606,6 +606,46 @@ int32_t llmi_profile_kernels(struct llama_context* ctx, llama_token first, int32
 }
 
 
+int32_t llmi_engine_trace(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t layer, uint64_t* out,
+                          int64_t n_out) {
+    API_TRY
+    if (!ctx || !out) { set_err("llmi_engine_trace: bad arguments"); return -1; }
+    Context& c = ctx->c;
+    if (first < 0 || first >= c.m->hp.n_vocab || pos0 < 0 || pos0 >= c.n_ctx || layer < 0 || layer >= c.m->hp.n_layer) {
+        set_err("llmi_engine_trace: token/position/layer out of range");
+        return -1;
+    }
+    (void)hipSetDevice(c.m->device);
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.m->device);
+    const size_t n = (size_t)cus * 8 * 32;
+    if ((size_t)n_out < n) { set_err("llmi_engine_trace: out holds fewer than CUs x 256 stamps"); return -1; }
+    // one eager warm step, then one traced step at (first, pos0); the state is reset after
+    const int kv_bound = std::min(c.n_ctx, (pos0 / 256 + 1) * 256);
+    std::string err;
+    int rc = 0;
+    if (!c.le_trace && hipMalloc(&c.le_trace, n * 8) != hipSuccess) { set_err("llmi_engine_trace: hipMalloc"); return -3; }
+    (void)hipMemsetAsync(c.le_trace, 0, n * 8, c.stream);
+    bool ok = launch_state_set(c.st, first, pos0, c.stream) == hipSuccess && step_enqueue(c, kv_bound, err);
+    c.le_trace_layer = layer;
+    ok = ok && launch_state_set(c.st, first, pos0, c.stream) == hipSuccess && step_enqueue(c, kv_bound, err);
+    c.le_trace_layer = -1;
+    if (!ok || hipMemcpyAsync(out, c.le_trace, n * 8, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+        hipStreamSynchronize(c.stream) != hipSuccess) {
+        set_err("llmi_engine_trace: " + (err.empty() ? std::string("launch failed") : err));
+        rc = -4;
+    }
+    if (launch_state_set(c.st, first, pos0, c.stream) != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess)
+        if (rc == 0) { set_err("llmi_engine_trace: state reset failed"); rc = -4; }
+    c.n_past = pos0;
+    return rc == 0 ? cus : rc;
+    API_CATCH(-5)
+}
+
+double llmi_le_stream_bench(const void* src, int64_t bytes, int32_t mode, int32_t iters, int32_t nt) {
+    return le_stream_bench(src, (size_t)bytes, mode, iters, nt);
+}
+
 // numerics of this thread's kernel-level entry points (llmi_test_option "numerics")
 static thread_local int t_hook_numerics = 0;
 
@@ -630,6 +670,8 @@ int32_t llmi_test_option(const char* name, int32_t value) {
     else if (!strcmp(name, "pf_max_kv")) opt = &g_pf_max_kv;
     else if (!strcmp(name, "xspin_limit")) opt = &g_xspin_limit;
     else if (!strcmp(name, "xtag_skew")) opt = &g_xtag_skew;
+    else if (!strcmp(name, "engine")) opt = &g_le_on;      // layer engine on/off (contexts made after)
+    else if (!strcmp(name, "le_spin")) opt = &g_le_spin;   // layer engine's bounded-wait polls
     if (!opt) { set_err("llmi_test_option: unknown option"); return -1; }
     const int old = *opt;
     if (value >= 0) *opt = value;

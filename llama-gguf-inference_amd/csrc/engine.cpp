@@ -52,7 +52,7 @@ Context::~Context() {
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     for (auto& g : bgraphs) (void)hipGraphExecDestroy(g.second);
     void* bufs[] = {x, q, att, h, logits, scores, rope, kc0, vc0, st0, hist0, pf_tok, pf_x, pf_q, pf_att, pf_h, pf_aq, pf_abs, pf_ad, pf_abf, pf_wsc,
-                    bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad, babf};
+                    bx, bq, batt, bh, blogits, bscores, btpos, btseq, baq, babs, bad, babf, le_cnt, le_trace};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -406,6 +406,7 @@ bool context_init(Model* m, int n_ctx, bool use_graphs, int n_seq, Context& c, s
     HIPC(hipMalloc(&c.scores, attn_scratch_floats(hp.n_head, c.n_ctx) * 4));
     c.fault_dev = (unsigned*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx) + 2 * (size_t)hp.n_head * kXAttnMaxKV);
     HIPC(hipHostMalloc((void**)&c.fault_host, 16, hipHostMallocDefault));
+    HIPC(hipMalloc(&c.le_cnt, le_counter_bytes(hp.n_layer)));
     *c.fault_host = 0;
     if (n_seq < 1 || n_seq > 64) { err = "n_seq_max must be in [1, 64]"; return false; }
     c.n_seq = n_seq;
@@ -496,8 +497,9 @@ void context_fault_readback(Context& c) {
 
 bool context_fault_ok(Context& c, std::string& err) {
     if (*c.fault_host == 0) return true;
-    err = "an in-kernel bounded wait gave up (attention hand-off never completed; device fault word " +
-          std::to_string(*c.fault_host) + "); this call's outputs are invalid";
+    err = "an in-kernel bounded wait gave up (device fault word " + std::to_string(*c.fault_host) +
+          ": bit 0 attention hand-off, 0x100.. layer engine ring / edge / barrier / ring space); this call's "
+          "outputs are invalid";
     *c.fault_host = 0;
     (void)hipMemsetAsync(c.fault_dev, 0, 4, c.stream);
     (void)hipStreamSynchronize(c.stream);
@@ -613,38 +615,60 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
             }                                              \
         }                                                  \
     } while (0)
+    // layer engine (leng.hip): one persistent launch per layer for attn_output, gate/up,
+    // down and the next layer's QKV when the shapes qualify (LLMI_ENGINE=0: separate
+    // launches); its edge counters are zeroed once per step
+    const bool use_le = le_wanted() && c.le_cnt && !exp_skip && !exp_xfirst && !xq_for(0) && !xq_for(1) && !xq_for(2) &&
+                        !xq_for(3);
+    if (use_le && hipMemsetAsync(c.le_cnt, 0, le_counter_bytes(hp.n_layer), c.stream) != hipSuccess) {
+        err = "hipMemsetAsync(le_cnt) failed";
+        return false;
+    }
     LLMI_RUN(K_EMBED, launch_embed(ea, c.stream));
     if (P) P->add(K_EMBED, (double)m.tok_embd.bytes / hp.n_vocab + E * 4.0);
-    for (int l = 0; l < hp.n_layer; ++l) {
+    const int num = m.numerics;
+    // QKV + RoPE + KV write of layer l, grouped by activation kind: n launches' args
+    auto qkv_groups = [&](int l, MVArgs (&out)[3], double (&bytes)[3]) -> int {
         const Layer& L = m.layers[(size_t)l];
-        // --- QKV + RoPE + KV write (grouped by activation kind) ---
-        const int num = m.numerics;
         MVArgs a; a.xfirst = exp_xfirst >> 0 & 1; a.num = num; a.xq = xq_for(0);
         a.cols = E; a.x = c.x; a.nw = (const float*)(m.arena + L.attn_norm.off_a); a.eps = hp.eps; a.y = c.q;
         a.kc = c.kc + l * kv_layer; a.vc = c.vc + l * kv_layer; a.rope = c.rope; a.st = c.st;
         a.head_dim = D; a.n_rot = hp.n_rot; a.n_ctx = c.n_ctx; a.nq = nq; a.nk = nk;
         const Seg qkv[3] = {seg_of(m, L.wq, 0), seg_of(m, L.wk, nq), seg_of(m, L.wv, nq + nk)};
-        int i = 0;
+        int i = 0, n = 0;
         while (i < 3) {
             int j = i;
             a.nseg = 0;
             int rows = 0;
             while (j < 3 && act_kind(qkv[j].type) == act_kind(qkv[i].type)) { a.seg[a.nseg++] = qkv[j]; rows += qkv[j].rows; ++j; }
             a.npairs = rows / 2;
-            LLMI_RUN(K_QKV, launch_matvec(a, EPI_QKV, c.max_blocks, c.stream));
-            if (P) {
-                double b = 8.0 * E;
-                for (int k = i; k < j; ++k) {
-                    const DevMat& dm = k == 0 ? L.wq : k == 1 ? L.wk : L.wv;
-                    b += (double)dm.bytes + (k == 0 ? 4.0 * nq : 2.0 * nk);
-                }
-                P->add(K_QKV, b);
+            double b = 8.0 * E;
+            for (int k = i; k < j; ++k) {
+                const DevMat& dm = k == 0 ? L.wq : k == 1 ? L.wk : L.wv;
+                b += (double)dm.bytes + (k == 0 ? 4.0 * nq : 2.0 * nk);
             }
+            out[n] = a;
+            bytes[n++] = b;
             i = j;
         }
+        return n;
+    };
+    bool qkv_done = false;  // layer l's QKV already ran inside layer l-1's engine launch
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const Layer& L = m.layers[(size_t)l];
+        if (!qkv_done) {
+            MVArgs qg[3];
+            double qb[3];
+            const int nqg = qkv_groups(l, qg, qb);
+            for (int i = 0; i < nqg; ++i) {
+                LLMI_RUN(K_QKV, launch_matvec(qg[i], EPI_QKV, c.max_blocks, c.stream));
+                if (P) P->add(K_QKV, qb[i]);
+            }
+        }
+        qkv_done = false;
         // --- attention ---
         AttnArgs at;
-        at.q = c.q; at.kc = a.kc; at.vc = a.vc; at.scores = c.scores; at.out = c.att; at.st = c.st;
+        at.q = c.q; at.kc = c.kc + l * kv_layer; at.vc = c.vc + l * kv_layer; at.scores = c.scores; at.out = c.att; at.st = c.st;
         at.tmax = c.scores + (size_t)hp.n_head * c.n_ctx;
         at.n_ctx = c.n_ctx; at.scale = 1.0f / sqrtf((float)D);
         at.layer = l;
@@ -656,20 +680,49 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         // --- output projection + residual ---
         MVArgs o; o.xfirst = exp_xfirst >> 1 & 1; o.num = num; o.xq = xq_for(1);
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = nq; o.x = c.att; o.y = c.x; o.npairs = (E + 1) / 2;
-        LLMI_RUN(K_ATTN_OUT, launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
-        if (P) P->add(K_ATTN_OUT, (double)L.wo.bytes + 4.0 * nq + 8.0 * E);
+        const double o_bytes = (double)L.wo.bytes + 4.0 * nq + 8.0 * E;
         // --- gate/up + SwiGLU ---
         MVArgs gu; gu.xfirst = exp_xfirst >> 2 & 1; gu.num = num; gu.xq = xq_for(2);
         gu.seg[0] = seg_of(m, L.wg, 0); gu.seg[1] = seg_of(m, L.wu, 0); gu.nseg = 2;
         gu.cols = E; gu.x = c.x; gu.nw = (const float*)(m.arena + L.ffn_norm.off_a); gu.eps = hp.eps;
         gu.y = c.h; gu.npairs = hp.n_ff;
-        LLMI_RUN(K_FFN_GATE_UP, launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
-        if (P) P->add(K_FFN_GATE_UP, (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff);
+        const double gu_bytes = (double)(L.wg.bytes + L.wu.bytes) + 8.0 * E + 4.0 * hp.n_ff;
         // --- down + residual ---
         MVArgs dn; dn.xfirst = exp_xfirst >> 3 & 1; dn.num = num; dn.xq = xq_for(3);
         dn.seg[0] = seg_of(m, L.wd, 0); dn.nseg = 1; dn.cols = hp.n_ff; dn.x = c.h; dn.y = c.x; dn.npairs = (E + 1) / 2;
-        LLMI_RUN(K_FFN_DOWN, launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
-        if (P) P->add(K_FFN_DOWN, (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E);
+        const double dn_bytes = (double)L.wd.bytes + 4.0 * hp.n_ff + 8.0 * E;
+        bool engine_ran = false;
+        if (use_le && want(K_LAYER)) {
+            LeArgs la;
+            la.op[0] = o; la.op[1] = gu; la.op[2] = dn; la.nops = 3;
+            double lb = o_bytes + gu_bytes + dn_bytes;
+            if (l + 1 < hp.n_layer) {
+                MVArgs qn[3];
+                double qb[3];
+                if (qkv_groups(l + 1, qn, qb) == 1) { la.op[3] = qn[0]; la.nops = 4; lb += qb[0]; }
+            }
+            la.cnt = c.le_cnt + (size_t)l * (le_counter_bytes(1) / 4);
+            la.fault = c.fault_dev;
+            if (l == c.le_trace_layer) la.trace = c.le_trace;
+            const hipError_t ep = layer_engine_prepare(la);
+            if (ep == hipSuccess) {
+                LLMI_RUN(K_LAYER, launch_layer_engine(la, c.stream));
+                if (P) P->add(K_LAYER, lb);
+                engine_ran = true;
+                qkv_done = la.nops == 4;
+            } else if (ep != hipErrorNotSupported) {
+                err = "layer_engine_prepare: " + hip_err(ep);
+                return false;
+            }
+        }
+        if (!engine_ran) {
+            LLMI_RUN(K_ATTN_OUT, launch_matvec(o, EPI_ADD, c.max_blocks, c.stream));
+            if (P) P->add(K_ATTN_OUT, o_bytes);
+            LLMI_RUN(K_FFN_GATE_UP, launch_matvec(gu, EPI_SWIGLU, c.max_blocks, c.stream));
+            if (P) P->add(K_FFN_GATE_UP, gu_bytes);
+            LLMI_RUN(K_FFN_DOWN, launch_matvec(dn, EPI_ADD, c.max_blocks, c.stream));
+            if (P) P->add(K_FFN_DOWN, dn_bytes);
+        }
     }
     MVArgs lo;
     lo.num = m.numerics; lo.xq = xq_for(4);

@@ -57,7 +57,8 @@ struct Model {
 // Kernel-class timing (llmi_profile_kernels): step_enqueue with a Prof attached only
 // enqueues the launches of class `only` (all classes if -1), records their algorithmic
 // bytes per class and, when `timed`, arms an event pair (kernel start / end) on each.
-enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_NCLASS };
+enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_ATTN_OUT, K_FFN_GATE_UP, K_FFN_DOWN, K_OUTPUT, K_LAYER, K_NCLASS };
+// (K_LAYER: one layer-engine launch, leng.hip = attn_output + gate/up + down + next QKV)
 struct Prof {
     int only = -1;               // class filter (-1: every class)
     bool timed = false;          // arm an event pair around every filtered launch
@@ -120,6 +121,9 @@ struct Context {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     unsigned* fault_dev = nullptr;          // device fault word: a bounded in-kernel wait gave up
     unsigned* fault_host = nullptr;         // pinned copy, read back with every decode call
+    unsigned* le_cnt = nullptr;             // layer-engine edge counters (le_counter_bytes), zeroed per step
+    unsigned long long* le_trace = nullptr; // llmi_engine_trace: stamps of layer le_trace_layer's launch
+    int le_trace_layer = -1;
     double last_bytes = 0, last_us = 0;
     Prof* prof = nullptr;                   // non-null only inside llmi_profile_kernels
     // batched prefill scratch (allocated on first use; ubatches of <= pf_cap tokens)

@@ -92,6 +92,34 @@ struct MVArgs {
     int num = 0;                 // numerics: 0 ggml's generic order, 1 upstream's x86 association (mv_device.h)
 };
 
+// Layer engine (leng.hip): one persistent launch per decode layer runs up to kLeOps
+// matvecs in stream order -- attn_output + residual (EPI_ADD), ffn_gate+up + SwiGLU
+// (EPI_SWIGLU), ffn_down + residual (EPI_ADD), the next layer's QKV (EPI_QKV) -- with the
+// weights streamed into an LDS ring ahead of the activation hand-offs between them.
+constexpr int kLeOps = 4;
+struct LeArgs {
+    MVArgs op[kLeOps];           // set like launch_matvec's (geometry filled by the launcher)
+    int nops = 0;                // 3 (last layer: no next QKV) or 4
+    unsigned* cnt = nullptr;     // this layer's edge counters [kLeOps][8 shards][16 words], zero at launch
+    unsigned* fault = nullptr;   // context fault word: a bounded in-kernel wait gave up
+    int spin_limit = 0;          // polls before a wait gives up (0: default)
+    int nt = 1;                  // weight DMA nontemporal (MI355X_MICROARCH.md nt-weights)
+    // LDS carve (set by the launcher)
+    int npieces = 0, img_off0 = 0, img_off1 = 0, fold_off = 0, ring_off = 0, act = -1;
+    int lag = 40;                // DMA pieces kept in flight past the published prefix (16/24/32/40/48)
+    int exp = 0;                 // LLMI_LE_EXP experiments (results garbage): 1 no math, 2 no edges / images
+    unsigned long long* trace = nullptr;  // llmi_engine_trace: [block][wave][32] s_memrealtime stamps
+};
+// bytes of the edge counters of n_layer layers (one memset per step zeroes them)
+size_t le_counter_bytes(int n_layer);
+// fills the geometry and LDS carve; hipErrorNotSupported: shapes / types / LDS / residency
+// the engine does not take (the caller runs the layer as separate launches)
+hipError_t layer_engine_prepare(LeArgs& a);
+hipError_t launch_layer_engine(const LeArgs& a, hipStream_t s);  // a prepared
+double le_stream_bench(const void* src, size_t bytes, int mode, int iters, int nt);  // GB/s (tools/lestream.py)
+bool le_wanted();                 // LLMI_ENGINE (default 1) / test option "engine"
+extern int g_le_on, g_le_spin;    // test options: engine on/off, spin limit
+
 struct AttnArgs {
     const float* q = nullptr;      // f32[H*D] (roped)
     const uint16_t* kc = nullptr;  // layer base

@@ -1216,7 +1216,9 @@ __device__ __forceinline__ LaneUnit lane_unit(const TaskGeo& g, const Sub& b, co
 // After the lanes' unit terms: store, fold, and on the row set's last sub-item the row
 // results and the epilogue (lane r' < R handles row r' of the task).
 // (X86: the lane's terms are already in F, unit_store_x86; tm is unused)
-template <int ACT, int EPI, class MA, int X86 = 0>
+// (WT: write-through epilogue stores, for outputs handed to other workgroups of the same
+// launch: the layer engine, leng.hip)
+template <int ACT, int EPI, class MA, int X86 = 0, bool WT = false>
 __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo& g, int s, const Sub& b, const Seg& sg,
                                            const float (&tm)[9], const LaneUnit& lu, int r, int ul, float& acc,
                                            float& vg, int pos, unsigned long long& best) {
@@ -1242,12 +1244,12 @@ __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo&
             ref.type = sg.type;
             if constexpr (EPI == EPI_SWIGLU) {
                 if (s < g.nj) vg = v;
-                else epilogue<EPI, false, MA, true, X86>(A, ref, row, PairSum{vg, v}, pos, best);
+                else epilogue<EPI, WT, MA, true, X86>(A, ref, row, PairSum{vg, v}, pos, best);
             } else if constexpr (EPI == EPI_QKV) {
                 ref.vb = 1;  // RoPE pairs (row, row + 1): R and every segment start are even
-                if ((lane & 1) == 0) epilogue<EPI, false, MA, true, X86>(A, ref, row, PairSum{v, final_of(lane + 1)}, pos, best);
+                if ((lane & 1) == 0) epilogue<EPI, WT, MA, true, X86>(A, ref, row, PairSum{v, final_of(lane + 1)}, pos, best);
             } else {
-                epilogue<EPI, false, MA, true, X86>(A, ref, row, PairSum{v, 0.f}, pos, best);
+                epilogue<EPI, WT, MA, true, X86>(A, ref, row, PairSum{v, 0.f}, pos, best);
             }
         }
     }

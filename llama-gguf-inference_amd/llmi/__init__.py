@@ -380,18 +380,29 @@ class Context:
         lib().llmi_last_step_stats(self._h, C.byref(b), C.byref(u))
         return b.value, u.value
 
-    KERNEL_CLASSES = ("embed", "qkv", "attention", "attn_output", "ffn_gate_up", "ffn_down", "output")
+    KERNEL_CLASSES = ("embed", "qkv", "attention", "attn_output", "ffn_gate_up", "ffn_down", "output", "layer")
 
     def profile_kernels(self, first: int, pos0: int, n_steps: int) -> dict:
         """Per-kernel-class mean kernel execution time / algorithmic bytes per launch:
         each class's launches of n_steps steps at pos0, every launch bracketed by HIP
         events recorded at kernel start/end (llmi_profile_kernels).  Consumes no tokens."""
-        us, by, nl = (C.c_double * 7)(), (C.c_double * 7)(), (C.c_int32 * 7)()
+        n = len(self.KERNEL_CLASSES)
+        us, by, nl = (C.c_double * n)(), (C.c_double * n)(), (C.c_int32 * n)()
         if lib().llmi_profile_kernels(self._h, int(first), int(pos0), int(n_steps), us, by, nl) != 0:
             raise LlmiError(last_error())
         return {k: {"us": us[i], "bytes": by[i], "launches_per_step": nl[i],
                     "GBps": (by[i] / (us[i] * 1e-6) / 1e9) if us[i] > 0 else 0.0}
                 for i, k in enumerate(self.KERNEL_CLASSES)}
+
+    def engine_trace(self, first: int, pos0: int, layer: int) -> np.ndarray:
+        """llmi_engine_trace: s_memrealtime stamps (10 ns ticks) of layer `layer`'s layer-engine
+        launch in one eager step at pos0, shaped [CUs][8 waves][32] (tools/letrace.py)."""
+        n = 256 * 8 * 32 * 4
+        out = (C.c_uint64 * n)()
+        g = int(lib().llmi_engine_trace(self._h, int(first), int(pos0), int(layer), out, n))
+        if g < 0:
+            raise LlmiError(last_error())
+        return np.ctypeslib.as_array(out)[: g * 8 * 32].reshape(g, 8, 32).copy()
 
     def kv_clear(self) -> None:
         lib().llama_kv_self_clear(self._h)

@@ -102,6 +102,8 @@ SIGNATURES = {
     "llmi_model_upload_s": (C.c_double, [_P]),
     "llmi_last_step_stats": (None, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "llmi_test_option": (C.c_int32, [C.c_char_p, C.c_int32]),
+    "llmi_le_stream_bench": (C.c_double, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32]),
+    "llmi_engine_trace": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.c_int64]),
     "llmi_bytes_per_token": (C.c_double, [_P, C.c_int32]),
     "llmi_profile_kernels": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_double),
                                          C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
