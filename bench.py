@@ -109,6 +109,14 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, obj) -> list:
+        """Every rank's `obj`, in rank order (all_gather_object; [obj] on one rank)."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def bcast_bytes(self, b: bytes | None) -> bytes:
         if not self.dist:
             return b
@@ -147,19 +155,35 @@ def timed_decode(engine, dist: Dist, steps: int, warmup: int) -> tuple[float, fl
     return dt, dist.max(dt)
 
 
-def load_replica(path: str, dist: Dist, rccl_unique_id, load_fanout, load_plain):
+def load_replica(path: str, dist: Dist, rccl_unique_id, load_fanout, load_plain, arena_hash=None):
     """This rank's replica of the model.  One rank: load_plain(path, gpu).
     Several: rank 0 makes the RCCL unique id, the torch.distributed group broadcasts it,
     and every rank calls load_fanout(path, gpu, uid, nranks, rank) (llmi_model_load_fanout):
     rank 0 uploads the GGUF and the arena reaches the other ranks over xGMI in 256 MB
-    pieces pipelined behind that upload.  Returns (model, fan-out seconds of this rank,
-    0.0 on one rank)."""
+    pieces pipelined behind that upload.  Then every rank's (load error, arena_hash(model))
+    is gathered over the process group: if any rank failed or any replica's hash differs
+    from rank 0's, EVERY rank raises (and exits non-zero) instead of timing garbage or
+    hanging in the next barrier.  Returns (model, fan-out seconds of this rank, 0.0 on one
+    rank)."""
     if dist.world <= 1:
         return load_plain(path, dist.local_rank), 0.0
     uid = dist.bcast_bytes(rccl_unique_id() if dist.rank == 0 else None)
     t = time.perf_counter()
-    m = load_fanout(path, dist.local_rank, uid, dist.world, dist.rank)
-    return m, time.perf_counter() - t
+    m, err, h = None, None, None
+    try:
+        m = load_fanout(path, dist.local_rank, uid, dist.world, dist.rank)
+        if arena_hash is not None:
+            h = arena_hash(m)
+    except Exception as e:  # reported to every rank below
+        err = f"{type(e).__name__}: {e}"
+    dt = time.perf_counter() - t
+    views = dist.gather((err, h))
+    failed = [(r, e) for r, (e, _) in enumerate(views) if e]
+    if failed:
+        raise RuntimeError(f"replica load failed on rank(s) {failed}")
+    if len({hv for _, hv in views}) > 1:
+        raise RuntimeError(f"replica arena hashes differ: {[hv for _, hv in views]}")
+    return m, dt
 
 
 class LlmiEngine:
@@ -190,7 +214,8 @@ class LlmiEngine:
         self.model, self.fanout_s = load_replica(
             path, dist, llmi.rccl_unique_id,
             lambda p, g, uid, nr, r: llmi.Model.load_fanout(p, g, uid, nr, r, numerics=num),
-            lambda p, g: llmi.Model(p, main_gpu=g, numerics=num))
+            lambda p, g: llmi.Model(p, main_gpu=g, numerics=num),
+            arena_hash=lambda m: m.arena_hash())
         self.load_s = time.perf_counter() - t
         last = window_start(args.prompt, args.steps, args.warmup) + args.steps
         n_ctx = ((max(last, args.prompt + C2_DECODE) + args.profile_steps + 2 + 255) // 256) * 256

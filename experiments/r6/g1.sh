@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out/r6a
+timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r6a/engine_tests.log 2>&1 || { tail -30 gpurun_out/r6a/engine_tests.log; exit 1; }
+tail -3 gpurun_out/r6a/engine_tests.log
+bash tools/le_bench.sh 2>&1 | tee gpurun_out/r6a/le_bench.txt || exit 1
+for p in tinyllama-q8_0 llama3-8b-q4km; do
+  LLMI_ENGINE=1 LE_PRESET=$p timeout -k 10 200 python -u tools/letrace.py > gpurun_out/r6a/letrace_$p.txt 2>&1 || exit 1
+done
+cat gpurun_out/r6a/letrace_*.txt

@@ -52,8 +52,10 @@ struct llama_model_params {
     int32_t numerics;      /* llmi: the fp32 association every kernel reproduces bit for bit,
                               fixed at load (the weights' device byte order depends on it):
                               LLMI_NUMERICS_GENERIC (default) ggml's generic scalar order;
-                              LLMI_NUMERICS_X86 upstream's x86 AVX2 build, the reference's
-                              NGL=0 path (Dockerfile.cpu:11) — DESIGN.md §5 */
+                              LLMI_NUMERICS_X86 the oracle's model of upstream's x86 AVX2
+                              association (non-repacked Q4_K, non-flash attention).  Whether
+                              the reference's CPU image (Dockerfile.cpu:11: AVX-512 variant,
+                              CPU_REPACK, -fa auto) computes these bits is unpinned — DESIGN.md §5 */
 };
 #define LLMI_NUMERICS_GENERIC 0
 #define LLMI_NUMERICS_X86 1
@@ -203,7 +205,7 @@ void llmi_last_step_stats(struct llama_context* ctx, double* bytes, double* usec
 double llmi_le_stream_bench(const void* src, int64_t bytes, int32_t mode, int32_t iters, int32_t nt);
 /* Timeline of one layer-engine launch (leng.hip): one eager step at (first, pos0) with
  * layer `layer`'s launch writing s_memrealtime stamps (100 MHz) to out[block][wave][32]
- * (n_out >= CUs * 256); the state is left ready to decode `first` at pos0.  Returns the
+ * (n_out >= CUs * 512: [CU][16 waves][32]); the state is left ready to decode `first` at pos0.  Returns the
  * grid size (CUs), < 0 on error.  Stamp layout: tools/letrace.py. */
 int32_t llmi_engine_trace(struct llama_context* ctx, llama_token first, int32_t pos0, int32_t layer, uint64_t* out,
                           int64_t n_out);
@@ -233,6 +235,12 @@ double llmi_bytes_per_token(const struct llama_model* model, int32_t n_kv);
 int32_t llmi_prefill_supported(const struct llama_model* model);
 /* Device weight arena (for RCCL broadcast by a caller that owns the communicator). */
 int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64_t* bytes);
+/* Replica check: an order-independent 64-bit hash of the model's device arena (sum over
+ * 8-byte words i mod 2^64 of splitmix64's finalizer of word_i ^ (i * 0x9E3779B97F4A7C15),
+ * the last word zero-padded).  Equal arenas give equal hashes on any device.  0 ok. */
+int32_t llmi_model_arena_hash(const struct llama_model* model, uint64_t* out);
+/* The same hash of `bytes` of any device memory (test hook; synchronous). */
+int32_t llmi_device_hash(const void* dev_ptr, uint64_t bytes, uint64_t* out);
 /* In-process replica fan-out: copies model's arena to devices[0..n) with an RCCL
  * broadcast over xGMI and returns one model handle per device (out[i]). 0 on success;
  * -1 (nothing allocated) for bad arguments, an out-of-range device, or a device listed
@@ -243,8 +251,10 @@ int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_
  * uploaded weights, ranks 1..n-1 loaded the same GGUF with params.no_upload.  Every rank
  * calls llmi_model_fanout with the same 128-byte RCCL unique id (made by rank 0 with
  * llmi_rccl_unique_id and shared by any out-of-band channel); the arena is broadcast
- * from rank 0 over xGMI as 256 MB ncclBroadcast pieces on a dedicated stream.  Returns
- * 0 on success. */
+ * from rank 0 over xGMI as 256 MB ncclBroadcast pieces on a dedicated stream.  After
+ * the pieces, rank 0's status word and arena hash go to every rank (one more broadcast):
+ * a rank whose root failed, or whose arena hash differs from the root's, fails too.
+ * Returns 0 on success, -6 when the root failed or the hashes differ (llmi_last_error). */
 int32_t llmi_rccl_unique_id(uint8_t* out, int32_t n);
 int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t nranks, int32_t rank);
 
@@ -253,7 +263,9 @@ int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t
  * arena prefix covering it.  llmi_model_load_fanout: every rank calls it with the same
  * RCCL unique id; rank 0 reads and uploads the GGUF, the others only plan the layout and
  * receive.  llmi_model_load_replicated: one process, the model on params.main_gpu plus a
- * replica on each of `devices` (out[i]), as llmi_replicate.  NULL on error. */
+ * replica on each of `devices` (out[i]), as llmi_replicate.  Both end with the status +
+ * hash check above (a rank whose root's upload failed returns NULL with llmi_last_error
+ * set, instead of a partly written arena).  NULL on error. */
 struct llama_model* llmi_model_load_fanout(const char* path, struct llama_model_params params, const uint8_t* uid,
                                            int32_t nranks, int32_t rank);
 struct llama_model* llmi_model_load_replicated(const char* path, struct llama_model_params params,

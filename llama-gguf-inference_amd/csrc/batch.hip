@@ -642,7 +642,9 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
     BmStage<T, NW> cur;
     bm_load<T, NW>(cur, rp, aq, abf, ad, wave < S ? wave : S - 1, S, nt, 0, false);
     bmd_dma<T, EPI, NW>(A, si, row0, 0, Wb);
-    __syncthreads();  // vmcnt(0): round 0 in LDS
+    // explicit: a workgroup barrier alone need not wait for this wave's LDS-DMA writes
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // round 0 in LDS
     int rho = 0;
     for (;;) {
         const int s = rho * kBmW + wave;
@@ -673,7 +675,8 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
                             make_float4(tm[wi][c][0], tm[wi][c][1], tm[wi][c][2], tm[wi][c][3]);
             }
         }
-        __syncthreads();  // the terms in LDS; vmcnt(0) retires the next round's DMA
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next round's DMA has landed ...
+        __syncthreads();  // ... in every wave; the terms in LDS
         const int nv = S - rho * kBmW < kBmW ? S - rho * kBmW : kBmW;
         const bool last = rho == R - 1;
 #pragma unroll
@@ -891,7 +894,9 @@ static hipError_t bmm_launch(const MVArgs& a, const void* aq, const void* abf, c
     auto k = dma ? k_bmd<T, EPI> : k_bmm<T, EPI>;
     const size_t lds = dma ? (size_t)(kBmW + 1) * NW * 9 * 32 * 16 + bmd_wbytes<T, NW>()
                            : (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    // shape / occupancy rejections are hipErrorNotSupported: the caller then runs the two
+    // type groups as separate launches (engine.cpp) instead of failing the step
+    if (lds > 160 * 1024) return hipErrorNotSupported;
     const int cap = bmm_cap((const void*)k, lds);
     int rows = 0;
     if (EPI == EPI_SWIGLU) rows = a.seg[0].rows;
@@ -914,13 +919,15 @@ static hipError_t bmm2_launch(const MVArgs& a1, const MVArgs& a2, const void* aq
                               hipStream_t s) {
     auto k = k_bmd2<T, T2>;
     const size_t lds = (size_t)(kBmW + 1) * 9 * 32 * 16 + std::max(bmd_wbytes<T, 1>(), bmd_wbytes<T2, 1>());
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    // shape / occupancy rejections are hipErrorNotSupported: the caller then runs the two
+    // type groups as separate launches (engine.cpp) instead of failing the step
+    if (lds > 160 * 1024) return hipErrorNotSupported;
     const int cap = bmm_cap((const void*)k, lds);
     int r1 = 0, r2 = 0;
     for (int i = 0; i < a1.nseg; ++i) r1 += a1.seg[i].rows;
     for (int i = 0; i < a2.nseg; ++i) r2 += a2.seg[i].rows;
     const int nt1 = r1 / 16, nt2 = r2 / 16;
-    if (nt1 < 1 || nt2 < 1 || cap < 2) return hipErrorInvalidValue;
+    if (nt1 < 1 || nt2 < 1 || cap < 2) return hipErrorNotSupported;
     // workgroups dealt by weight bytes, each group no more than its tiles
     const double b1 = (double)nt1 * block_bytes(T), b2 = (double)nt2 * block_bytes(T2);
     int w1 = (int)(cap * b1 / (b1 + b2) + 0.5);

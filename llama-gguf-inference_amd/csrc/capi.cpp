@@ -618,8 +618,8 @@ int32_t llmi_engine_trace(struct llama_context* ctx, llama_token first, int32_t 
     (void)hipSetDevice(c.m->device);
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.m->device);
-    const size_t n = (size_t)cus * 8 * 32;
-    if ((size_t)n_out < n) { set_err("llmi_engine_trace: out holds fewer than CUs x 256 stamps"); return -1; }
+    const size_t n = (size_t)cus * 16 * 32;
+    if ((size_t)n_out < n) { set_err("llmi_engine_trace: out holds fewer than CUs x 512 stamps"); return -1; }
     // one eager warm step, then one traced step at (first, pos0); the state is reset after
     const int kv_bound = std::min(c.n_ctx, (pos0 / 256 + 1) * 256);
     std::string err;
@@ -747,6 +747,40 @@ int32_t llmi_model_arena(const struct llama_model* model, void** dev_ptr, uint64
     return 0;
 }
 
+// synchronous hash of device memory on `device` (launch_arena_hash, kernels.hip)
+static bool device_hash(int device, const void* p, size_t bytes, uint64_t* out, std::string& err) {
+    if (hipSetDevice(device) != hipSuccess) { err = "hipSetDevice"; return false; }
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 8) != hipSuccess) { err = "hipMalloc (hash)"; return false; }
+    hipError_t e = launch_arena_hash(p, bytes, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) { err = std::string("arena hash: ") + hipGetErrorString(e); return false; }
+    return true;
+}
+
+int32_t llmi_model_arena_hash(const struct llama_model* model, uint64_t* out) {
+    API_TRY
+    if (!model || !out || !model->m.arena) { set_err("llmi_model_arena_hash: bad arguments"); return -1; }
+    std::string err;
+    if (!device_hash(model->m.device, model->m.arena, model->m.arena_bytes, out, err)) { set_err(err); return -2; }
+    return 0;
+    API_CATCH(-5)
+}
+
+int32_t llmi_device_hash(const void* dev_ptr, uint64_t bytes, uint64_t* out) {
+    API_TRY
+    if (!dev_ptr || !out) { set_err("llmi_device_hash: bad arguments"); return -1; }
+    hipPointerAttribute_t at{};
+    int dev = 0;
+    if (hipPointerGetAttributes(&at, dev_ptr) == hipSuccess && at.device >= 0) dev = at.device;
+    else (void)hipGetDevice(&dev);
+    std::string err;
+    if (!device_hash(dev, dev_ptr, (size_t)bytes, out, err)) { set_err(err); return -2; }
+    return 0;
+    API_CATCH(-5)
+}
+
 // ---- replica fan-out ------------------------------------------------
 // The arena goes out in kFanoutChunk (256 MB) pieces on real streams.  When the source is
 // still uploading (llmi_model_load_fanout / llmi_model_load_replicated), piece k is issued
@@ -827,6 +861,72 @@ struct Fanout {
         }
         return ok;
     }
+    // After finish(): the root's {status, arena hash} goes to every rank of the
+    // communicator (one more broadcast, so every rank leaves the fan-out together), and
+    // each rank compares its own arena's hash with the root's.  root_ok: the caller's own
+    // view of the root's load (upload + pieces).  Returns whether THIS process's ranks
+    // hold the root's bytes; err says why not.  (a rank used to return
+    // success with a partly written arena when the root's upload failed.)
+    bool verify(bool root_ok, std::string& err) {
+        if (comm.empty()) return root_ok;
+        const size_t n = dev.size();
+        std::vector<uint64_t> own(n, 0);
+        bool hashed = true;
+        for (size_t r = 0; r < n; ++r) {
+            std::string e;
+            if (!device_hash(dev[r], buf[r], bytes, &own[r], e)) { hashed = false; err = e; }
+        }
+        std::vector<unsigned long long*> w(n, nullptr);
+        bool alloc = true;
+        for (size_t r = 0; r < n; ++r) {
+            (void)hipSetDevice(dev[r]);
+            if (hipMalloc(&w[r], 16) != hipSuccess) alloc = false;
+        }
+        // the root's words: status (0 ok), its arena hash; other ranks' buffers are overwritten
+        const bool is_root = rank0;
+        uint64_t msg[2] = {(root_ok && hashed) ? 0ull : 1ull, own[0]};
+        for (size_t r = 0; r < n && alloc; ++r) {
+            (void)hipSetDevice(dev[r]);
+            if (hipMemcpy(w[r], msg, 16, hipMemcpyHostToDevice) != hipSuccess) alloc = false;
+        }
+        bool ok_all = alloc;
+        if (alloc) {
+            ncclResult_t nr = n > 1 ? ncclGroupStart() : ncclSuccess;
+            for (size_t r = 0; r < n && nr == ncclSuccess; ++r) {
+                (void)hipSetDevice(dev[r]);
+                nr = ncclBroadcast(w[r], w[r], 16, ncclUint8, 0, comm[r], st[r]);
+            }
+            if (n > 1) {
+                const ncclResult_t ne = ncclGroupEnd();
+                if (nr == ncclSuccess) nr = ne;
+            }
+            if (nr != ncclSuccess) { ok_all = false; err = "status broadcast failed"; }
+            for (size_t r = 0; r < n && ok_all; ++r) {
+                (void)hipSetDevice(dev[r]);
+                uint64_t got[2] = {1, 0};
+                if (hipStreamSynchronize(st[r]) != hipSuccess ||
+                    hipMemcpy(got, w[r], 16, hipMemcpyDeviceToHost) != hipSuccess) {
+                    ok_all = false;
+                    err = "status read back failed";
+                } else if (got[0] != 0) {
+                    ok_all = false;
+                    if (err.empty()) err = is_root && r == 0 ? "the upload failed" : "the root rank's upload failed";
+                } else if (!hashed || got[1] != own[r]) {
+                    ok_all = false;
+                    if (err.empty()) err = "arena hash of rank-local replica differs from the root's";
+                }
+            }
+        } else if (err.empty()) {
+            err = "status buffers";
+        }
+        for (size_t r = 0; r < n; ++r) {
+            (void)hipSetDevice(dev[r]);
+            if (w[r]) (void)hipFree(w[r]);
+        }
+        (void)hipSetDevice(dev[0]);
+        return ok_all;
+    }
+    bool rank0 = true;  // entry 0 is the communicator's root (in-process fan-outs, rank 0)
     // the model_load hook of the root: record the prefix on the upload stream, issue what it covers
     UploadHook hook() {
         return [this](size_t prefix_end, hipStream_t us) -> bool {
@@ -901,7 +1001,8 @@ int32_t llmi_replicate(struct llama_model* model, const int32_t* devices, int32_
     {
         Fanout F;
         if (!replica_setup(model->m, devices, n, reps, F, err)) rc = -2;
-        else if (!F.finish()) { err = "ncclBroadcast failed"; rc = -4; }
+        else if (!F.finish()) { err = "ncclBroadcast failed"; rc = -4; (void)F.verify(false, err); }
+        else if (!F.verify(true, err)) rc = -6;
     }
     if (rc) {
         set_err("llmi_replicate: " + err);
@@ -945,7 +1046,14 @@ struct llama_model* llmi_model_load_replicated(const char* path, struct llama_mo
         if (ok) {
             const UploadHook h = F.hook();
             ok = model_upload(m->m, err, n > 0 ? &h : nullptr);
-            if (ok && n > 0 && !F.finish()) { err = "ncclBroadcast failed"; ok = false; }
+            if (n > 0) {
+                // every piece and the status go out even after a failed upload (every
+                // replica learns it), then each replica's hash is checked against the root's
+                const bool pieces = F.finish();
+                if (ok && !pieces) { err = "ncclBroadcast failed"; ok = false; }
+                std::string verr;
+                if (!F.verify(ok, verr) && ok) { err = verr; ok = false; }
+            }
         }
     }
     if (!ok) {
@@ -995,7 +1103,11 @@ int32_t llmi_model_fanout(struct llama_model* model, const uint8_t* uid, int32_t
     if (nranks == 1) return 0;
     Fanout F;
     if (!proc_fanout_init(F, model->m, uid, nranks, rank)) return -2;
-    if (!F.finish()) { set_err("llmi_model_fanout: broadcast failed"); return -3; }
+    F.rank0 = rank == 0;
+    const bool pieces = F.finish();
+    std::string err;
+    if (!F.verify(pieces || rank != 0, err)) { set_err("llmi_model_fanout: " + err); return pieces ? -6 : -3; }
+    if (!pieces) { set_err("llmi_model_fanout: broadcast failed"); return -3; }
     return 0;
     API_CATCH(-5)
 }
@@ -1025,6 +1137,7 @@ struct llama_model* llmi_model_load_fanout(const char* path, struct llama_model_
     if (nranks > 1) {
         Fanout F;
         ok = proc_fanout_init(F, m->m, uid, nranks, rank);
+        F.rank0 = rank == 0;
         if (ok && rank == 0) {
             const UploadHook h = F.hook();
             ok = model_upload(m->m, err, &h);
@@ -1032,7 +1145,17 @@ struct llama_model* llmi_model_load_fanout(const char* path, struct llama_model_
         }
         // every piece is issued even after a failed upload: the other ranks are blocked in
         // their matching broadcasts and would otherwise never return
-        if (!F.comm.empty() && !F.finish() && ok) { set_err("llmi_model_load_fanout: broadcast failed"); ok = false; }
+        if (!F.comm.empty()) {
+            const bool pieces = F.finish();
+            if (!pieces && ok) { set_err("llmi_model_load_fanout: broadcast failed"); ok = false; }
+            // then the root's status + arena hash: a rank whose root failed (or whose
+            // replica differs) returns NULL instead of a partly written arena
+            std::string verr;
+            if (!F.verify(rank == 0 ? ok : true, verr) && ok) {
+                set_err("llmi_model_load_fanout: " + verr);
+                ok = false;
+            }
+        }
     } else {
         ok = model_upload(m->m, err, nullptr);
         if (!ok) set_err(err);

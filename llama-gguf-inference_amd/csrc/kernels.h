@@ -103,12 +103,11 @@ struct LeArgs {
     unsigned* cnt = nullptr;     // this layer's edge counters [kLeOps][8 shards][16 words], zero at launch
     unsigned* fault = nullptr;   // context fault word: a bounded in-kernel wait gave up
     int spin_limit = 0;          // polls before a wait gives up (0: default)
-    int nt = 1;                  // weight DMA nontemporal (MI355X_MICROARCH.md nt-weights)
+    int kmin = 9;                // smallest sub-item of the launch in ring pieces (sets the loaders' DMA depth)
     // LDS carve (set by the launcher)
     int npieces = 0, img_off0 = 0, img_off1 = 0, fold_off = 0, ring_off = 0, act = -1;
-    int lag = 40;                // DMA pieces kept in flight past the published prefix (16/24/32/40/48)
     int exp = 0;                 // LLMI_LE_EXP experiments (results garbage): 1 no math, 2 no edges / images
-    unsigned long long* trace = nullptr;  // llmi_engine_trace: [block][wave][32] s_memrealtime stamps
+    unsigned long long* trace = nullptr;  // llmi_engine_trace: [block][16 waves][32] s_memrealtime stamps
 };
 // bytes of the edge counters of n_layer layers (one memset per step zeroes them)
 size_t le_counter_bytes(int n_layer);
@@ -272,6 +271,8 @@ int pf_attn_x86_max_kv(int n_head, int n_head_kv, int head_dim);
 // writes the prologue's quantized activation in ggml block form (test hook)
 hipError_t launch_quant_dump(const MVArgs& a, int act, void* out, hipStream_t stream);
 hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int blocks, hipStream_t stream);
+// order-independent 64-bit hash of `bytes` of device memory into *out (device), kernels.hip
+hipError_t launch_arena_hash(const void* p, size_t bytes, unsigned long long* out, hipStream_t stream);
 hipError_t launch_state_set(StepState* st, int token_in, int pos_next, hipStream_t stream);
 hipError_t launch_state_tick(StepState* st, hipStream_t stream);  // seq += 1 (microbenchmarks)
 

@@ -954,6 +954,46 @@ hipError_t launch_stream_read(const void* p, size_t bytes, unsigned* out, int bl
     return hipGetLastError();
 }
 
+// Arena hash (replica check): H = sum over 8-byte words i (mod 2^64) of
+// mix64(word_i ^ (i * phi)), mix64 = splitmix64's finalizer; the last partial word is
+// zero-padded.  A sum of per-position terms is independent of the order the grid visits
+// the words in, so every replica of the same bytes gets the same value on any device
+// (tests/test_fanout_check.py restates it in numpy).
+__device__ __forceinline__ unsigned long long hash_mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_arena_hash(const uint8_t* p, size_t bytes, unsigned long long* out) {
+    const size_t nw = bytes >> 3, n16 = bytes >> 4;
+    unsigned long long acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        const u32x4 v = ldw(p + i * 16);
+        const unsigned long long w0 = ((unsigned long long)v.y << 32) | v.x, w1 = ((unsigned long long)v.w << 32) | v.z;
+        acc += hash_mix64(w0 ^ ((2 * i) * 0x9E3779B97F4A7C15ull));
+        acc += hash_mix64(w1 ^ ((2 * i + 1) * 0x9E3779B97F4A7C15ull));
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the word past the last 16-B piece, and the tail
+        for (size_t i = 2 * n16; i * 8 < bytes; ++i) {
+            unsigned long long w = 0;
+            for (size_t b = 0; b < 8 && i * 8 + b < bytes; ++b) w |= (unsigned long long)p[i * 8 + b] << (8 * b);
+            acc += hash_mix64(w ^ (i * 0x9E3779B97F4A7C15ull));
+        }
+    }
+    (void)nw;
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+hipError_t launch_arena_hash(const void* p, size_t bytes, unsigned long long* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, 8, s);
+    if (e != hipSuccess) return e;
+    const size_t n16 = bytes >> 4;
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(4096, (n16 + 255) / 256));
+    hipLaunchKernelGGL(k_arena_hash, dim3(blocks), dim3(256), 0, s, (const uint8_t*)p, bytes, out);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------

@@ -12,13 +12,15 @@
 // matvecs stream into an LDS ring from the start of the launch, and the activation edges
 // between the matvecs become in-launch hand-offs that the stream runs ahead of.
 //
-// Workgroup = 512 threads, one per CU (grid = CU count, every workgroup resident):
-//   wave 0      LOADER: walks the CU's sub-items of every op in order and moves each one's
-//               weights global -> LDS ring by LDS-DMA (one 1-KiB piece per wave
-//               instruction, lane L's 16 B of its unit), keeping kLeLag pieces in flight
-//               and publishing the landed prefix (ctl.ready); it never waits on an
-//               activation, only on ring space (ctl.cons[], what each consumer still needs)
-//   waves 1..7  CONSUMERS: per op, wait for the op's input edge, build the q8 activation
+// Workgroup = 576 threads, one per CU (grid = CU count, every workgroup resident):
+//   waves 0, 1  LOADERS: both walk the CU's sub-items of every op in order; loader l moves
+//               the weights of every sub-item n with n % 2 == l global -> LDS ring by
+//               LDS-DMA (one 1-KiB piece per wave instruction, lane L's 16 B of its unit),
+//               keeps its last kLeDepth sub-items in flight and publishes how many of its
+//               sub-items have landed (ctl.ready[l]); a loader never waits on an
+//               activation, only on ring space (ctl.cons[], what each consumer still
+//               needs).  One loader wave issued 16 GB/s per CU, two 27 (tools/lestream.py)
+//   waves 2..8  CONSUMERS: per op, wait for the op's input edge, build the q8 activation
 //               image in LDS (RMSNorm + quantize_row_q8_K / q8_0, bit-exact, mv_device.h),
 //               then reduce their own tasks' sub-items straight from the ring with
 //               k_matvec's unit-term / fold / epilogue code (unit_terms, sub_finish):
@@ -50,15 +52,16 @@ namespace llmi {
 
 namespace {
 
-constexpr int kLeT = 512;   // threads per workgroup
-constexpr int kLeC = 7;     // consumer waves (waves 1..7)
-constexpr int kLeLag = 40;  // DMA pieces the loader keeps in flight past the published prefix
-constexpr int kLeMaxPieces = 120;
+constexpr int kLeNL = 2;                  // loader waves (waves 0 .. kLeNL-1)
+constexpr int kLeC = 7;                   // consumer waves (waves kLeNL .. kLeNL+6)
+constexpr int kLeT = (kLeNL + kLeC) * 64;  // threads per workgroup
+constexpr int kLeMaxPieces = 136;
+constexpr int kLeTraceWaves = 16;          // trace layout [block][16 waves][32 stamps]
 constexpr unsigned kLeFaultRing = 0x100u, kLeFaultEdge = 0x200u, kLeFaultBar = 0x400u, kLeFaultSpace = 0x800u;
 
 // LDS control block (16-B aligned, at offset 0 of the dynamic LDS)
 struct LeCtl {
-    unsigned ready;    // ring pieces landed (loader; monotonic)
+    unsigned ready[2]; // loader l: its sub-items landed (monotonic)
     unsigned dead;     // a bounded wait gave up: every wave leaves
     unsigned bar;      // consumer-barrier arrivals
     unsigned edge;     // highest op whose input edge the poller wave has seen
@@ -82,7 +85,8 @@ __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) {
 
 // timeline stamps (llmi_engine_trace; null trace: one uniform branch each)
 #define LE_STAMP(I, V)                                                                                      \
-    if (A.trace && (threadIdx.x & 63) == 0) A.trace[((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 32 + (I)] = (V);
+    if (A.trace && (threadIdx.x & 63) == 0)                                                                 \
+        A.trace[((size_t)blockIdx.x * kLeTraceWaves + (threadIdx.x >> 6)) * 32 + (I)] = (V);
 #define LE_NOW __builtin_amdgcn_s_memrealtime()
 
 __device__ __forceinline__ void le_fault(const LeArgs& A, LeCtl* ctl, unsigned code) {
@@ -113,58 +117,67 @@ __device__ __forceinline__ bool le_cbar(const LeArgs& A, LeCtl* ctl, int& barn) 
     return le_spin_lds(A, ctl, &ctl->bar, (unsigned)barn * kLeC, kLeFaultBar);
 }
 
-// ---- loader ----------------------------------------------------------------------
+// ---- loaders ---------------------------------------------------------------------
 // LDS-DMA in inline asm (cdna_hip_programming.md §5.7 item 1): the compiler neither counts
-// it nor waits for it; the loader's own s_waitcnt vmcnt(N) publishes the landed prefix.
-__device__ __forceinline__ void le_dma16(const uint8_t* src, uint32_t lds, int nt) {
+// it nor waits for it; the loader's own s_waitcnt vmcnt(N) publishes landed sub-items.
+// Always nontemporal: streamed weights one CU reads once (MI355X_MICROARCH.md nt-weights).
+__device__ __forceinline__ void le_dma16(const uint8_t* src, uint32_t lds) {
     unsigned keep;
-    if (nt)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
 }
-__device__ __forceinline__ void le_dma4(const uint8_t* src, uint32_t lds, int nt) {
+__device__ __forceinline__ void le_dma4(const uint8_t* src, uint32_t lds) {
     unsigned keep;
-    if (nt)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
 }
 template <int N>
 __device__ __forceinline__ void le_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
+// sub-items a loader keeps in flight past its published ones, by the launch's smallest
+// sub-item (pieces): ~30 pieces per loader wave (vmcnt counts at most 63)
+__host__ __device__ constexpr int le_depth(int kmin) { return kmin >= 14 ? 2 : 3; }
+// wait until at most le_depth(kmin) x kmin of this wave's pieces are in flight: every
+// sub-item of this loader but its last le_depth(kmin) has landed
+__device__ __forceinline__ void le_vm_lag(int kmin) {
+    switch (kmin) {
+        case 9: le_vmcnt<9 * le_depth(9)>(); break;
+        case 11: le_vmcnt<11 * le_depth(11)>(); break;
+        case 14: le_vmcnt<14 * le_depth(14)>(); break;
+        default: le_vmcnt<17 * le_depth(17)>(); break;
+    }
+}
 
-// ring state of the loader (all wave-uniform)
+// walk state of a loader (all wave-uniform).  Both loaders walk every sub-item (so both
+// know every sub-item's ring position); each issues its own.
 struct LeLoad {
-    unsigned issued = 0;   // pieces issued
-    unsigned pw = 0;       // ring slot of the next piece
-    unsigned pub = 0;      // published ready
+    unsigned pieces = 0;   // ring pieces of all sub-items walked (both loaders')
+    unsigned sn = 0;       // sub-items walked
+    unsigned mine = 0;     // this loader's sub-items issued
+    unsigned pub = 0;      // this loader's sub-items published
     unsigned lowest = 0;   // last seen min over consumers of ctl.cons
+    uint32_t ring = 0;     // LDS address of the ring (uniform)
     unsigned long long waits = 0, wait_ticks = 0;  // ring-full waits (traced launches)
     unsigned long long vm_ticks = 0;                // time in the lag's vmcnt waits (traced launches)
 };
 
-__device__ __forceinline__ void le_publish(LeCtl* ctl, LeLoad& L, unsigned v) {
+__device__ __forceinline__ void le_publish(LeCtl* ctl, LeLoad& L, unsigned v, int l) {
     if (v > L.pub) {
         L.pub = v;
         asm volatile("" ::: "memory");
-        lds_st(&ctl->ready, v);
+        lds_st(&ctl->ready[l], v);
     }
 }
 
-// room in the ring for pieces [issued, issued + k)?  Waits (publishing everything in
+// room in the ring for pieces [p0, p0 + k)?  Waits (publishing everything of its own in
 // flight first) until every consumer has released what the new pieces overwrite.
-__device__ __forceinline__ bool le_space(const LeArgs& A, LeCtl* ctl, LeLoad& L, int k) {
-    const unsigned long long end = (unsigned long long)L.issued + (unsigned)k, NP = (unsigned)A.npieces;
+__device__ __forceinline__ bool le_space(const LeArgs& A, LeCtl* ctl, LeLoad& L, unsigned p0, int k, int l) {
+    const unsigned long long end = (unsigned long long)p0 + (unsigned)k, NP = (unsigned)A.npieces;
     if (end <= (unsigned long long)L.lowest + NP) return true;
     const unsigned long long t0 = A.trace ? LE_NOW : 0ull;
     le_vmcnt<0>();
-    le_publish(ctl, L, L.issued);
+    le_publish(ctl, L, L.mine, l);
     for (int n = 0;; ++n) {
         unsigned m = 0xffffffffu;
 #pragma unroll
@@ -186,111 +199,92 @@ __device__ __forceinline__ bool le_space(const LeArgs& A, LeCtl* ctl, LeLoad& L,
     }
 }
 
-// one sub-item's pieces, lane = (row r, unit ul) of the task as in k_matvec
+// one sub-item's pieces at ring piece p0, lane = (row r, unit ul) of the task as in k_matvec
 template <int T>
-__device__ __forceinline__ void le_issue(const Seg& sg, const LaneUnit& lu, uint32_t U, uint8_t* ring, unsigned pw, int NP,
-                                         int nt) {
-    const uint32_t base = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)ring;
-    auto slot = [&](int q) -> uint32_t {
+__device__ __forceinline__ void le_issue(const Seg& sg, const LaneUnit& lu, uint32_t U, uint32_t ring, unsigned p0,
+                                         unsigned NP) {
+    unsigned pw = __builtin_amdgcn_readfirstlane(p0 % NP);
+    auto slot = [&](int q) -> uint32_t {  // uniform: scalar arithmetic
         unsigned p = pw + (unsigned)q;
-        if (p >= (unsigned)NP) p -= (unsigned)NP;
-        return __builtin_amdgcn_readfirstlane(base + p * 1024u);
+        if (p >= NP) p -= NP;
+        return ring + p * 1024u;
     };
     constexpr int NPART = unit_parts<T>();
     const uint32_t P = (U * 16u) << sg.rgs, ru = lu.row * U + lu.u;
-    const uint32_t oa = piece_off(lu.row, 0, lu.u, U, NPART, sg.rgs);
+    const uint8_t* a = sg.a + piece_off(lu.row, 0, lu.u, U, NPART, sg.rgs);
 #pragma unroll
-    for (int q = 0; q < NPART; ++q) le_dma16(sg.a + oa + (uint32_t)q * P, slot(q), nt);
+    for (int q = 0; q < NPART; ++q) le_dma16(a + (size_t)q * P, slot(q));
     if constexpr (T == T_Q8_0) {
-        le_dma16(sg.d + ru * 16u, slot(NPART), nt);
+        le_dma16(sg.d + ru * 16u, slot(NPART));
     } else {
         constexpr int NH = (T == T_Q5_K || T == T_Q6_K) ? unit_hparts<T>() : 0;
         if constexpr (NH > 0) {
-            const uint32_t oh = piece_off(lu.row, 0, lu.u, U, NH, sg.rgs);
+            const uint8_t* h = sg.h + piece_off(lu.row, 0, lu.u, U, NH, sg.rgs);
 #pragma unroll
-            for (int c = 0; c < NH; ++c) le_dma16(sg.h + oh + (uint32_t)c * P, slot(NPART + c), nt);
+            for (int c = 0; c < NH; ++c) le_dma16(h + (size_t)c * P, slot(NPART + c));
         }
-        le_dma16(sg.s + ru * 16u, slot(NPART + NH), nt);
-        if constexpr (T == T_Q6_K) le_dma4(sg.d + ((ru * 2u) & ~3u), slot(NPART + NH + 1), nt);
+        le_dma16(sg.s + ru * 16u, slot(NPART + NH));
+        if constexpr (T == T_Q6_K) le_dma4(sg.d + ((ru * 2u) & ~3u), slot(NPART + NH + 1));
     }
 }
 
-// The op's segments held in registers (static kernarg offsets, scalar loads) and picked by
-// a wave-uniform index: a pick by a per-lane index compiles to vector loads from the
-// kernarg segment, whose compiler-inserted vmcnt waits would also wait for the loader's
-// LDS-DMA (the hardware counts both) and serialize the stream.
-struct LeSegs {
-    Seg s[3];
-};
-__device__ __forceinline__ LeSegs le_segs(const MVArgs& M) {
-    LeSegs r;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) r.s[i] = M.seg[i];
-    return r;
-}
-__device__ __forceinline__ Seg le_pick(const LeSegs& S, int si) {
+// A segment of an op by a wave-uniform index, read straight from the kernel arguments
+// (scalar loads at a dynamic offset: lgkmcnt only).  Copying the segments into a local
+// array and selecting from it made the compiler keep a private copy of the arguments and
+// load the selected fields from scratch once per sub-item; the vmcnt(0) before their use
+// drained the loader's whole DMA stream (ISA, round 6).
+__device__ __forceinline__ Seg le_pick(const MVArgs& M, int si) {
     si = __builtin_amdgcn_readfirstlane(si);
-    return si == 0 ? S.s[0] : si == 1 ? S.s[1] : S.s[2];
+    return M.seg[si];
 }
 
 template <int EPI>
-__device__ __forceinline__ int le_task_pieces(const MVArgs& M, const LeSegs& SG, const TaskGeo& g, int task) {
-    if constexpr (EPI == EPI_SWIGLU) return g.nj * (le_pieces(SG.s[0].type) + le_pieces(SG.s[1].type));
-    else return g.nj * le_pieces(le_pick(SG, sub_of<EPI>(M, g, task, 0).si).type);
+__device__ __forceinline__ int le_task_pieces(const MVArgs& M, const TaskGeo& g, int task) {
+    if constexpr (EPI == EPI_SWIGLU) return g.nj * (le_pieces(M.seg[0].type) + le_pieces(M.seg[1].type));
+    else return g.nj * le_pieces(le_pick(M, sub_of<EPI>(M, g, task, 0).si).type);
 }
 
 template <int OP, int ACT, int EPI>
-__device__ __forceinline__ bool le_load_op(const LeArgs& A, LeCtl* ctl, uint8_t* ring, LeLoad& L) {
+__device__ __forceinline__ bool le_load_op(const LeArgs& A, LeCtl* ctl, LeLoad& L, int l) {
     if (OP >= A.nops) return true;
     const MVArgs& M = A.op[OP];
-    const LeSegs SG = le_segs(M);
     const TaskGeo g = task_geo(M);
     const int lane = threadIdx.x & 63, r = lane / g.lr, ul = lane - r * g.lr;
     const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
-    const int NP = A.npieces;
-    bool first = OP > 0;  // the first sub-item of an op: publish the previous op's tail early
+    const unsigned NP = (unsigned)A.npieces;
     LE_STAMP(1 + 2 * OP, LE_NOW)
+    int cur = -1;  // segment held in registers (reloaded only when the sub-item's changes)
+    Seg sg;
     for (int task = blockIdx.x; task < M.ntasks; task += gridDim.x) {
         for (int s = 0; s < S; ++s) {
             const Sub b = sub_of<EPI>(M, g, task, s);
-            const Seg sg = le_pick(SG, b.si);
+            if (b.si != cur) {
+                sg = le_pick(M, b.si);
+                cur = b.si;
+            }
             const int k = le_pieces(sg.type);
-            if (!le_space(A, ctl, L, k)) return false;
+            const unsigned p0 = L.pieces;
+            const bool own = (L.sn & (kLeNL - 1)) == (unsigned)l;
+            L.pieces += (unsigned)k;
+            ++L.sn;
+            if (!own) continue;
+            if (!le_space(A, ctl, L, p0, k, l)) return false;
             const LaneUnit lu = lane_unit(g, b, sg, r, ul);
             if constexpr (ACT == 1) {
-                le_issue<T_Q8_0>(sg, lu, (uint32_t)g.U, ring, L.pw, NP, A.nt);
+                le_issue<T_Q8_0>(sg, lu, (uint32_t)g.U, L.ring, p0, NP);
             } else {
                 switch (sg.type) {
-                    case T_Q4_K: le_issue<T_Q4_K>(sg, lu, (uint32_t)g.U, ring, L.pw, NP, A.nt); break;
-                    case T_Q5_K: le_issue<T_Q5_K>(sg, lu, (uint32_t)g.U, ring, L.pw, NP, A.nt); break;
-                    default: le_issue<T_Q6_K>(sg, lu, (uint32_t)g.U, ring, L.pw, NP, A.nt); break;
+                    case T_Q4_K: le_issue<T_Q4_K>(sg, lu, (uint32_t)g.U, L.ring, p0, NP); break;
+                    case T_Q5_K: le_issue<T_Q5_K>(sg, lu, (uint32_t)g.U, L.ring, p0, NP); break;
+                    default: le_issue<T_Q6_K>(sg, lu, (uint32_t)g.U, L.ring, p0, NP); break;
                 }
             }
-            L.issued += (unsigned)k;
-            L.pw += (unsigned)k;
-            if (L.pw >= (unsigned)NP) L.pw -= (unsigned)NP;
-            if (first) {
-                // everything before this sub-item: wait for exactly it to remain in flight
-                switch (k) {
-                    case 9: le_vmcnt<9>(); break;
-                    case 11: le_vmcnt<11>(); break;
-                    case 14: le_vmcnt<14>(); break;
-                    default: le_vmcnt<17>(); break;
-                }
-                le_publish(ctl, L, L.issued - (unsigned)k);
-                first = false;
-            } else {
-                const unsigned long long tv = A.trace ? LE_NOW : 0ull;
-                switch (A.lag) {
-                    case 16: le_vmcnt<16>(); break;
-                    case 24: le_vmcnt<24>(); break;
-                    case 32: le_vmcnt<32>(); break;
-                    case 48: le_vmcnt<48>(); break;
-                    default: le_vmcnt<kLeLag>(); break;
-                }
-                if (A.trace) L.vm_ticks += LE_NOW - tv;
-                if (L.issued > (unsigned)A.lag) le_publish(ctl, L, L.issued - (unsigned)A.lag);
-            }
+            ++L.mine;
+            const unsigned long long tv = A.trace ? LE_NOW : 0ull;
+            le_vm_lag(A.kmin);
+            if (A.trace) L.vm_ticks += LE_NOW - tv;
+            const unsigned depth = (unsigned)le_depth(A.kmin);
+            if (L.mine > depth) le_publish(ctl, L, L.mine - depth, l);
         }
     }
     LE_STAMP(2 + 2 * OP, LE_NOW)
@@ -300,16 +294,17 @@ __device__ __forceinline__ bool le_load_op(const LeArgs& A, LeCtl* ctl, uint8_t*
 }
 
 template <int ACT>
-__device__ __forceinline__ void le_loader(const LeArgs& A, LeCtl* ctl, uint8_t* ring) {
+__device__ __forceinline__ void le_loader(const LeArgs& A, LeCtl* ctl, uint8_t* ring, int l) {
     LeLoad L;
-    bool ok = le_load_op<0, ACT, EPI_ADD>(A, ctl, ring, L) && le_load_op<1, ACT, EPI_SWIGLU>(A, ctl, ring, L) &&
-              le_load_op<2, ACT, EPI_ADD>(A, ctl, ring, L) && le_load_op<3, ACT, EPI_QKV>(A, ctl, ring, L);
+    L.ring = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)ring);
+    bool ok = le_load_op<0, ACT, EPI_ADD>(A, ctl, L, l) && le_load_op<1, ACT, EPI_SWIGLU>(A, ctl, L, l) &&
+              le_load_op<2, ACT, EPI_ADD>(A, ctl, L, l) && le_load_op<3, ACT, EPI_QKV>(A, ctl, L, l);
     le_vmcnt<0>();  // no LDS-DMA may land after the workgroup's LDS is released
-    if (ok) le_publish(ctl, L, L.issued);
+    if (ok) le_publish(ctl, L, L.mine, l);
     LE_STAMP(9, LE_NOW)
     LE_STAMP(10, L.waits)
     LE_STAMP(11, L.wait_ticks)
-    LE_STAMP(12, L.issued)
+    LE_STAMP(12, L.mine)
     LE_STAMP(13, ((unsigned long long)(__builtin_amdgcn_s_getreg(6164) & 15)))
 }
 
@@ -453,6 +448,7 @@ __device__ __forceinline__ void le_sub(const MVArgs& M, LeCtl* ctl, const uint8_
 // ring position of the consumers' walk (identical in every consumer wave)
 struct LeWalk {
     unsigned base = 0;  // first piece of the current op
+    unsigned sn = 0;    // first sub-item of the current op (loader (sn % kLeNL) issues it)
     int rot = 0;        // task-to-wave rotation of the current op
     int barn = 0;       // consumer barriers passed
 };
@@ -462,7 +458,6 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
                                            LeWalk& W) {
     if (OP >= A.nops) return true;
     const MVArgs& M = A.op[OP];
-    const LeSegs SG = le_segs(M);
     const TaskGeo g = task_geo(M);
     const int lane = threadIdx.x & 63, r = lane / g.lr, ul = lane - r * g.lr;
     const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
@@ -474,7 +469,7 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
         int i = 0;
         for (int task = blockIdx.x; task < M.ntasks; task += NB, ++i) {
             if ((i + W.rot) % kLeC == cw) break;
-            b += (unsigned)le_task_pieces<EPI>(M, SG, g, task);
+            b += (unsigned)le_task_pieces<EPI>(M, g, task);
         }
         lds_st(&ctl->cons[cw], b);
     }
@@ -490,24 +485,25 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
     // 3. this wave's tasks, straight from the ring
     int pos = 0;
     if constexpr (EPI == EPI_QKV) pos = M.st->pos;
-    unsigned b = W.base;
+    unsigned b = W.base, sn = W.sn;
     unsigned pw = W.base % (unsigned)NP;
     int i = 0;
     for (int task = blockIdx.x; task < M.ntasks; task += NB, ++i) {
         if ((i + W.rot) % kLeC != cw) {
-            const unsigned n = (unsigned)le_task_pieces<EPI>(M, SG, g, task);
+            const unsigned n = (unsigned)le_task_pieces<EPI>(M, g, task);
             b += n;
             pw = (pw + n) % (unsigned)NP;
+            sn += (unsigned)S;
             continue;
         }
         float acc = 0.f, vg = 0.f;
         for (int s = 0; s < S; ++s) {
             const Sub sb = sub_of<EPI>(M, g, task, s);
-            const Seg sg = le_pick(SG, sb.si);
+            const Seg sg = le_pick(M, sb.si);
             const unsigned k = (unsigned)le_pieces(sg.type);
             lds_st(&ctl->cons[cw], b);
             const unsigned long long tw = A.trace ? LE_NOW : 0ull;
-            if (!le_spin_lds(A, ctl, &ctl->ready, b + k, kLeFaultRing)) return false;
+            if (!le_spin_lds(A, ctl, &ctl->ready[sn & (kLeNL - 1)], sn / kLeNL + 1, kLeFaultRing)) return false;
             if (A.trace) {
                 const unsigned long long tn = LE_NOW;
                 ring_ticks += tn - tw;
@@ -527,12 +523,14 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
             }
             b += k;
             pw = (pw + k) % (unsigned)NP;
+            ++sn;
         }
     }
     lds_st(&ctl->cons[cw], b);
     LE_STAMP(4 + 4 * OP, LE_NOW)
     LE_STAMP(20 + OP, ring_ticks)
     W.base = b;
+    W.sn = sn;
     W.rot = (W.rot + i) % kLeC;
     // 4. hand the op's output on: every wave drains its write-through stores, the last
     //    wave of the workgroup adds to the edge counter (the last op's output is read by
@@ -561,11 +559,11 @@ __global__ __launch_bounds__(kLeT, 1) void k_leng(LeArgs A) {
     LE_STAMP(0, LE_NOW)
     if (threadIdx.x < sizeof(LeCtl) / 4) ((unsigned*)smem)[threadIdx.x] = 0u;
     __syncthreads();  // the only full-workgroup barrier
-    if (wave == 0) {
-        le_loader<ACT>(A, ctl, ring);
+    if (wave < kLeNL) {
+        le_loader<ACT>(A, ctl, ring, wave);
         return;
     }
-    const int cw = wave - 1;
+    const int cw = wave - kLeNL;
     float* F = (float*)(smem + A.fold_off) + (size_t)cw * fold_floats<ACT, X86>();
     uint8_t* img0 = smem + A.img_off0;
     uint8_t* img1 = smem + A.img_off1;
@@ -595,14 +593,6 @@ int g_le_exp = [] {  // LLMI_LE_EXP (experiments, results garbage): 1 consumers 
     const char* e = getenv("LLMI_LE_EXP");
     return e ? atoi(e) : 0;
 }();
-int g_le_lag = [] {  // LLMI_LE_LAG (A/B): DMA pieces in flight past the published prefix
-    const char* e = getenv("LLMI_LE_LAG");
-    return e ? atoi(e) : kLeLag;
-}();
-int g_le_nt = [] {  // LLMI_LE_NT (A/B): nontemporal weight DMA
-    const char* e = getenv("LLMI_LE_NT");
-    return e ? atoi(e) : 1;
-}();
 bool le_wanted() { return g_le_on != 0; }
 
 static hipError_t le_kernel(int act, int x86, const void** k) {
@@ -613,7 +603,7 @@ static hipError_t le_kernel(int act, int x86, const void** k) {
 
 hipError_t layer_engine_prepare(LeArgs& a) {
     if (a.nops < 1 || a.nops > kLeOps || !a.cnt || !a.fault) return hipErrorInvalidValue;
-    int act = -1, maxp = 0;
+    int act = -1, maxp = 0, kmin = 99;
     size_t img[2] = {0, 0};
     const int x86 = a.op[0].num ? 1 : 0;
     for (int k = 0; k < a.nops; ++k) {
@@ -628,6 +618,7 @@ hipError_t layer_engine_prepare(LeArgs& a) {
             act = act_kind(t);
             if ((m.seg[i].x86 != 0) != (x86 != 0)) return hipErrorInvalidValue;
             maxp = std::max(maxp, le_pieces(t));
+            kmin = std::min(kmin, le_pieces(t));
         }
         img[k & 1] = std::max(img[k & 1], (size_t)(m.cols >> 8) * kRec);
     }
@@ -642,13 +633,12 @@ hipError_t layer_engine_prepare(LeArgs& a) {
     off = a16(off + fold);
     a.ring_off = (int)off;
     const int np = std::min(kLeMaxPieces, (int)((160 * 1024 - (int)off) / 1024));
-    if (np < 3 * maxp) return hipErrorNotSupported;
+    if (np < 2 * kLeNL * maxp) return hipErrorNotSupported;
     a.npieces = np;
     a.act = act;
     if (a.spin_limit <= 0) a.spin_limit = g_le_spin;
     a.exp = g_le_exp;
-    a.nt = g_le_nt;
-    a.lag = g_le_lag == 16 || g_le_lag == 24 || g_le_lag == 32 || g_le_lag == 48 ? g_le_lag : kLeLag;
+    a.kmin = kmin;
     if (cu_count() < 8) return hipErrorNotSupported;
     // every workgroup must be resident at once (persistent grid): one per CU by LDS, and
     // the occupancy query must admit one (cached per kernel, LDS bytes and device)
@@ -691,7 +681,7 @@ hipError_t launch_layer_engine(const LeArgs& a, hipStream_t s) {
 namespace llmi {
 namespace {
 // every CU streams its contiguous share of `src` in 1-KiB pieces (lane L: bytes 16 L..)
-//   mode 0: one loader wave, asm LDS-DMA with M0 saved / restored (the engine's le_dma16)
+//   mode 0: one loader wave, asm LDS-DMA with M0 saved / restored (the engine's le_dma16, always nt)
 //   mode 1: one loader wave, __builtin_amdgcn_global_load_lds (compiler-managed M0)
 //   mode 2 / 3: two / four loader waves (asm), pieces dealt round-robin
 //   mode 4: eight waves of plain 16-B loads into registers, 8 in flight per wave (k_matvec's form)
@@ -732,7 +722,7 @@ __global__ __launch_bounds__(512, 1) void k_le_stream(const uint8_t* src, size_t
                 __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
                                                  (void __attribute__((address_space(3)))*)(size_t)l, 16, 0, 0);
         } else {
-            le_dma16(g, l, nt);
+            le_dma16(g, l);
         }
         slot += NL;
         if (slot >= 128) slot -= 128;

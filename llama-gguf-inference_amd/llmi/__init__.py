@@ -142,6 +142,14 @@ class Vocab:
             pass
 
 
+
+def device_hash(ptr: int, nbytes: int) -> int:
+    """llmi_device_hash: the arena hash of any device memory (test hook)."""
+    h = C.c_uint64()
+    if lib().llmi_device_hash(C.c_void_p(ptr), int(nbytes), C.byref(h)) != 0:
+        raise LlmiError(last_error())
+    return int(h.value)
+
 class Model:
     """llama_model_load_from_file: GGUF -> HBM arena on `main_gpu`."""
 
@@ -253,6 +261,14 @@ class Model:
         p, n = C.c_void_p(), C.c_uint64()
         lib().llmi_model_arena(self._h, C.byref(p), C.byref(n))
         return int(p.value or 0), int(n.value)
+
+    def arena_hash(self) -> int:
+        """Order-independent 64-bit hash of the device arena (llmi_model_arena_hash): equal
+        on every replica of the same weights (the fan-out's replica check)."""
+        h = C.c_uint64()
+        if lib().llmi_model_arena_hash(self._h, C.byref(h)) != 0:
+            raise LlmiError(last_error())
+        return int(h.value)
 
     def replicate(self, devices: Sequence[int]) -> list["Model"]:
         """In-process RCCL broadcast of the arena to `devices`."""
@@ -396,13 +412,13 @@ class Context:
 
     def engine_trace(self, first: int, pos0: int, layer: int) -> np.ndarray:
         """llmi_engine_trace: s_memrealtime stamps (10 ns ticks) of layer `layer`'s layer-engine
-        launch in one eager step at pos0, shaped [CUs][8 waves][32] (tools/letrace.py)."""
-        n = 256 * 8 * 32 * 4
+        launch in one eager step at pos0, shaped [CUs][16 wave slots][32] (tools/letrace.py)."""
+        n = 256 * 16 * 32 * 4
         out = (C.c_uint64 * n)()
         g = int(lib().llmi_engine_trace(self._h, int(first), int(pos0), int(layer), out, n))
         if g < 0:
             raise LlmiError(last_error())
-        return np.ctypeslib.as_array(out)[: g * 8 * 32].reshape(g, 8, 32).copy()
+        return np.ctypeslib.as_array(out)[: g * 16 * 32].reshape(g, 16, 32).copy()
 
     def kv_clear(self) -> None:
         lib().llama_kv_self_clear(self._h)

@@ -112,6 +112,8 @@ SIGNATURES = {
     "llmi_pf_gemm": (C.c_int32, [C.c_int32, _P, C.c_int64, C.c_int64, _P, _P, C.c_float, C.c_int32, _P,
                                  C.POINTER(C.c_double)]),
     "llmi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "llmi_model_arena_hash": (C.c_int32, [_P, C.POINTER(C.c_uint64)]),
+    "llmi_device_hash": (C.c_int32, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "llmi_attention": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32]),
     "llmi_pf_attention": (C.c_double, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P,
                                        _P, C.c_int32, C.c_int64]),

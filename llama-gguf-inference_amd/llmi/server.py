@@ -689,9 +689,10 @@ def parse_args(argv=None):
     ap.add_argument("-np", "--parallel", type=int, default=int(os.environ.get("LLMI_SLOTS", "4")),
                     help="sequences (slots) per replica decoded together (continuous batching)")
     ap.add_argument("--decode-chunk", type=int, default=8, help="tokens per batched decode call")
-    ap.add_argument("--numerics", choices=("generic", "x86"), default=os.environ.get("LLMI_NUMERICS", "generic"),
-                    help="fp32 association of every kernel: ggml's generic order, or upstream's x86 AVX2 build "
-                         "(the reference's NGL=0 path)")
+    ap.add_argument("--numerics", choices=("generic", "x86"), default=None,
+                    help="fp32 association of every kernel: ggml's generic order, or the oracle's model of "
+                         "upstream's x86 AVX2 association (non-repack, non-flash; match with the reference's "
+                         "CPU image unpinned)")
     # llama-server's sampling flags and defaults (per-request fields override them)
     d = SamplingParams()
     ap.add_argument("--temp", type=float, default=d.temperature)
@@ -704,6 +705,12 @@ def parse_args(argv=None):
     ap.add_argument("--frequency-penalty", type=float, default=d.frequency_penalty)
     ap.add_argument("-s", "--seed", type=int, default=d.seed)
     args, extra = ap.parse_known_args(argv)
+    if args.numerics is None:
+        # argparse does not check a default against `choices`: validate the env value here
+        env = os.environ.get("LLMI_NUMERICS", "generic").strip().lower()
+        if env not in ("generic", "x86"):
+            ap.error(f"LLMI_NUMERICS={os.environ.get('LLMI_NUMERICS')!r}: expected 'generic' or 'x86'")
+        args.numerics = env
     return args, extra
 
 

@@ -147,3 +147,54 @@ def test_single_rank_loads_plain():
     ld = StubLoader()
     m, s = bench.load_replica("/x.gguf", D(), lambda: pytest.fail("no uid on one rank"), ld.fanout, ld.plain)
     assert m == "model" and s == 0.0 and ld.calls == [("plain", "/x.gguf", 0)]
+
+
+def _check_worker(rank, world, port, q, mode):
+    """mode 'fail1': rank 1's load raises; 'hash': the replicas' hashes differ; 'ok'."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import bench
+
+    d = bench.Dist("gloo")
+
+    def fanout(path, gpu, uid, nranks, r):
+        if mode == "fail1" and r == 1:
+            raise RuntimeError("llmi_model_load_fanout: the root rank's upload failed")
+        return f"model{r}"
+
+    def arena_hash(m):
+        return 1234 + (int(m[-1]) if mode == "hash" else 0)
+
+    try:
+        bench.load_replica("/x.gguf", d, lambda: b"uid", fanout, lambda p, g: "plain", arena_hash=arena_hash)
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+        d.close()
+        sys.exit(3)
+    d.close()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("mode", ["fail1", "hash", "ok"])
+def test_replica_check_every_rank_fails_together_gloo(mode):
+    """after the fan-out every rank's load status and arena hash are
+    gathered; a failure on ANY rank (or a replica whose hash differs from rank 0's) makes
+    BOTH ranks exit non-zero, with no hang; equal hashes let both go on."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(30)
+    codes = [p.exitcode for p in procs]
+    if mode == "ok":
+        assert codes == [0, 0] and res == {0: "ok", 1: "ok"}
+    else:
+        assert codes == [3, 3], (codes, res)
+        want = "failed on rank(s) [(1," if mode == "fail1" else "hashes differ"
+        assert all(want in res[r] for r in range(world)), res

@@ -233,6 +233,21 @@ def test_version_and_argv():
     assert extra == ["--flash-attn"]
 
 
+def test_numerics_env_validated(monkeypatch):
+    """LLMI_NUMERICS is checked like --numerics' choices (argparse does not check a
+    default): case-folded, and an unknown value is an error, never a silent generic."""
+    from llmi.server import parse_args
+
+    monkeypatch.setenv("LLMI_NUMERICS", "X86")
+    assert parse_args(["-m", "/m.gguf"])[0].numerics == "x86"
+    monkeypatch.setenv("LLMI_NUMERICS", "1")
+    with pytest.raises(SystemExit):
+        parse_args(["-m", "/m.gguf"])
+    assert parse_args(["-m", "/m.gguf", "--numerics", "generic"])[0].numerics == "generic"
+    monkeypatch.delenv("LLMI_NUMERICS")
+    assert parse_args(["-m", "/m.gguf"])[0].numerics == "generic"
+
+
 def test_gateway_forwarded_bytes(server):
     """The exact request shape the reference gateway forwards (SURVEY.md §8b capture of
     scripts/gateway.py:721-745: lowercase client headers, backend Bearer key, Connection:

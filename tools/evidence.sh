@@ -137,7 +137,7 @@ batch)
   ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $SQ1 --kernel-trace --output-format csv -d "$R/$OUT/batch_sq" -o run -- \
       python3 "$R/bench.py" --no-cpu-baseline --preset llama3-8b-q4km --prompt 128 --steps 8 --warmup 2 --profile-steps 0 \
       --no-c2-full --no-other-numerics --eager --batch-seqs "$SEQS" --batch-steps 8 > "$R/$OUT/batch_sq.log" 2>&1 ) || { tail -5 "$OUT/batch_sq.log"; exit 2; }
-  python3 tools/sq_summary.py "$OUT/batch_sq" k_bmm > "$OUT/batch_sq_bmm.json"
+  python3 tools/sq_summary.py "$OUT/batch_sq" k_bm > "$OUT/batch_sq_bmm.json"  # k_bmd / k_bmd2 (default) and k_bmm
   trim "$OUT/batch_sq"
   python3 -c "import json; d=json.load(open('$OUT/batch_sq_bmm.json')); [print(k[:70], {c: v[c] for c in v if c.endswith('_share')}) for k, v in d.items()]"
   ;;

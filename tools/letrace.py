@@ -5,7 +5,7 @@ Loads a synthetic preset (LE_PRESET, default llama3-8b-q4km; LE_LAYERS layers, 0
 prefills a 128-token prompt, decodes up to LE_POS (default 384, the C2 window's mean
 context), then llmi_engine_trace()s layer LE_LAYER (default the middle one) and prints,
 in microseconds from the first workgroup's entry, the distribution over workgroups of:
-  loader   op k issue start / end, loader done, ring-full waits (count, us)
+  loader   (wave 0 of the LE_NL loader waves) op k issue start / end, loader done, ring-full waits
   consumers (per wave) op k edge seen, image built, first sub-item ready, op done,
            time spent waiting for ring data
 Stamps: s_memrealtime (100 MHz).  LE_DUMP=<file.npy> saves the raw stamps.
@@ -43,9 +43,11 @@ for rep in range(reps):
 if os.environ.get("LE_DUMP"):
     np.save(os.environ["LE_DUMP"], t)
 G = t.shape[0]
+NL = int(os.environ.get("LE_NL", "2"))  # loader waves (leng.hip kLeNL), then 7 consumer waves
+lds = t[:, :NL, :]
 ld = t[:, 0, :]
-cs = t[:, 1:, :]
-t0 = min(ld[:, 0].min(), cs[:, :, 0].min())
+cs = t[:, NL:NL + 7, :]
+t0 = min(lds[:, :, 0].min(), cs[:, :, 0].min())
 us = lambda a: (a - t0) * 0.01  # noqa: E731
 
 
@@ -56,7 +58,7 @@ def row(name, a):
 
 
 print(f"== {preset} layer {layer} pos {pos}: {G} workgroups; us from first entry: min p10 p50 p90 max")
-row("entry (all waves)", us(np.concatenate([ld[:, 0], cs[:, :, 0].ravel()])))
+row("entry (all waves)", us(np.concatenate([lds[:, :, 0].ravel(), cs[:, :, 0].ravel()])))
 ops = ["attn_output", "gate+up", "down", "qkv(next)"]
 for k in range(4):
     if ld[:, 1 + 2 * k].max() == 0:
@@ -70,9 +72,9 @@ for k in range(4):
     sp = ld[:, 15 + 2 * k] - (ld[:, 13 + 2 * k] if k > 0 else 0)
     row(f"loader {ops[k]} vmcnt-wait us", vm * 0.01)
     row(f"loader {ops[k]} ring-full us", sp * 0.01)
-row("loader done", us(ld[:, 9]))
-row("loader ring-full waits (count)", ld[:, 10] + t0 - t0)
-row("loader ring-full wait us", ld[:, 11] * 0.01)
+row("loader done (last loader)", us(lds[:, :, 9].max(axis=1)))
+row("loader ring-full waits (count, sum)", lds[:, :, 10].sum(axis=1))
+row("loader ring-full wait us (max)", lds[:, :, 11].max(axis=1) * 0.01)
 for k in range(4):
     e = cs[:, :, 1 + 4 * k]
     if e.max() == 0:
@@ -84,4 +86,4 @@ for k in range(4):
     row(f"{ops[k]} done (wave max)", us(cs[:, :, 4 + 4 * k].max(axis=1)))
     row(f"{ops[k]} ring wait us (wave max)", cs[:, :, 20 + k].max(axis=1) * 0.01)
 row("consumer exit (wave max)", us(cs[:, :, 17].max(axis=1)))
-print(f"  launch span {us(max(cs[:, :, 17].max(), ld[:, 9].max())):.2f} us")
+print(f"  launch span {us(max(cs[:, :, 17].max(), lds[:, :, 9].max())):.2f} us")
