@@ -701,7 +701,8 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
                 double qb[3];
                 if (qkv_groups(l + 1, qn, qb) == 1) { la.op[3] = qn[0]; la.nops = 4; lb += qb[0]; }
             }
-            la.cnt = c.le_cnt + (size_t)l * (le_counter_bytes(1) / 4);
+            la.cnt = c.le_cnt + (size_t)l * kLeOps * 16;
+            la.cnt_stride = le_counter_stride(hp.n_layer);
             la.fault = c.fault_dev;
             if (l == c.le_trace_layer) la.trace = c.le_trace;
             const hipError_t ep = layer_engine_prepare(la);

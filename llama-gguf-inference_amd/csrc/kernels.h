@@ -100,10 +100,11 @@ constexpr int kLeOps = 4;
 struct LeArgs {
     MVArgs op[kLeOps];           // set like launch_matvec's (geometry filled by the launcher)
     int nops = 0;                // 3 (last layer: no next QKV) or 4
-    unsigned* cnt = nullptr;     // this layer's edge counters [kLeOps][8 shards][16 words], zero at launch
+    unsigned* cnt = nullptr;     // this layer's edge counters: shard j of op k at cnt[j * cnt_stride + 16 k], zero at launch
+    size_t cnt_stride = 0;       // words between shards (le_counter_stride)
     unsigned* fault = nullptr;   // context fault word: a bounded in-kernel wait gave up
     int spin_limit = 0;          // polls before a wait gives up (0: default)
-    int kmin = 9;                // smallest sub-item of the launch in ring pieces (sets the loaders' DMA depth)
+    int kmin = 9;                // smallest sub-item of the launch in ring pieces
     // LDS carve (set by the launcher)
     int npieces = 0, img_off0 = 0, img_off1 = 0, fold_off = 0, ring_off = 0, act = -1;
     int exp = 0;                 // LLMI_LE_EXP experiments (results garbage): 1 no math, 2 no edges / images
@@ -111,6 +112,7 @@ struct LeArgs {
 };
 // bytes of the edge counters of n_layer layers (one memset per step zeroes them)
 size_t le_counter_bytes(int n_layer);
+size_t le_counter_stride(int n_layer);  // words
 // fills the geometry and LDS carve; hipErrorNotSupported: shapes / types / LDS / residency
 // the engine does not take (the caller runs the layer as separate launches)
 hipError_t layer_engine_prepare(LeArgs& a);

@@ -53,7 +53,11 @@ namespace llmi {
 namespace {
 
 constexpr int kLeNL = 2;                  // loader waves (waves 0 .. kLeNL-1)
-constexpr int kLeC = 7;                   // consumer waves (waves kLeNL .. kLeNL+6)
+#ifndef LLMI_LE_C
+#define LLMI_LE_C 7
+#endif
+constexpr int kLeC = LLMI_LE_C;           // consumer waves (waves kLeNL .. kLeNL+kLeC-1); experiment builds: -DLLMI_LE_C=n
+static_assert(kLeC >= 1 && kLeC <= 14, "16 wave slots");
 constexpr int kLeT = (kLeNL + kLeC) * 64;  // threads per workgroup
 constexpr int kLeMaxPieces = 136;
 constexpr int kLeTraceWaves = 16;          // trace layout [block][16 waves][32 stamps]
@@ -65,9 +69,10 @@ struct LeCtl {
     unsigned dead;     // a bounded wait gave up: every wave leaves
     unsigned bar;      // consumer-barrier arrivals
     unsigned edge;     // highest op whose input edge the poller wave has seen
-    unsigned cons[8];  // consumer wave w: first ring piece it still needs (monotonic)
+    unsigned cons[16]; // consumer wave w: first ring piece it still needs (monotonic)
     unsigned done[4];  // per op: consumer waves whose stores have drained
-    double red[8];     // RMSNorm partial sums, one per consumer wave
+    unsigned quiet;    // LLMI_LE_EXP & 4: the workgroup is between an op's end and the next image
+    double red[16];    // RMSNorm partial sums, one per consumer wave
 };
 
 // ring pieces (1 KiB = 64 lanes x 16 B) of one sub-item: the A-plane parts, then the H
@@ -171,7 +176,9 @@ __device__ __forceinline__ void le_publish(LeCtl* ctl, LeLoad& L, unsigned v, in
 }
 
 // room in the ring for pieces [p0, p0 + k)?  Waits (publishing everything of its own in
-// flight first) until every consumer has released what the new pieces overwrite.
+// flight first) until every consumer has released what the new pieces overwrite.  (A
+// variant that published its in-flight sub-items one at a time while waiting, never
+// draining the stream, measured slower: DESIGN.md §4 "Layer engine".)
 __device__ __forceinline__ bool le_space(const LeArgs& A, LeCtl* ctl, LeLoad& L, unsigned p0, int k, int l) {
     const unsigned long long end = (unsigned long long)p0 + (unsigned)k, NP = (unsigned)A.npieces;
     if (end <= (unsigned long long)L.lowest + NP) return true;
@@ -269,6 +276,9 @@ __device__ __forceinline__ bool le_load_op(const LeArgs& A, LeCtl* ctl, LeLoad& 
             ++L.sn;
             if (!own) continue;
             if (!le_space(A, ctl, L, p0, k, l)) return false;
+            if (A.exp & 4) {  // experiment: no new weight DMA while the workgroup gathers an edge
+                for (int n = 0; lds_ld(&ctl->quiet) && n < A.spin_limit; ++n) __builtin_amdgcn_s_sleep(1);
+            }
             const LaneUnit lu = lane_unit(g, b, sg, r, ul);
             if constexpr (ACT == 1) {
                 le_issue<T_Q8_0>(sg, lu, (uint32_t)g.U, L.ring, p0, NP);
@@ -342,7 +352,7 @@ typedef unsigned long long __attribute__((address_space(1))) le_gu64;
 template <int ACT, bool NORM, int X86>
 __device__ __forceinline__ bool le_image(const LeArgs& A, const MVArgs& M, uint8_t* img, LeCtl* ctl, int cw, int& barn) {
     constexpr int NTc = kLeC * 64, NR = 4;
-    const int ct = (int)threadIdx.x - 64, cols = M.cols, nsub = cols >> 4;
+    const int ct = (int)threadIdx.x - 64 * kLeNL, cols = M.cols, nsub = cols >> 4;
     const int lane = threadIdx.x & 63;
     Lds L;
     L.act = img;
@@ -378,7 +388,14 @@ __device__ __forceinline__ bool le_image(const LeArgs& A, const MVArgs& M, uint8
         double r[kLeC];
 #pragma unroll
         for (int w = 0; w < kLeC; ++w) r[w] = ctl->red[w];
-        const double t = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + r[6]);
+        double t;
+        if constexpr (kLeC == 7) {
+            t = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + r[6]);
+        } else {
+            t = r[0];
+#pragma unroll
+            for (int w = 1; w < kLeC; ++w) t += r[w];
+        }
         const float mean = (float)(t / (double)cols);
         scale = 1.0f / sqrtf(mean + M.eps);
     }
@@ -411,10 +428,13 @@ __device__ __forceinline__ bool le_edge(const LeArgs& A, LeCtl* ctl, int cw) {
     if (cw == 0) {
         const int lane = threadIdx.x & 63, j = lane & 7, NB = gridDim.x;
         const unsigned tgt = (unsigned)(NB / 8 + (j < (NB & 7) ? 1 : 0));
-        const gu32_t* c = (const gu32_t*)(A.cnt + ((OP - 1) * 8 + j) * 16);
+        const gu32_t* c = (const gu32_t*)(A.cnt + (size_t)j * A.cnt_stride + (OP - 1) * 16);
         for (int n = 0;; ++n) {
             const unsigned v = lane < 8 ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
-            if (__all(v >= tgt)) break;
+            if (__all(v >= tgt)) {
+                LE_STAMP(27 + OP, (unsigned long long)n + 1)
+                break;
+            }
             if (lds_ld(&ctl->dead)) return false;
             if (n >= (A.spin_limit >> 3)) {  // a global poll takes ~8x an LDS poll
                 le_fault(A, ctl, kLeFaultEdge);
@@ -432,7 +452,7 @@ __device__ __forceinline__ bool le_edge(const LeArgs& A, LeCtl* ctl, int cw) {
 template <int T, int ACT, int EPI, bool WT, int X86>
 __device__ __forceinline__ void le_sub(const MVArgs& M, LeCtl* ctl, const uint8_t* ring, unsigned pw, int NP,
                                        const uint8_t* img, float* F, const TaskGeo& g, int s, const Sub& sb, const Seg& sg,
-                                       int r, int ul, unsigned bend, int cw, float& acc, float& vg, int pos) {
+                                       int r, int ul, unsigned bend, int cw, float& acc, float& vg, int pos, float2 pre) {
     const int lane = threadIdx.x & 63;
     const LaneUnit lu = lane_unit(g, sb, sg, r, ul);
     const UnitW<T> w = le_ring_unit<T>(ring, pw, NP, lane, lu.row * (uint32_t)g.U + lu.u);
@@ -442,7 +462,8 @@ __device__ __forceinline__ void le_sub(const MVArgs& M, LeCtl* ctl, const uint8_
     if constexpr (X86) unit_store_x86<T>(w, img + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
     else unit_terms<T>(w, img + (size_t)lu.u * kRec, tm);
     unsigned long long best = 0;
-    sub_finish<ACT, EPI, MVArgs, X86, WT>(M, F, g, s, sb, sg, tm, lu, r, ul, acc, vg, pos, best);
+    sub_finish<ACT, EPI, MVArgs, X86, WT, EPI == EPI_ADD || EPI == EPI_QKV>(M, F, g, s, sb, sg, tm, lu, r, ul, acc, vg,
+                                                                           pos, best, pre);
 }
 
 // ring position of the consumers' walk (identical in every consumer wave)
@@ -479,6 +500,7 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
     LE_STAMP(1 + 4 * OP, LE_NOW)
     // 2. activation image
     if (!(A.exp & 2) && !le_image<ACT, NORM, X86>(A, M, img, ctl, cw, W.barn)) return false;
+    if ((A.exp & 4) && cw == 0) lds_st(&ctl->quiet, 0u);
     LE_STAMP(2 + 4 * OP, LE_NOW)
     bool first_sub = true;
     unsigned long long ring_ticks = 0;
@@ -497,6 +519,23 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
             continue;
         }
         float acc = 0.f, vg = 0.f;
+        // the epilogue's dependent load (residual / RoPE pair) issued now, before the ring
+        // wait and the reduction, instead of behind the weight stream at the task's end
+        float2 pre = float2{0.f, 0.f};
+        if constexpr (EPI == EPI_ADD || EPI == EPI_QKV) {
+            const Sub b0 = sub_of<EPI>(M, g, task, 0);
+            const Seg s0 = le_pick(M, b0.si);
+            const int row = b0.row0 + lane;
+            if (lane < g.R && row < s0.rows) {
+                if constexpr (EPI == EPI_ADD) {
+                    pre.x = ld_f32<true>(M.y + s0.row0 + row);
+                } else {
+                    const int hd = M.head_dim, d = row - (row / hd) * hd;
+                    if ((lane & 1) == 0 && s0.row0 < M.nq + M.nk && d < M.n_rot)
+                        pre = *(const float2*)(M.rope + ((size_t)pos * (M.n_rot / 2) + d / 2) * 2);
+                }
+            }
+        }
         for (int s = 0; s < S; ++s) {
             const Sub sb = sub_of<EPI>(M, g, task, s);
             const Seg sg = le_pick(M, sb.si);
@@ -513,12 +552,12 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
             if (A.exp & 1) {  // experiment: release the pieces unread (results garbage)
                 lds_st(&ctl->cons[cw], b + k);
             } else if constexpr (ACT == 1) {
-                le_sub<T_Q8_0, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos);
+                le_sub<T_Q8_0, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos, pre);
             } else {
                 switch (sg.type) {
-                    case T_Q4_K: le_sub<T_Q4_K, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos); break;
-                    case T_Q5_K: le_sub<T_Q5_K, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos); break;
-                    default: le_sub<T_Q6_K, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos); break;
+                    case T_Q4_K: le_sub<T_Q4_K, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos, pre); break;
+                    case T_Q5_K: le_sub<T_Q5_K, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos, pre); break;
+                    default: le_sub<T_Q6_K, ACT, EPI, WT, X86>(M, ctl, ring, pw, NP, img, F, g, s, sb, sg, r, ul, b + k, cw, acc, vg, pos, pre); break;
                 }
             }
             b += k;
@@ -537,11 +576,14 @@ __device__ __forceinline__ bool le_cons_op(const LeArgs& A, LeCtl* ctl, uint8_t*
     //    the next launch)
     if (OP + 1 < A.nops) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        LE_STAMP(24 + OP, LE_NOW)
         if (lane == 0) {
             const unsigned old = __hip_atomic_fetch_add(&ctl->done[OP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old == kLeC - 1)
-                __hip_atomic_fetch_add((gu32_t*)(A.cnt + (OP * 8 + (blockIdx.x & 7)) * 16), 1u, __ATOMIC_RELAXED,
+            if (old == kLeC - 1) {
+                if (A.exp & 4) lds_st(&ctl->quiet, 1u);
+                __hip_atomic_fetch_add((gu32_t*)(A.cnt + (size_t)(blockIdx.x & 7) * A.cnt_stride + OP * 16), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     return true;
@@ -578,7 +620,13 @@ __global__ __launch_bounds__(kLeT, 1) void k_leng(LeArgs A) {
 
 }  // namespace
 
-size_t le_counter_bytes(int n_layer) { return (size_t)n_layer * kLeOps * 8 * 16 * 4; }
+// Edge counters: 8 shards (one per XCD under round-robin dispatch: blockIdx % 8), each a
+// block [layers][kLeOps][16 words] (64 B per counter); the shards of one counter lie
+// le_counter_stride() words apart (>= 8 KiB) so their 32 arrivals each and the 256
+// pollers' loads spread over memory channels instead of serialising on one or two lines
+// (MI355X_MICROARCH.md fanin: ~12 ns per atomic on one counter).
+size_t le_counter_stride(int n_layer) { return (size_t)std::max(n_layer, 32) * kLeOps * 16; }
+size_t le_counter_bytes(int n_layer) { return 8 * le_counter_stride(n_layer) * 4; }
 
 // the engine's op order and epilogues: attn_output + residual, gate/up + SwiGLU, down +
 // residual, the next layer's QKV + RoPE + KV write
@@ -589,7 +637,8 @@ int g_le_on = [] {  // LLMI_ENGINE: 1 layer engine, 0 separate launches (the def
     return e ? atoi(e) : 0;
 }();
 int g_le_spin = 1 << 20;
-int g_le_exp = [] {  // LLMI_LE_EXP (experiments, results garbage): 1 consumers skip the math, 2 skip edges + images
+int g_le_exp = [] {  // LLMI_LE_EXP (experiments): 1 consumers skip the math, 2 skip edges + images (both: results
+                     // garbage), 4 loaders issue nothing while the workgroup gathers an edge (results exact)
     const char* e = getenv("LLMI_LE_EXP");
     return e ? atoi(e) : 0;
 }();

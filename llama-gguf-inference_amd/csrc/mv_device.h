@@ -1114,9 +1114,12 @@ __device__ __forceinline__ void st_u16(uint16_t* p, uint16_t v) {
 
 // Epilogue of one finished pair (every lane holds both row sums; lane 0 writes).
 // (ANY_LANE: the calling lane writes; the batched matvec runs one token per lane)
-template <int EPI, bool WT = false, class MA, bool ANY_LANE = false, int X86 = 0>
+// PRE (the layer engine, leng.hip): the epilogue's one dependent load was issued early by
+// the caller -- ADD: pre.x = the residual y[row a] (r.vb == 0); QKV: pre = the RoPE (cos,
+// sin) of the pair -- so it does not wait behind the CU's weight stream at the task's end.
+template <int EPI, bool WT = false, class MA, bool ANY_LANE = false, int X86 = 0, bool PRE = false>
 __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, PairSum v, int pos,
-                                         unsigned long long& best) {
+                                         unsigned long long& best, float2 pre = float2{0.f, 0.f}) {
     const int lane = threadIdx.x & 63;
     const float va = v.a, vb = v.b;
     if (!ANY_LANE && lane != 0) return;
@@ -1125,7 +1128,7 @@ __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, P
         if (r.vb) st_f32<WT>(A.y + r.sa.row0 + r.rb, vb);
     } else if constexpr (EPI == EPI_ADD) {
         float* ya = A.y + r.sa.row0 + r.ra;
-        st_f32<WT>(ya, ld_f32<WT>(ya) + va);
+        st_f32<WT>(ya, (PRE ? pre.x : ld_f32<WT>(ya)) + va);
         if (r.vb) {
             float* yb = A.y + r.sa.row0 + r.rb;
             st_f32<WT>(yb, ld_f32<WT>(yb) + vb);
@@ -1148,7 +1151,7 @@ __device__ __forceinline__ void epilogue(const MA& A, const PairRef& r, int p, P
         if (r.sa.row0 < A.nq + A.nk) {
             float o0 = va, o1 = vb;
             if (d < A.n_rot) {  // ggml rope NORM mode on the adjacent pair (d, d+1)
-                const float2 cs = *(const float2*)(A.rope + ((size_t)pos * (A.n_rot / 2) + d / 2) * 2);
+                const float2 cs = PRE ? pre : *(const float2*)(A.rope + ((size_t)pos * (A.n_rot / 2) + d / 2) * 2);
                 o0 = va * cs.x - vb * cs.y;
                 o1 = va * cs.y + vb * cs.x;
             }
@@ -1218,10 +1221,11 @@ __device__ __forceinline__ LaneUnit lane_unit(const TaskGeo& g, const Sub& b, co
 // (X86: the lane's terms are already in F, unit_store_x86; tm is unused)
 // (WT: write-through epilogue stores, for outputs handed to other workgroups of the same
 // launch: the layer engine, leng.hip)
-template <int ACT, int EPI, class MA, int X86 = 0, bool WT = false>
+template <int ACT, int EPI, class MA, int X86 = 0, bool WT = false, bool PRE = false>
 __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo& g, int s, const Sub& b, const Seg& sg,
                                            const float (&tm)[9], const LaneUnit& lu, int r, int ul, float& acc,
-                                           float& vg, int pos, unsigned long long& best) {
+                                           float& vg, int pos, unsigned long long& best,
+                                           float2 pre = float2{0.f, 0.f}) {
     if constexpr (!X86)
         if (lu.valid) store_terms<ACT ? T_Q8_0 : T_Q4_K>(F, r, ul, g.lr, tm);
     wave_lds_sync();
@@ -1247,9 +1251,10 @@ __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo&
                 else epilogue<EPI, WT, MA, true, X86>(A, ref, row, PairSum{vg, v}, pos, best);
             } else if constexpr (EPI == EPI_QKV) {
                 ref.vb = 1;  // RoPE pairs (row, row + 1): R and every segment start are even
-                if ((lane & 1) == 0) epilogue<EPI, WT, MA, true, X86>(A, ref, row, PairSum{v, final_of(lane + 1)}, pos, best);
+                if ((lane & 1) == 0)
+                    epilogue<EPI, WT, MA, true, X86, PRE>(A, ref, row, PairSum{v, final_of(lane + 1)}, pos, best, pre);
             } else {
-                epilogue<EPI, WT, MA, true, X86>(A, ref, row, PairSum{v, 0.f}, pos, best);
+                epilogue<EPI, WT, MA, true, X86, PRE>(A, ref, row, PairSum{v, 0.f}, pos, best, pre);
             }
         }
     }

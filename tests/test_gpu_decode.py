@@ -155,7 +155,10 @@ def test_profile_kernels_leaves_state(gpu, tiny_models):
     prof = c.profile_kernels(nxt, len(prompt), 4)
     n_layer = m.n_layer
     for k, v in prof.items():
-        assert v["us"] > 0 and v["bytes"] > 0, (k, v)
+        if v["launches_per_step"] == 0:  # a class this step does not launch (the layer engine when off)
+            assert v["us"] == 0, (k, v)
+        else:
+            assert v["us"] > 0 and v["bytes"] > 0, (k, v)
     assert prof["embed"]["launches_per_step"] == 1 and prof["output"]["launches_per_step"] == 1
     assert prof["ffn_gate_up"]["launches_per_step"] == n_layer
     assert prof["attention"]["launches_per_step"] == n_layer

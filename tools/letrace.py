@@ -85,5 +85,13 @@ for k in range(4):
     row(f"{ops[k]} first ready (wave min)", us(np.where(fr > 0, fr, fr.max()).min(axis=1)))
     row(f"{ops[k]} done (wave max)", us(cs[:, :, 4 + 4 * k].max(axis=1)))
     row(f"{ops[k]} ring wait us (wave max)", cs[:, :, 20 + k].max(axis=1) * 0.01)
+for k in range(3):
+    if cs[:, :, 24 + k].max() == 0:
+        continue
+    row(f"{ops[k]} stores drained (wave max)", us(cs[:, :, 24 + k].max(axis=1)))
+for k in range(1, 4):
+    if cs[:, 0, 27 + k].max() == 0:
+        continue
+    row(f"{ops[k]} edge polls (poller)", cs[:, 0, 27 + k])
 row("consumer exit (wave max)", us(cs[:, :, 17].max(axis=1)))
 print(f"  launch span {us(max(cs[:, :, 17].max(), lds[:, :, 9].max())):.2f} us")
