@@ -451,6 +451,20 @@ static inline float hsum8(__m256 v) {
     a = _mm_add_ss(a, _mm_movehdup_ps(a));
     return _mm_cvtss_f32(a);
 }
+/* the 8 scales and 8 mins of a Q4_K/Q5_K block at once: upstream's utmp/kmask unpack
+ * (the same values as get_scale_min_k4 j = 0..7, without its per-j branches) */
+static inline void scales_mins_k4(const uint8_t* q, uint8_t* sc, uint8_t* mn) {
+    uint32_t u[4];
+    memcpy(u, q, 12);
+    const uint32_t k1 = 0x3f3f3f3fu, k2 = 0x0f0f0f0fu, k3 = 0x03030303u;
+    u[3] = ((u[2] >> 4) & k2) | (((u[1] >> 6) & k3) << 4);
+    const uint32_t m01 = u[1] & k1;
+    u[1] = (u[2] & k2) | (((u[0] >> 6) & k3) << 4);
+    u[2] = m01;
+    u[0] &= k1;
+    memcpy(sc, u, 8);
+    memcpy(mn, u + 2, 8);
+}
 static inline int kq_mins_dot(const int16_t* bsums, const uint8_t* mn) {
     int s = 0;
     for (int j = 0; j < 16; ++j) s += bsums[j] * mn[j / 2];
@@ -462,7 +476,7 @@ static float fd_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
     __m128 accm4 = _mm_setzero_ps();
     for (int i = 0; i < n / QK_K; ++i) {
         uint8_t sc[8], mn[8];
-        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
+        scales_mins_k4(x[i].scales, sc, mn);
         __m256i sumi = _mm256_setzero_si256();
         for (int j = 0; j < 4; ++j) {
             const __m256i qb = _mm256_loadu_si256((const __m256i*)(x[i].qs + 32 * j));
@@ -491,7 +505,7 @@ static float fd_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
     float summs = 0.f;
     for (int i = 0; i < n / QK_K; ++i) {
         uint8_t sc[8], mn[8];
-        for (int j = 0; j < 8; ++j) get_scale_min_k4(j, x[i].scales, &sc[j], &mn[j]);
+        scales_mins_k4(x[i].scales, sc, mn);
         const __m256i hb = _mm256_loadu_si256((const __m256i*)x[i].qh);
         __m256i sumi = _mm256_setzero_si256();
         for (int j = 0; j < 4; ++j) {
@@ -1037,6 +1051,37 @@ static void matvec_t(const or_tensor* T, const float* x, float* y, int nth) {
     or_matvec(T->type, T->data, T->ne[1], T->ne[0], x, y, nth);
 }
 
+/* or_matvec of n tensors with the same input in ONE parallel loop over all their rows
+ * (q/k/v, gate/up): the activation conversion once per distinct vec_dot type, one
+ * fork/join instead of n.  Each row's dot is or_matvec's. */
+static void matvec_multi(const or_tensor* const* T, int n, const float* x, float* const* y, int nth) {
+    void* act[3] = {NULL, NULL, NULL};
+    int64_t rows0[4] = {0, 0, 0, 0};
+    size_t rb[3];
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < i && !act[i]; ++j)
+            if (or_vec_dot_type(T[j]->type) == or_vec_dot_type(T[i]->type)) act[i] = act[j];
+        if (!act[i]) {
+            act[i] = malloc(act_bytes(T[i]->type, T[i]->ne[0]));
+            quantize_act(T[i]->type, x, act[i], T[i]->ne[0]);
+        }
+        rows0[i + 1] = rows0[i] + T[i]->ne[1];
+        rb[i] = (size_t)(T[i]->ne[0] / or_block_size(T[i]->type)) * or_type_size(T[i]->type);
+    }
+#pragma omp parallel for schedule(static) num_threads(nth > 0 ? nth : 1)
+    for (int64_t g = 0; g < rows0[n]; ++g) {
+        int i = 0;
+        while (g >= rows0[i + 1]) ++i;
+        const int64_t r = g - rows0[i];
+        y[i][r] = or_vec_dot(T[i]->type, (int)T[i]->ne[0], (const uint8_t*)T[i]->data + (size_t)r * rb[i], act[i]);
+    }
+    for (int i = 0; i < n; ++i) {
+        int shared = 0;
+        for (int j = 0; j < i; ++j) shared |= act[j] == act[i];
+        if (!shared) free(act[i]);
+    }
+}
+
 /* Non-flash attention of query head h (roped q, f32[D]) over the layer's first n_kv
  * cached positions: kq = mul_mat(K_f16, q) with q rounded to f16 (ggml_vec_dot_f16,
  * double sum), soft_max_ext(kq, scale 1/sqrt(D)) with a double sum, kqv =
@@ -1123,9 +1168,11 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
     }
     for (int l = 0; l < m->n_layer; ++l) {
         or_rms_norm_mul(m->x, (const float*)m->L[l].an->data, m->xb, E, m->eps);
-        matvec_t(m->L[l].wq, m->xb, m->q, nth);
-        matvec_t(m->L[l].wk, m->xb, m->k, nth);
-        matvec_t(m->L[l].wv, m->xb, m->v, nth);
+        {
+            const or_tensor* const T[3] = {m->L[l].wq, m->L[l].wk, m->L[l].wv};
+            float* const Y[3] = {m->q, m->k, m->v};
+            matvec_multi(T, 3, m->xb, Y, nth);
+        }
         rope_norm(m->q, H, D, m->n_rot, pos, m->rope_base, ff);
         rope_norm(m->k, HK, D, m->n_rot, pos, m->rope_base, ff);
         uint16_t* kl = m->kc + ((size_t)l * m->n_ctx) * kvd;
@@ -1136,8 +1183,11 @@ int or_decode(or_model* m, int32_t token, int32_t pos, float* logits, int nth) {
         matvec_t(m->L[l].wo, m->att, m->tmp, nth);
         for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
         or_rms_norm_mul(m->x, (const float*)m->L[l].fn->data, m->xb, E, m->eps);
-        matvec_t(m->L[l].wg, m->xb, m->hb, nth);
-        matvec_t(m->L[l].wu, m->xb, m->hb2, nth);
+        {
+            const or_tensor* const T[2] = {m->L[l].wg, m->L[l].wu};
+            float* const Y[2] = {m->hb, m->hb2};
+            matvec_multi(T, 2, m->xb, Y, nth);
+        }
         for (int i = 0; i < F; ++i) m->hb[i] = mode_silu(m->hb[i]) * m->hb2[i];
         matvec_t(m->L[l].wd, m->hb, m->tmp, nth);
         for (int i = 0; i < E; ++i) m->x[i] = m->tmp[i] + m->x[i];
