@@ -59,6 +59,11 @@ struct llama_model_params {
 };
 #define LLMI_NUMERICS_GENERIC 0
 #define LLMI_NUMERICS_X86 1
+/* OR-ed into either: decode attention in ggml's CPU flash-attention numerics (online
+ * softmax, f16 V accumulation, glibc expf; what a llama-server without --flash-attn runs
+ * when -fa auto resolves to on), oracle flag OR_X86_FA.  Such a model runs prompts as
+ * decode steps and batched sequences one after another; up to 8192 positions. */
+#define LLMI_NUMERICS_FA 2
 
 /* upstream llama_context_params (subset) */
 struct llama_context_params {

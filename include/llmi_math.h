@@ -108,6 +108,70 @@ LLMI_HD float llmi_expf(float x) {
     return p * llmi_u2f((uint32_t)(n + 127) << 23);
 }
 
+/* glibc's expf (sysdeps/ieee754/flt-32/e_expf.c, the ARM optimized-routines algorithm,
+ * glibc >= 2.27; upstream, not vendored), restated for the flash-attention numerics
+ * (ggml's CPU flash_attn_ext calls libm expf for its online-softmax factors):
+ * x*32/ln2 = k + r in double, 2^(k/32) from a 32-entry table of correctly rounded
+ * doubles, a degree-3 polynomial in r, one final double -> float rounding.  FMA: the
+ * glibc build an x86-64 FMA host dispatches to (__expf_fma) contracts the polynomial's
+ * a*b+c; fma != 0 selects that form.  Which form equals THIS host's libm is checked
+ * exhaustively over the softmax range by tests/test_oracle_math.py. */
+LLMI_HD uint64_t llmi_d2u(double d) {
+    union { double d; uint64_t u; } v; v.d = d; return v.u;
+}
+LLMI_HD double llmi_u2d(uint64_t u) {
+    union { double d; uint64_t u; } v; v.u = u; return v.d;
+}
+LLMI_HD uint64_t llmi_exp2f_tab(uint32_t i) {  /* asuint64(2^(i/32)) - (i << 47) */
+    switch (i & 31u) {
+        case 0: return 0x3ff0000000000000ull; case 1: return 0x3fefd9b0d3158574ull;
+        case 2: return 0x3fefb5586cf9890full; case 3: return 0x3fef9301d0125b51ull;
+        case 4: return 0x3fef72b83c7d517bull; case 5: return 0x3fef54873168b9aaull;
+        case 6: return 0x3fef387a6e756238ull; case 7: return 0x3fef1e9df51fdee1ull;
+        case 8: return 0x3fef06fe0a31b715ull; case 9: return 0x3feef1a7373aa9cbull;
+        case 10: return 0x3feedea64c123422ull; case 11: return 0x3feece086061892dull;
+        case 12: return 0x3feebfdad5362a27ull; case 13: return 0x3feeb42b569d4f82ull;
+        case 14: return 0x3feeab07dd485429ull; case 15: return 0x3feea47eb03a5585ull;
+        case 16: return 0x3feea09e667f3bcdull; case 17: return 0x3fee9f75e8ec5f74ull;
+        case 18: return 0x3feea11473eb0187ull; case 19: return 0x3feea589994cce13ull;
+        case 20: return 0x3feeace5422aa0dbull; case 21: return 0x3feeb737b0cdc5e5ull;
+        case 22: return 0x3feec49182a3f090ull; case 23: return 0x3feed503b23e255dull;
+        case 24: return 0x3feee89f995ad3adull; case 25: return 0x3feeff76f2fb5e47ull;
+        case 26: return 0x3fef199bdd85529cull; case 27: return 0x3fef3720dcef9069ull;
+        case 28: return 0x3fef5818dcfba487ull; case 29: return 0x3fef7c97337b9b5full;
+        case 30: return 0x3fefa4afa2a490daull; default: return 0x3fefd0765b6e4540ull;
+    }
+}
+LLMI_HD double llmi_fma_d(double a, double b, double c, int fma) { return fma ? __builtin_fma(a, b, c) : a * b + c; }
+LLMI_HD float llmi_expf_glibc(float x, int fma) {
+    const uint32_t abstop = (llmi_f2u(x) >> 20) & 0x7ffu;
+    if (abstop >= 0x42bu) {                 /* |x| >= 88 or nan (top12(88.0f) = 0x42b) */
+        if (llmi_f2u(x) == 0xff800000u) return 0.0f;
+        if (abstop >= 0x7f8u) return x + x;
+        if (x > 88.72283172607421875f) return llmi_u2f(0x7f800000u);   /* 0x1.62e42ep6 */
+        if (x < -103.97207641601562f) return 0.0f;                     /* -0x1.9fe368p6 */
+    }
+    const double InvLn2N = 0x1.71547652b82fep+0 * 32, SHIFT = 0x1.8p+52;
+    const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+                 C2 = 0x1.62e42ff0c52d6p-1 / 32;
+    const double xd = (double)x;
+    /* the FMA build contracts every add/sub use of InvLn2N * xd, i.e. both: the
+     * rounding to k and r are then taken from the exact product */
+    double kd = fma ? __builtin_fma(InvLn2N, xd, SHIFT) : InvLn2N * xd + SHIFT;
+    const uint64_t ki = llmi_d2u(kd);
+    kd -= SHIFT;
+    const double r = fma ? __builtin_fma(InvLn2N, xd, -kd) : InvLn2N * xd - kd;
+    double z;
+    const uint64_t t = llmi_exp2f_tab((uint32_t)ki) + (ki << 47);
+    const double s = llmi_u2d(t);
+    z = llmi_fma_d(C0, r, C1, fma);
+    const double r2 = r * r;
+    double y = llmi_fma_d(C2, r, 1.0, fma);
+    y = llmi_fma_d(z, r2, y, fma);
+    y = y * s;
+    return (float)y;
+}
+
 /* ggml SiLU: x / (1 + exp(-x)) with the shared exp. */
 LLMI_HD float llmi_silu(float x) { return x / (1.0f + llmi_expf(-x)); }
 

@@ -87,7 +87,9 @@ extern "C" {
 
 const char* llmi_last_error(void) { return g_err.c_str(); }
 
-int32_t llmi_model_numerics(const struct llama_model* model) { return model ? model->m.numerics : -1; }
+int32_t llmi_model_numerics(const struct llama_model* model) {
+    return model ? model->m.numerics | (model->m.fa ? NUMERICS_FA : 0) : -1;
+}
 
 void llama_backend_init(void) { (void)hipInit(0); }
 void llama_backend_free(void) {}
@@ -475,7 +477,7 @@ int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const i
         context_select_seq(c, seqs[0]);
         return llmi_generate_greedy(ctx, first[0], pos0[0], n_gen, out);
     }
-    if (c.m->numerics != NUMERICS_GENERIC) {  // no batched step in x86 numerics: one sequence after another
+    if (c.m->numerics != NUMERICS_GENERIC || c.m->fa) {  // no batched step in x86 / FA numerics: one sequence after another
         for (int k = 0; k < n; ++k) {
             context_select_seq(c, seqs[k]);
             const int32_t r = llmi_generate_greedy(ctx, first[k], pos0[k], n_gen, out + (size_t)k * n_gen);
@@ -654,8 +656,8 @@ int32_t llmi_test_option(const char* name, int32_t value) {
     int* opt = nullptr;
     if (!strcmp(name, "numerics")) {
         const int old = t_hook_numerics;
-        if (value == NUMERICS_GENERIC || value == NUMERICS_X86) t_hook_numerics = value;
-        else if (value >= 0) { set_err("llmi_test_option: numerics must be 0 or 1"); return -1; }
+        if (value >= 0 && value <= (NUMERICS_X86 | NUMERICS_FA)) t_hook_numerics = value;
+        else if (value >= 0) { set_err("llmi_test_option: numerics must be 0..3"); return -1; }
         return old;
     }
     if (!strcmp(name, "pf_attn_simple")) opt = &g_pf_attn_simple;
@@ -1318,7 +1320,7 @@ static Seg seg_at(int32_t type, const void* w, int64_t rows, int64_t cols) {
     s.rows = (int)rows;
     s.row0 = 0;
     s.rgs = dm.rgs;
-    s.x86 = t_hook_numerics == NUMERICS_X86;
+    s.x86 = (t_hook_numerics & NUMERICS_X86) != 0;
     return s;
 }
 
@@ -1338,7 +1340,7 @@ int32_t llmi_repack(int32_t type, const void* raw, void* w, int64_t rows, int64_
     if (needs_repack(type)) {
         e = launch_repack(type, raw, (uint8_t*)w + dm.off_a, (uint8_t*)w + dm.off_h, (uint8_t*)w + dm.off_s,
                           (uint8_t*)w + dm.off_d, rows * (cols / block_elems(type)), cols, dm.rgs,
-                          t_hook_numerics == NUMERICS_X86, nullptr);
+                          (t_hook_numerics & NUMERICS_X86) != 0, nullptr);
     } else {
         e = hipMemcpy(w, raw, dm.bytes, hipMemcpyDeviceToDevice);
     }
@@ -1359,7 +1361,7 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
     a.cols = (int)cols;
     a.npairs = (int)((rows + 1) / 2);
     a.x = x; a.nw = nw; a.eps = eps; a.y = y;
-    a.num = t_hook_numerics;
+    a.num = t_hook_numerics & NUMERICS_X86;
     int dev = 0;
     (void)hipGetDevice(&dev);
     hipDeviceProp_t prop;
@@ -1373,7 +1375,7 @@ int32_t llmi_matvec(int32_t type, const void* w, int64_t rows, int64_t cols, con
 int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, const float* x, const float* nw, float eps,
                      int32_t n_tok, float* y, double* usec) {
     if (!pf_gemm_ok(type, (int)rows, (int)cols) || n_tok <= 0) { set_err("llmi_pf_gemm: unsupported type/shape"); return -1; }
-    const int x86 = t_hook_numerics == NUMERICS_X86;
+    const int x86 = (t_hook_numerics & NUMERICS_X86) != 0;
     if (x86 && type == T_Q8_0) { set_err("llmi_pf_gemm: x86 numerics take K-quants only"); return -1; }
     const int tpad = (n_tok + 63) / 64 * 64;
     void* aq = nullptr;
@@ -1414,7 +1416,7 @@ int32_t llmi_quantize_act(int32_t type, int64_t cols, const float* x, const floa
     if (cols % 256) { set_err("cols must be a multiple of 256"); return -1; }
     MVArgs a;
     a.cols = (int)cols; a.x = x; a.nw = nw; a.eps = eps;
-    a.num = t_hook_numerics;
+    a.num = t_hook_numerics & NUMERICS_X86;
     hipError_t e = launch_quant_dump(a, act_kind(type), out, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) { set_err(hip_err(e)); return -2; }
@@ -1563,7 +1565,8 @@ int32_t llmi_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim, int3
     a.tmax = scores + (size_t)n_head * n_ctx;
     a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
     a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);
-    a.num = t_hook_numerics;
+    a.num = t_hook_numerics & NUMERICS_X86;
+    a.fa = (t_hook_numerics & NUMERICS_FA) ? 1 : 0;
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
     hipError_t e = launch_attention(a, n_head, n_head_kv, head_dim, kv_bound, nullptr, mode);
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1648,7 +1651,7 @@ double llmi_bench_attention(int32_t n_head, int32_t n_head_kv, int32_t head_dim,
     const int kv_bound = std::min(n_ctx, (n_kv + 255) / 256 * 256);
     AttnArgs a;
     a.q = q; a.scores = scores; a.out = out; a.st = st; a.n_ctx = n_ctx; a.scale = 1.0f / sqrtf((float)head_dim);
-    a.num = t_hook_numerics;
+    a.num = t_hook_numerics & NUMERICS_X86;
     a.tmax = scores + (size_t)n_head * n_ctx;
     a.gran = (unsigned long long*)(scores + attn_gran_off(n_head, n_ctx));
     a.fault = (unsigned*)(scores + attn_gran_off(n_head, n_ctx) + 2 * (size_t)n_head * kXAttnMaxKV);

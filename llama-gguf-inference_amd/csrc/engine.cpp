@@ -125,8 +125,9 @@ bool model_load(const std::string& path, int device, bool vocab_only, bool no_up
                 const UploadHook* hook, int numerics) {
     M.path = path;
     M.device = device;
-    if (numerics != NUMERICS_GENERIC && numerics != NUMERICS_X86) { err = "unknown numerics " + std::to_string(numerics); return false; }
-    M.numerics = numerics;
+    if (numerics < 0 || numerics > (NUMERICS_X86 | NUMERICS_FA)) { err = "unknown numerics " + std::to_string(numerics); return false; }
+    M.numerics = numerics & NUMERICS_X86;
+    M.fa = (numerics & NUMERICS_FA) ? 1 : 0;
     M.file = std::make_shared<GgufFile>();
     GgufFile& f = *M.file;
     if (!f.open(path, err)) return false;
@@ -361,6 +362,7 @@ bool model_upload(Model& M, std::string& err, const UploadHook* hook) {
 bool model_clone_layout(const Model& src, int device, Model& dst, std::string& err) {
     dst.device = device;
     dst.numerics = src.numerics;
+    dst.fa = src.fa;
     dst.path = src.path;
     dst.desc = src.desc;
     dst.file = src.file;
@@ -675,6 +677,7 @@ bool step_enqueue(Context& c, int kv_bound, std::string& err) {
         at.gran = (unsigned long long*)(c.scores + attn_gran_off(hp.n_head, c.n_ctx));
         at.fault = c.fault_dev;
         at.num = num;
+        at.fa = m.fa;
         LLMI_RUN(K_ATTN, launch_attention(at, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         if (P) P->add(K_ATTN, 8.0 * nq, 2.0 * kvpos);
         // --- output projection + residual ---
@@ -898,7 +901,7 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
 bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err) {
     const HParams& hp = c.m->hp;
     if (nt < 1 || nt > kMaxBatch || c.n_seq < 2) { err = "batched step: 1..8 slots of a context with n_seq_max >= 2"; return false; }
-    if (c.m->numerics != NUMERICS_GENERIC) { err = "batched step: generic numerics only (x86 numerics decode one sequence per step)"; return false; }
+    if (c.m->numerics != NUMERICS_GENERIC || c.m->fa) { err = "batched step: generic numerics only (x86 / flash-attention numerics decode one sequence per step)"; return false; }
     for (const Layer& L : c.m->layers)
         if (L.wg.type != L.wu.type) { err = "batched step: ffn_gate / ffn_up of different types"; return false; }
     if (!balloc(c, err)) return false;
@@ -948,6 +951,7 @@ bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& er
 // ---------------------------------------------------------------------------------
 bool prefill_supported(const Model& m) {
     const HParams& hp = m.hp;
+    if (m.fa) return false;  // flash-attention numerics: prompts as decode steps (attnfa.hip is decode-only)
     if (hp.head_dim != 128 && hp.head_dim != 64) return false;
     if (hp.n_rot % 2 || hp.n_rot > hp.head_dim) return false;
     const bool x86 = m.numerics == NUMERICS_X86;

@@ -32,11 +32,15 @@ struct Layer {
 //   1 upstream's x86 AVX2 association (the oracle's or_set_x86_mode(X86_ALL)): the weight
 //     planes in the x86 byte order (common.h), fma chains per 4-byte lane, the x86
 //     attention (attn86.hip), ggml_v_expf softmax / SiLU, round-half-even q8_0
-enum : int { NUMERICS_GENERIC = 0, NUMERICS_X86 = 1 };
+//   + NUMERICS_FA (bit 1 of llama_model_params.numerics): decode attention in ggml's CPU
+//     flash-attention numerics (attnfa.hip) in the association of bit 0; such a model
+//     runs prompts as decode steps and batched sequences one after another
+enum : int { NUMERICS_GENERIC = 0, NUMERICS_X86 = 1, NUMERICS_FA = 2 };
 
 struct Model {
     int device = 0;
     int numerics = NUMERICS_GENERIC;      // fixed at load: the weight planes' byte order depends on it
+    int fa = 0;                           // 1: flash-attention numerics (NUMERICS_FA)
     std::string path, desc;
     std::shared_ptr<GgufFile> file;
     HParams hp;

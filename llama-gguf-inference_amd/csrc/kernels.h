@@ -138,6 +138,7 @@ struct AttnArgs {
     int tag_skew = 0;                     // test option: consumers expect tag + skew
     unsigned long long* trace = nullptr;  // LLMI_EXP_TRACE builds: [kernel][block][wave][4] stamps
     int num = 0;                          // numerics (MVArgs::num): 1 = the x86 attention kernels (attn86.hip)
+    int fa = 0;                           // 1: flash-attention numerics (attnfa.hip; num picks its association)
 };
 
 // Batched decode (batch.hip): up to kMaxBatch sequences advance one token per step.
@@ -256,6 +257,9 @@ int attn_d_slices(int n_head, int head_dim);
 // arm (or with nullptrs disarm) per-op kernel timing events for this thread's launches
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 void set_attn_mode(int mode);
+// flash-attention numerics decode attention (attnfa.hip): up to kFaMaxKV positions
+constexpr int kFaMaxKV = 8192;
+hipError_t launch_attention_fa(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream,
                             int mode = -1);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);

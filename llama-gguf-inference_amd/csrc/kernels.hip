@@ -1261,6 +1261,7 @@ int attn_path(int n_head, int n_head_kv, int kv_bound, int head_dim, int mode) {
 hipError_t launch_attention(const AttnArgs& a0, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s,
                             int mode) {
     if (n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    if (a0.fa) return launch_attention_fa(a0, n_head, n_head_kv, head_dim, kv_bound, s);
     if (a0.num) return launch_attention_x86(a0, n_head, n_head_kv, head_dim, kv_bound, s, mode < 0 ? g_attn_mode : mode);
     AttnArgs a = a0;
     a.spin_limit = g_xspin_limit;

@@ -19,7 +19,7 @@ from ._lib import LlmiLibraryError, last_error, lib, llama_context_params, llama
 F32, F16, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 8, 12, 13, 14, 15
 # model numerics (llama_model_params.numerics): ggml's generic scalar order, or upstream's
 # x86 AVX2 association (the reference's NGL=0 build)
-NUMERICS_GENERIC, NUMERICS_X86 = 0, 1
+NUMERICS_GENERIC, NUMERICS_X86, NUMERICS_FA = 0, 1, 2  # NUMERICS_FA is OR-ed into either (llmi.h)
 PRESETS = (
     "llama3-8b-q4km", "llama3-70b-q4km", "tinyllama-q8_0", "mistral7b-q6k", "mistral7b-q5km",
     "tiny-mixed", "tiny-mixed-d128",

@@ -57,6 +57,26 @@ static inline float mode_expf(float x);
 /* exp as the softmax / SiLU use it: llmi_expf (generic), ggml_v_expf or libm expf (x86 mode) */
 float or_expf(float x) { return mode_expf(x); }
 
+/* llmi_expf_glibc (llmi_math.h) against THIS host's libm expf for every float in
+ * [lo, hi] (both finite, lo <= hi): the number of inputs whose bits differ, and the
+ * first such input in *first.  Test infrastructure: pins the restatement the
+ * flash-attention numerics use to a real glibc. */
+int64_t or_expf_glibc_check(float lo, float hi, int fma, int stride, float* first) {
+    int64_t bad = 0;
+    /* walk the float line from lo to hi in order (every stride-th float) */
+    float x = lo;
+    for (;;) {
+        const float a = llmi_expf_glibc(x, fma), b = expf(x);
+        if (llmi_f2u(a) != llmi_f2u(b)) {
+            if (!bad && first) *first = x;
+            ++bad;
+        }
+        if (x >= hi) break;
+        for (int i = 0; i < stride && x < hi; ++i) x = nextafterf(x, hi);
+    }
+    return bad;
+}
+
 size_t or_type_size(int t) {
     switch (t) {
         case OR_F32: return 4; case OR_F16: return 2; case OR_Q8_0: return 34;
@@ -593,8 +613,10 @@ int or_set_fast_dots(int on) { g_fast = 0; (void)on; return 0; }  /* no AVX2 in 
  *   OR_X86_VEXP   ggml_v_expf / ggml_v_silu (AVX2 polynomial exp) in soft_max and SwiGLU,
  *                 and ggml_vec_soft_max_f32's sum: per 8 positions an fp32 hsum, added in double
  *   OR_X86_LIBM   libm expf in soft_max and SiLU (scalar sums) instead of llmi_expf
- *   OR_X86_NOFMA  Q5_K's scalar min term without FMA contraction (-ffp-contract=off build) */
-enum { OR_X86_DOTS = 1, OR_X86_Q80 = 2, OR_X86_F16DOT = 4, OR_X86_VEXP = 8, OR_X86_LIBM = 16, OR_X86_NOFMA = 32 };
+ *   OR_X86_NOFMA  Q5_K's scalar min term without FMA contraction (-ffp-contract=off build)
+ *   OR_X86_FA     flash attention instead of the non-flash path (attn_head_fa below) */
+enum { OR_X86_DOTS = 1, OR_X86_Q80 = 2, OR_X86_F16DOT = 4, OR_X86_VEXP = 8, OR_X86_LIBM = 16, OR_X86_NOFMA = 32,
+       OR_X86_FA = 64 };
 static int g_x86 = 0;
 int or_set_x86_mode(int flags) { g_x86 = flags; return g_x86; }
 int or_get_x86_mode(void) { return g_x86; }
@@ -1082,11 +1104,71 @@ static void matvec_multi(const or_tensor* const* T, int n, const float* x, float
     }
 }
 
+/* Flash attention of query head h (OR_X86_FA): upstream's CPU
+ * ggml_compute_forward_flash_attn_ext_f16 for one query row with f16 K and V [ggml-cpu
+ * ops.cpp, "one_chunk"; upstream, recalled, not vendored] -- what a llama-server started
+ * without --flash-attn runs on the CPU when `-fa auto` resolves to on:
+ *   q16 = f16(q); S = 0, M = -inf, VKQ16[D] = 0 (f16)
+ *   per position t: s = ggml_vec_dot_f16(K[t], q16) * scale (+ 0, the unmasked mask)
+ *     s > M: M = s, ms = expf(Mold - M), VKQ16 = f16(f32(VKQ16) * ms)   (vec_scale_f16)
+ *     else:  vs = expf(s - M)
+ *     VKQ16 = f16(f32(VKQ16) + f32(V[t]) * vs)                           (vec_mad_f16)
+ *     S = S * ms + vs
+ *   out = f32(VKQ16) * (S == 0 ? 0 : 1 / S)                               (vec_scale_f32)
+ * expf is libm's (llmi_expf_glibc with FMA: what glibc's ifunc picks on an FMA host,
+ * whichever ggml-cpu variant calls it; pinned to this host's libm, test_oracle_math.py).
+ * With OR_X86_F16DOT (the AVX2+F16C build) the dot is the 4 x 8-lane form and vec_mad /
+ * the S update are FMA-contracted; without it (the generic scalar build, no FMA) they are
+ * a multiply and an add.  Single-query rows only: prompts run through it token by token. */
+static void attn_head_fa(const or_model* m, int l, const float* q, int h, int n_kv, float* out) {
+    const int HK = m->n_head_kv, D = m->head_dim, kvd = HK * D, g = h / (m->n_head / HK);
+    const uint16_t* kl = m->kc + ((size_t)l * m->n_ctx) * kvd;
+    const uint16_t* vl = m->vc + ((size_t)l * m->n_ctx) * kvd;
+    const float scale = 1.0f / sqrtf((float)D);
+    const int x86 = (g_x86 & OR_X86_F16DOT) != 0;
+    float qf[512], kf[512], vkq[512];
+    uint16_t vkq16[512];
+    for (int d = 0; d < D; ++d) { qf[d] = llmi_h2f(llmi_f2h(q[d])); vkq16[d] = 0; }
+    float S = 0.0f, M = -INFINITY;
+    for (int t = 0; t < n_kv; ++t) {
+        const uint16_t* kr = kl + (size_t)t * kvd + (size_t)g * D;
+        const uint16_t* vr = vl + (size_t)t * kvd + (size_t)g * D;
+        float sc;
+        if (x86) {
+            for (int d = 0; d < D; ++d) kf[d] = llmi_h2f(kr[d]);
+            sc = x86_dot_f16f(D, kf, qf);
+        } else {
+            double sumf = 0.0;
+            for (int d = 0; d < D; ++d) sumf += (double)(llmi_h2f(kr[d]) * qf[d]);
+            sc = (float)sumf;
+        }
+        sc = sc * scale;
+        sc = sc + 0.0f;  /* s += slope * mask (0 for every position the query sees) */
+        const float Mold = M;
+        float ms = 1.0f, vs = 1.0f;
+        if (sc > M) {
+            M = sc;
+            ms = llmi_expf_glibc(Mold - M, 1);
+            for (int d = 0; d < D; ++d) vkq16[d] = llmi_f2h(llmi_h2f(vkq16[d]) * ms);
+        } else {
+            vs = llmi_expf_glibc(sc - M, 1);
+        }
+        for (int d = 0; d < D; ++d)
+            vkq16[d] = llmi_f2h(x86 ? fmaf(llmi_h2f(vr[d]), vs, llmi_h2f(vkq16[d]))
+                                    : llmi_h2f(vkq16[d]) + llmi_h2f(vr[d]) * vs);
+        S = x86 ? fmaf(S, ms, vs) : S * ms + vs;
+    }
+    const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
+    for (int d = 0; d < D; ++d) vkq[d] = llmi_h2f(vkq16[d]);
+    for (int d = 0; d < D; ++d) out[d] = vkq[d] * S_inv;
+}
+
 /* Non-flash attention of query head h (roped q, f32[D]) over the layer's first n_kv
  * cached positions: kq = mul_mat(K_f16, q) with q rounded to f16 (ggml_vec_dot_f16,
  * double sum), soft_max_ext(kq, scale 1/sqrt(D)) with a double sum, kqv =
  * mul_mat(V_f16, kq) with the probabilities rounded to f16.  w: f32[n_kv] scratch. */
 static void attn_head(const or_model* m, int l, const float* q, int h, int n_kv, float* w, float* out) {
+    if (g_x86 & OR_X86_FA) { attn_head_fa(m, l, q, h, n_kv, out); return; }
     const int HK = m->n_head_kv, D = m->head_dim, kvd = HK * D, g = h / (m->n_head / HK);
     const uint16_t* kl = m->kc + ((size_t)l * m->n_ctx) * kvd;
     const uint16_t* vl = m->vc + ((size_t)l * m->n_ctx) * kvd;

@@ -35,6 +35,7 @@ int or_vec_dot_type(int wtype); /* activation type the CPU quantizes to for this
 float or_fp16_to_fp32(uint16_t h);
 uint16_t or_fp32_to_fp16(float f);
 float or_expf(float x);
+int64_t or_expf_glibc_check(float lo, float hi, int fma, int stride, float* first);
 
 /* ggml dequantize_row_<type> (upstream ggml-quants.c) */
 int or_dequantize_row(int type, const void* src, float* dst, int64_t n);

@@ -45,7 +45,7 @@ def set_fast_dots(on: bool) -> bool:
 
 
 # x86 association flags (ggml_oracle.c "x86 association mode"): parity MEASUREMENT only
-X86_DOTS, X86_Q80, X86_F16DOT, X86_VEXP, X86_LIBM, X86_NOFMA = 1, 2, 4, 8, 16, 32
+X86_DOTS, X86_Q80, X86_F16DOT, X86_VEXP, X86_LIBM, X86_NOFMA, X86_FA = 1, 2, 4, 8, 16, 32, 64
 X86_ALL = X86_DOTS | X86_Q80 | X86_F16DOT | X86_VEXP  # upstream's AVX2 build as restated
 
 
@@ -69,6 +69,7 @@ def lib() -> C.CDLL:
         "or_fp16_to_fp32": (C.c_float, [C.c_uint16]),
         "or_fp32_to_fp16": (C.c_uint16, [C.c_float]),
         "or_expf": (C.c_float, [C.c_float]),
+        "or_expf_glibc_check": (C.c_int64, [C.c_float, C.c_float, C.c_int, C.c_int, C.POINTER(C.c_float)]),
         "or_dequantize_row": (C.c_int, [C.c_int, P, P, C.c_int64]),
         "or_quantize_row_q8_K": (None, [P, P, C.c_int64]),
         "or_quantize_row_q8_0": (None, [P, P, C.c_int64]),

@@ -66,3 +66,26 @@ def test_llmi_expf_special_values():
     assert L.or_expf(89.0) == float("inf") and L.or_expf(float("inf")) == float("inf")
     assert L.or_expf(-104.0) == 0.0 and L.or_expf(float("-inf")) == 0.0
     assert L.or_expf(0.0) == 1.0
+
+
+def _host_has_fma() -> bool:
+    try:
+        return " fma " in open("/proc/cpuinfo").read().replace("\n", " ")
+    except OSError:
+        return False
+
+
+def test_glibc_expf_restatement_equals_host_libm():
+    """llmi_expf_glibc (the flash-attention numerics' exp, llmi_math.h) equals this host's
+    libm expf bit for bit.  On an FMA host glibc dispatches to the build whose compiler
+    contracted every add/sub use of InvLn2N*x and the polynomial's a*b+c (fma=1); without
+    FMA the plain build (fma=0).  Here every 61st float of the softmax range [-104, 0] and
+    of (0, 88.7], plus the two inputs where the two builds differ (found by the exhaustive
+    run: all 2.1e9 floats of [-104, 88.7] agree)."""
+    L = pyoracle.lib()
+    fma = 1 if _host_has_fma() else 0
+    first = C.c_float(0)
+    assert L.or_expf_glibc_check(-104.0, 0.0, fma, 61, C.byref(first)) == 0, first.value
+    assert L.or_expf_glibc_check(0.0, 88.7, fma, 61, C.byref(first)) == 0, first.value
+    for x in (-63.09946060180664, 32.564632415771484):  # 1 ulp apart between the builds
+        assert L.or_expf_glibc_check(x, x, fma, 1, C.byref(first)) == 0, x

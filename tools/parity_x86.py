@@ -40,11 +40,11 @@ def top2(v: np.ndarray):
 
 
 def run(path: str, n_prompt: int, n_gen: int, flags: int, seed: int = 21, threads: int = 0,
-        n_vocab_prompt: int = 30000) -> dict:
+        n_vocab_prompt: int = 30000, ref_flags: int = 0) -> dict:
     rng = np.random.default_rng(seed)
     prompt = [1] + [int(t) for t in rng.integers(3, n_vocab_prompt, n_prompt - 1)]
     n_ctx = (n_prompt + n_gen + 255) // 256 * 256
-    g = po.OracleModel(path, n_ctx=n_ctx, threads=threads, x86=0)
+    g = po.OracleModel(path, n_ctx=n_ctx, threads=threads, x86=ref_flags)
     x = po.OracleModel(path, n_ctx=n_ctx, threads=threads, x86=flags)
     prompt = [t % g.n_vocab for t in prompt]
     t0 = time.time()
@@ -87,6 +87,9 @@ def main() -> None:
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--gen", type=int, default=512)
     ap.add_argument("--flags", type=int, default=po.X86_ALL)
+    ap.add_argument("--ref-flags", type=int, default=0,
+                    help="the reference run's oracle flags (0 = generic; e.g. 64 = generic + flash attention): "
+                         "the trajectory is teacher-forced with ITS ids; the 'generic_*' fields then mean 'reference'")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--dir", default="/tmp/llmi_parity")
     ap.add_argument("--out", default="")
@@ -98,13 +101,15 @@ def main() -> None:
         llmi.write_synthetic_gguf(path, args.preset, seed=3, n_layer=args.layers, n_vocab=args.vocab)
     po.prefer_simd()
     rep = {"preset": args.preset, "n_layer": args.layers, "n_vocab": args.vocab or "full",
-           "prompt": args.prompt, "gen": args.gen, "x86_flags": args.flags,
+           "prompt": args.prompt, "gen": args.gen, "x86_flags": args.flags, "ref_flags": args.ref_flags,
            "x86_parts": [n for n, b in (("dots", po.X86_DOTS), ("q8_0", po.X86_Q80), ("f16dot", po.X86_F16DOT),
                                         ("v_expf", po.X86_VEXP), ("libm_expf", po.X86_LIBM),
-                                        ("no_fma", po.X86_NOFMA)) if args.flags & b],
+                                        ("no_fma", po.X86_NOFMA), ("flash_attn", po.X86_FA)) if args.flags & b],
+           "ref_parts": [n for n, b in (("dots", po.X86_DOTS), ("q8_0", po.X86_Q80), ("f16dot", po.X86_F16DOT),
+                                        ("v_expf", po.X86_VEXP), ("flash_attn", po.X86_FA)) if args.ref_flags & b] or ["generic"],
            "note": "generic (== GPU bit for bit) vs upstream x86 AVX2 association as restated in "
                    "oracle/ggml_oracle.c (recalled, not vendored); teacher-forced with the generic ids"}
-    rep.update(run(path, args.prompt, args.gen, args.flags, threads=args.threads))
+    rep.update(run(path, args.prompt, args.gen, args.flags, threads=args.threads, ref_flags=args.ref_flags))
     line = json.dumps(rep)
     print(line, flush=True)
     if args.out:
