@@ -80,6 +80,7 @@ struct MVArgs {
     int split_tasks = 0;                   // two-type launches: tasks of the first type group ...
     int split_wgs = 0;                     // ... and the workgroups that run them
     int xfirst = 0;                        // experiment: 1 multi-round launches also wait for x before weights, -1 none does
+    int fw = 0;                            // 1: a wave's second sub-item is issued only once its first has landed (LLMI_MV_FW)
     int prio_alt = 0;                      // experiment builds: alternate s_setprio per sub-item (blocks >= prio_alt: other phase)
     // batched decode (batch.hip, k_mvn): token t of the batch is one decode step of
     // sequence tseq[t] at position tpos[t]; x / y rows are x_stride / y_stride floats

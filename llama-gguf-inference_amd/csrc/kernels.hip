@@ -1079,9 +1079,21 @@ bool mv_geometry(MVArgs& a, int epi) {
     return a.ntasks > 0;
 }
 
+// LLMI_MV_FW (A/B): 1 = each wave issues its second sub-item's weights only after its
+// first sub-item's have landed, so the launch's first chip-wide round of requests is one
+// sub-item per wave instead of two (every result is unchanged)
+static int mv_fw() {
+    static const int v = [] {
+        const char* e = getenv("LLMI_MV_FW");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 hipError_t launch_matvec(const MVArgs& a0, int epi, int max_blocks, hipStream_t s) {
     if (a0.nseg < 1 || a0.cols <= 0 || a0.cols % 256) return hipErrorInvalidValue;
     MVArgs a = a0;
+    a.fw = mv_fw();
     if (!mv_geometry(a, epi)) return hipErrorInvalidValue;
     const int act = act_kind(a.seg[0].type);
     for (int i = 1; i < a.nseg; ++i)

@@ -96,6 +96,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
     if (pipe) {
         int s = 0;
         float acc = 0.f, vg = 0.f;
+        bool first_sub = A.fw != 0;
         // One sub-item: prefetch the next one into `nxt`, reduce `cur`.  The loop runs it
         // twice per trip with the two register buffers' roles swapped (ping-pong), so no
         // `cur = nxt` copy of the 36-52 registers of a unit is made per sub-item (Q6_K:
@@ -116,6 +117,10 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
                 sgn = pick(A, bn.si);
             }
             const LaneUnit lun = lane_unit(g, bn, sgn, r, ul);
+            if (first_sub) {  // LLMI_MV_FW: the first sub-item lands before the second is requested
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                first_sub = false;
+            }
             // always issue the prefetch (straight-line vmcnt counting); past the wave's last
             // sub-item every lane reads unit 0 of row 0 -- one line per part per wave instead
             // of a nontemporal re-read of the wave's 9-14 KB (FETCH_SIZE: +14 MB per gate+up)

@@ -689,10 +689,10 @@ def parse_args(argv=None):
     ap.add_argument("-np", "--parallel", type=int, default=int(os.environ.get("LLMI_SLOTS", "4")),
                     help="sequences (slots) per replica decoded together (continuous batching)")
     ap.add_argument("--decode-chunk", type=int, default=8, help="tokens per batched decode call")
-    ap.add_argument("--numerics", choices=("generic", "x86"), default=None,
+    ap.add_argument("--numerics", choices=NUMERICS_CHOICES, default=None,
                     help="fp32 association of every kernel: ggml's generic order, or the oracle's model of "
-                         "upstream's x86 AVX2 association (non-repack, non-flash; match with the reference's "
-                         "CPU image unpinned)")
+                         "upstream's x86 AVX2 association (non-repack); '-fa': decode attention in ggml's CPU "
+                         "flash-attention numerics (match with the reference's CPU image unpinned)")
     # llama-server's sampling flags and defaults (per-request fields override them)
     d = SamplingParams()
     ap.add_argument("--temp", type=float, default=d.temperature)
@@ -708,10 +708,18 @@ def parse_args(argv=None):
     if args.numerics is None:
         # argparse does not check a default against `choices`: validate the env value here
         env = os.environ.get("LLMI_NUMERICS", "generic").strip().lower()
-        if env not in ("generic", "x86"):
-            ap.error(f"LLMI_NUMERICS={os.environ.get('LLMI_NUMERICS')!r}: expected 'generic' or 'x86'")
+        if env not in NUMERICS_CHOICES:
+            ap.error(f"LLMI_NUMERICS={os.environ.get('LLMI_NUMERICS')!r}: expected one of {', '.join(NUMERICS_CHOICES)}")
         args.numerics = env
     return args, extra
+
+
+# --numerics values -> llama_model_params.numerics (llmi.h LLMI_NUMERICS_*)
+NUMERICS_CHOICES = ("generic", "x86", "generic-fa", "x86-fa")
+
+
+def numerics_value(name: str) -> int:
+    return (1 if name.startswith("x86") else 0) | (2 if name.endswith("-fa") else 0)
 
 
 def main(argv=None) -> int:
@@ -731,7 +739,7 @@ def main(argv=None) -> int:
                         repeat_penalty=args.repeat_penalty, repeat_last_n=args.repeat_last_n,
                         presence_penalty=args.presence_penalty, frequency_penalty=args.frequency_penalty, seed=args.seed)
     eng = Engine(args.model, args.ctx_size, args.ngl, list(range(max(1, args.replicas))), slots=args.parallel,
-                 chunk=args.decode_chunk, sampling=sp, numerics=1 if args.numerics == "x86" else 0)
+                 chunk=args.decode_chunk, sampling=sp, numerics=numerics_value(args.numerics))
     srv = make_server(eng, args.host, args.port, key)
     threading.Thread(target=eng.load, daemon=True).start()
     print(f"[llmi-server] listening on {args.host}:{args.port}", file=sys.stderr, flush=True)

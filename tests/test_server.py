@@ -246,6 +246,10 @@ def test_numerics_env_validated(monkeypatch):
     assert parse_args(["-m", "/m.gguf", "--numerics", "generic"])[0].numerics == "generic"
     monkeypatch.delenv("LLMI_NUMERICS")
     assert parse_args(["-m", "/m.gguf"])[0].numerics == "generic"
+    from llmi.server import numerics_value
+
+    assert [numerics_value(n) for n in ("generic", "x86", "generic-fa", "x86-fa")] == [0, 1, 2, 3]
+    assert parse_args(["-m", "/m.gguf", "--numerics", "x86-fa"])[0].numerics == "x86-fa"
 
 
 def test_gateway_forwarded_bytes(server):
