@@ -59,7 +59,7 @@ def parse(argv=None):
     ap.add_argument("--eager", action="store_true",
                     help="launch the step kernels one by one instead of replaying HIP graphs (PMC passes)")
     ap.add_argument("--no-c2-full", action="store_true", help="skip the full-trajectory (128 -> 640) timing")
-    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r05"),
+    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r06"),
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
     ap.add_argument("--experiment", action="store_true", help="allow LLMI_EXP_* knobs (line marked as an experiment)")
     ap.add_argument("--numerics", choices=("generic", "x86"), default="generic",

@@ -39,7 +39,7 @@ __device__ __forceinline__ Lds carve_t(uint8_t* smem, int act, int cols, int t, 
 // in any association in practice, as for the K-split kernel's 1024-thread prologue).
 // Work item i = tid + kBT k is (token i / nsub, sub-block i % nsub): the 16 lanes of a
 // DPP row hold the 16 sub-blocks of one 256-element block of one token, as quant_sub needs.
-template <int ACT, bool NORM, int NT>
+template <int ACT, bool NORM, int NT, int X86 = 0>
 __device__ __forceinline__ void bprologue(const MVArgs& A, uint8_t* smem, size_t img, double* red) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cols = A.cols, nsub = cols >> 4, nitem = NT * nsub;
@@ -105,7 +105,7 @@ __device__ __forceinline__ void bprologue(const MVArgs& A, uint8_t* smem, size_t
                 v[4 * k + 3] = (v[4 * k + 3] * sc) * w.w;
             }
         }
-        quant_sub<ACT>(carve_t(smem, ACT, cols, t, img), cols, sb, v);
+        quant_sub<ACT, X86>(carve_t(smem, ACT, cols, t, img), cols, sb, v);
     }
     __syncthreads();
 }
@@ -121,14 +121,19 @@ __device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t, int seq) {
 
 }  // namespace
 
-template <int ACT, bool NORM, int EPI, int T, int NT>
+// X86 = 1: the x86 association (model numerics LLMI_NUMERICS_X86; mv_device.h "x86
+// numerics"): x86 q8 images, the lane's per-4-byte-lane integer sums stored as fp32 fma
+// chain terms (unit_store_x86), x86 fold and epilogues -- every token equal to its own
+// single-sequence x86 decode.  K-quants only (the Q8_0 x86 fold buffers of 8 waves do not
+// fit the LDS).
+template <int ACT, bool NORM, int EPI, int T, int NT, int X86 = 0>
 __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const size_t img = img_bytes(ACT, A.cols);
     double* red = (double*)(smem + NT * img);
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
-    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * kFoldFloats;
+    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * fold_floats<ACT, X86>();
     const TaskGeo g = task_geo(A);
     const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
     const int r = lane / g.lr, ul = lane - r * g.lr;
@@ -136,7 +141,7 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     unsigned long long best[NT];  // per token: the lane's LOGITS key
 #pragma unroll
     for (int t = 0; t < NT; ++t) best[t] = 0;
-    bprologue<ACT, NORM, NT>(A, smem, img, red);
+    bprologue<ACT, NORM, NT, X86>(A, smem, img, red);
 
     // the tokens' positions and sequences, read once: a global load inside the loop would
     // wait (in-order vmcnt) behind the weight prefetch every sub-item
@@ -175,9 +180,10 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 float tm[9];
-                unit_terms<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, tm);
+                if constexpr (X86) unit_store_x86<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
+                else unit_terms<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, tm);
                 const MVArgs B = token_view(A, t, tseq[t]);
-                sub_finish<ACT, EPI>(B, F, g, s, b, sg, tm, lu, r, ul, acc[t], vg[t], tpos[t], best[t]);
+                sub_finish<ACT, EPI, MVArgs, X86>(B, F, g, s, b, sg, tm, lu, r, ul, acc[t], vg[t], tpos[t], best[t]);
             }
             if (!has_next) break;
             cur = nxt;
@@ -731,8 +737,9 @@ __global__ __launch_bounds__(kBmT) void k_bmd2(MVArgs A1, MVArgs A2, const uint8
 }
 
 // ---- launchers -----------------------------------------------------------------------------
-size_t mvn_lds_bytes(int act, int cols, int nt) {
-    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * kFoldFloats * 4;
+size_t mvn_lds_bytes(int act, int cols, int nt, int x86) {
+    const size_t fold = x86 ? (act ? (size_t)kX86QFloats : (size_t)kX86KFloats) : (size_t)kFoldFloats;
+    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * fold * 4;
 }
 
 template <typename K>
@@ -762,45 +769,54 @@ static int mvn_grid(K kernel, int ntasks, size_t lds, int max_blocks) {
     return std::max(blocks, 1);
 }
 
-template <int ACT, bool NORM, int EPI, int T, int NT>
+template <int ACT, bool NORM, int EPI, int T, int NT, int X86>
 static hipError_t mvn_launch(const MVArgs& a, int max_blocks, hipStream_t s) {
-    auto k = k_mvn<ACT, NORM, EPI, T, NT>;
-    const size_t lds = mvn_lds_bytes(ACT, a.cols, NT);
+    auto k = k_mvn<ACT, NORM, EPI, T, NT, X86>;
+    const size_t lds = mvn_lds_bytes(ACT, a.cols, NT, X86);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int blocks = mvn_grid(k, a.ntasks, lds, max_blocks);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(kBT), lds, s, a);
     return hipGetLastError();
 }
 
-template <int ACT, bool NORM, int EPI, int T>
+template <int ACT, bool NORM, int EPI, int T, int X86>
 static hipError_t mvn_nt(const MVArgs& a, int nt, int mb, hipStream_t s) {
     switch (nt) {
-        case 1: return mvn_launch<ACT, NORM, EPI, T, 1>(a, mb, s);
-        case 2: return mvn_launch<ACT, NORM, EPI, T, 2>(a, mb, s);
-        case 3: case 4: return mvn_launch<ACT, NORM, EPI, T, 4>(a, mb, s);
-        default: return mvn_launch<ACT, NORM, EPI, T, 8>(a, mb, s);
+        case 1: return mvn_launch<ACT, NORM, EPI, T, 1, X86>(a, mb, s);
+        case 2: return mvn_launch<ACT, NORM, EPI, T, 2, X86>(a, mb, s);
+        case 3: case 4: return mvn_launch<ACT, NORM, EPI, T, 4, X86>(a, mb, s);
+        default: return mvn_launch<ACT, NORM, EPI, T, 8, X86>(a, mb, s);
     }
 }
 
-template <int ACT, int T>
+template <int ACT, int T, int X86>
 static hipError_t mvn_epi(const MVArgs& a, int epi, int nt, int mb, hipStream_t s) {
     const bool norm = a.nw != nullptr;
     switch (epi) {
-        case EPI_ADD: return norm ? hipErrorInvalidValue : mvn_nt<ACT, false, EPI_ADD, T>(a, nt, mb, s);
-        case EPI_STORE: return norm ? mvn_nt<ACT, true, EPI_STORE, T>(a, nt, mb, s) : mvn_nt<ACT, false, EPI_STORE, T>(a, nt, mb, s);
-        case EPI_QKV: return mvn_nt<ACT, true, EPI_QKV, T>(a, nt, mb, s);
-        case EPI_SWIGLU: return mvn_nt<ACT, true, EPI_SWIGLU, T>(a, nt, mb, s);
-        case EPI_LOGITS: return mvn_nt<ACT, true, EPI_LOGITS, T>(a, nt, mb, s);
+        case EPI_ADD: return norm ? hipErrorInvalidValue : mvn_nt<ACT, false, EPI_ADD, T, X86>(a, nt, mb, s);
+        case EPI_STORE:
+            return norm ? mvn_nt<ACT, true, EPI_STORE, T, X86>(a, nt, mb, s) : mvn_nt<ACT, false, EPI_STORE, T, X86>(a, nt, mb, s);
+        case EPI_QKV: return mvn_nt<ACT, true, EPI_QKV, T, X86>(a, nt, mb, s);
+        case EPI_SWIGLU: return mvn_nt<ACT, true, EPI_SWIGLU, T, X86>(a, nt, mb, s);
+        case EPI_LOGITS: return mvn_nt<ACT, true, EPI_LOGITS, T, X86>(a, nt, mb, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 static hipError_t mvn_type(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
+    if (a.num) {  // x86 association: K-quants (mvn_ok_x86)
+        switch (a.seg[0].type) {
+            case T_Q4_K: return mvn_epi<0, T_Q4_K, 1>(a, epi, nt, max_blocks, s);
+            case T_Q5_K: return mvn_epi<0, T_Q5_K, 1>(a, epi, nt, max_blocks, s);
+            case T_Q6_K: return mvn_epi<0, T_Q6_K, 1>(a, epi, nt, max_blocks, s);
+            default: return hipErrorNotSupported;
+        }
+    }
     switch (a.seg[0].type) {
-        case T_Q4_K: return mvn_epi<0, T_Q4_K>(a, epi, nt, max_blocks, s);
-        case T_Q5_K: return mvn_epi<0, T_Q5_K>(a, epi, nt, max_blocks, s);
-        case T_Q6_K: return mvn_epi<0, T_Q6_K>(a, epi, nt, max_blocks, s);
-        case T_Q8_0: return mvn_epi<1, T_Q8_0>(a, epi, nt, max_blocks, s);
+        case T_Q4_K: return mvn_epi<0, T_Q4_K, 0>(a, epi, nt, max_blocks, s);
+        case T_Q5_K: return mvn_epi<0, T_Q5_K, 0>(a, epi, nt, max_blocks, s);
+        case T_Q6_K: return mvn_epi<0, T_Q6_K, 0>(a, epi, nt, max_blocks, s);
+        case T_Q8_0: return mvn_epi<1, T_Q8_0, 0>(a, epi, nt, max_blocks, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -818,10 +834,13 @@ hipError_t launch_mvn(const MVArgs& a0, int epi, int nt, int max_blocks, hipStre
     // the caller keeps kMaxBatch rows allocated and finite.  Rows too long for NT LDS
     // images (70B ffn_down: 28672 columns, 32 KB per token) run as several launches of
     // fewer tokens each (each streams the weights again; results per token unchanged).
-    const int act = t == T_Q8_0 ? 1 : 0;
+    const int act = t == T_Q8_0 ? 1 : 0, x86 = a.num ? 1 : 0;
+    if (x86 && act) return hipErrorNotSupported;
+    for (int i = 0; i < a.nseg; ++i)
+        if ((a.seg[i].x86 != 0) != (x86 != 0)) return hipErrorInvalidValue;  // the planes' byte order
     int group = mvn_pad(nt);
-    while (group > 1 && mvn_lds_bytes(act, a.cols, group) > 160 * 1024) group >>= 1;
-    if (mvn_lds_bytes(act, a.cols, group) > 160 * 1024) return hipErrorInvalidValue;
+    while (group > 1 && mvn_lds_bytes(act, a.cols, group, x86) > 160 * 1024) group >>= 1;
+    if (mvn_lds_bytes(act, a.cols, group, x86) > 160 * 1024) return hipErrorInvalidValue;
     for (int t0 = 0; t0 < nt; t0 += group) {
         MVArgs b = a;
         const int n = nt - t0 < group ? nt - t0 : group;

@@ -820,12 +820,14 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     BC(launch_bembed(ea, c.stream));
     MVArgs base;
     base.tpos = c.btpos; base.tseq = c.btseq; base.kv_stride = c.kv_seq_elems; base.st = c.st0;
+    base.num = m.numerics;
+    const bool x86 = m.numerics == NUMERICS_X86;
     // one matvec of the step: k_bmm (matrix cores) after quantizing the nt inputs, where
-    // its segments qualify, else k_mvn; `quantized` skips the quantization for a launch
-    // that reads the same input as the previous one (QKV type groups)
+    // its segments qualify, else k_mvn (x86 numerics: always k_mvn's x86 form); `quantized`
+    // skips the quantization for a launch that reads the same input as the previous one
     bool qkv_quant = false;
     auto bmv = [&](const MVArgs& a, int epi, bool& quantized) -> hipError_t {
-        if (nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
+        if (x86 || nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
         if (!quantized) {
             const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream);
             if (e != hipSuccess) return e;
@@ -854,7 +856,7 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
             i = j;
         }
         bool done = false;
-        if (ng == 2 && nt >= bmm_min_tokens() && bmm_ok(grp[0], EPI_QKV) && bmm_ok(grp[1], EPI_QKV)) {
+        if (!x86 && ng == 2 && nt >= bmm_min_tokens() && bmm_ok(grp[0], EPI_QKV) && bmm_ok(grp[1], EPI_QKV)) {
             BC(launch_pf_quant(c.bx, E, grp[0].nw, hp.eps, E, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream));
             qkv_quant = true;
             const hipError_t e2 = launch_bmm_qkv2(grp[0], grp[1], nt, c.baq, c.babf, c.bad, c.stream);
@@ -874,8 +876,14 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
             at.scores = c.bscores + (size_t)s * scr; at.tmax = at.scores + (size_t)hp.n_head * c.n_ctx;
             at.out = c.batt + (size_t)s * QD; at.st = c.st0 + seqs[s]; at.n_ctx = c.n_ctx;
             at.scale = 1.0f / sqrtf((float)D); at.layer = l;
+            at.num = m.numerics;
+            at.fa = m.fa;
         }
-        BC(launch_battention(ba, nt, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
+        if (x86 || m.fa) {  // the x86 / flash-attention kernels, one launch set per slot
+            for (int s = 0; s < nt; ++s) BC(launch_attention(ba.a[s], hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
+        } else {
+            BC(launch_battention(ba, nt, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
+        }
         MVArgs o = base;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = QD; o.x = c.batt; o.x_stride = QD; o.y = c.bx; o.y_stride = E;
         o.npairs = (E + 1) / 2;
@@ -898,10 +906,23 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     return true;
 }
 
+// the batched step in this model's numerics: generic (matrix cores from 3 tokens) and
+// flash-attention models; x86 models through k_mvn's x86 form, K-quant weights only (the
+// Q8_0 x86 fold buffers of a workgroup's 8 waves do not fit the LDS)
+bool bstep_supported(const Model& m) {
+    if (m.numerics == NUMERICS_GENERIC) return true;
+    for (const Layer& L : m.layers) {
+        const DevMat* ms[] = {&L.wq, &L.wk, &L.wv, &L.wo, &L.wg, &L.wu, &L.wd};
+        for (const DevMat* d : ms)
+            if (d->type == T_Q8_0) return false;
+    }
+    return m.output.type != T_Q8_0;
+}
+
 bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err) {
     const HParams& hp = c.m->hp;
     if (nt < 1 || nt > kMaxBatch || c.n_seq < 2) { err = "batched step: 1..8 slots of a context with n_seq_max >= 2"; return false; }
-    if (c.m->numerics != NUMERICS_GENERIC || c.m->fa) { err = "batched step: generic numerics only (x86 / flash-attention numerics decode one sequence per step)"; return false; }
+    if (!bstep_supported(*c.m)) { err = "batched step: x86 numerics with Q8_0 weights decode one sequence per step"; return false; }
     for (const Layer& L : c.m->layers)
         if (L.wg.type != L.wu.type) { err = "batched step: ffn_gate / ffn_up of different types"; return false; }
     if (!balloc(c, err)) return false;

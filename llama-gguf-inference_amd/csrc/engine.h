@@ -176,6 +176,7 @@ bool step_run(Context& c, int pos, std::string& err);
 double bytes_per_token(const Model& m, int n_kv);
 // batched prefill: can the model's layers run through the MFMA prefill path?
 bool prefill_supported(const Model& m);
+bool bstep_supported(const Model& m);  // batched steps in this model's numerics (engine.cpp)
 // positions the batched prefill's attention reaches: the context when the tiled kernel
 // (k_pf_fa) takes the model's heads, else the LDS kernels' pf_max_kv()
 int prefill_max_kv(Context& c);

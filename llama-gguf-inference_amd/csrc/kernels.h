@@ -171,7 +171,7 @@ hipError_t launch_bmm_qkv2(const MVArgs& a1, const MVArgs& a2, int nt, const voi
                            hipStream_t s);
 hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
                              hipStream_t s);
-size_t mvn_lds_bytes(int act, int cols, int nt);
+size_t mvn_lds_bytes(int act, int cols, int nt, int x86 = 0);
 
 struct EmbArgs {
     Seg w;                          // token_embd in device layout

@@ -387,3 +387,49 @@ def test_x86_mistral_2048_prefill_vs_oracle(gpu, synth_dir, preset):
     om.close()
     _assert_same(got, want)
 
+
+
+# ---- batched steps in x86 numerics (k_mvn's x86 form) -----------------------
+@pytest.mark.parametrize("numerics", [llmi.NUMERICS_X86, llmi.NUMERICS_X86 | llmi.NUMERICS_FA,
+                                      llmi.NUMERICS_FA])
+def test_x86_and_fa_batched_steps_vs_oracle(gpu, synth_dir, numerics):
+    """A K-quant model in x86 (and/or flash-attention) numerics advances 5 sequences per
+    llama_decode call through the batched step (k_mvn x86 form / matrix cores, attention per
+    slot), each sequence's logits bit-identical to the oracle's decode in the same mode;
+    llmi_generate_greedy_batch (which fails rather than falling back) over 8 sequences
+    equals each sequence's single decode."""
+    path = str(synth_dir / "llama3-8b-q4km-L2-v32000.gguf")
+    if not os.path.exists(path):
+        llmi.write_synthetic_gguf(path, "llama3-8b-q4km", seed=3, n_layer=2, n_vocab=32000)
+    flags = (X86 if numerics & llmi.NUMERICS_X86 else 0) | (po.X86_FA if numerics & llmi.NUMERICS_FA else 0)
+    rng = np.random.default_rng(41)
+    prompts = [[1] + [int(t) for t in rng.integers(3, 30000, int(n))] for n in rng.integers(2, 40, 5)]
+    oms = [po.OracleModel(path, n_ctx=256, x86=flags) for _ in prompts]
+    m = llmi.Model(path, numerics=numerics)
+    c = llmi.Context(m, n_ctx=256, n_seq=5)
+    cur, pos = [], []
+    for s, p in enumerate(prompts):
+        for k, t in enumerate(p[:-1]):
+            oms[s].decode(t, k, logits=False)
+        assert c.decode(p[:-1], seq=[s] * (len(p) - 1)) == 0
+        cur.append(p[-1])
+        pos.append(len(p) - 1)
+    for step in range(5):
+        assert c.decode(cur, pos=pos, seq=[0, 1, 2, 3, 4], logits_all=True) == 0
+        for s in range(5):
+            want = oms[s].decode(cur[s], pos[s])
+            got = c.logits(s)
+            assert np.array_equal(got, want), f"step {step} seq {s}: max |d| {np.abs(got - want).max():.3g}"
+            cur[s] = int(np.argmax(want))
+            pos[s] += 1
+    for om in oms:
+        om.close()
+    c.close()
+    c8 = llmi.Context(m, n_ctx=128, n_seq=8)
+    firsts = [int(t) for t in rng.integers(3, 30000, 8)]
+    got = c8.generate_greedy_batch(list(range(8)), firsts, [0] * 8, 10)
+    c1 = llmi.Context(m, n_ctx=128)
+    for k in range(8):
+        c1.kv_clear()
+        assert c1.generate_greedy(firsts[k], 0, 10) == got[k], f"sequence {k}"
+    c8.close(), c1.close(), m.close()
