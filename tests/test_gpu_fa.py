@@ -3,7 +3,7 @@ r5 item 4): decode attention as upstream's CPU flash_attn_ext one
 (online max / sum, f16 V accumulator rescaled on a new maximum, glibc expf), in both dot
 associations, bit-identical to the oracle's OR_X86_FA mode (oracle/ggml_oracle.c
 attn_head_fa).  The matvecs keep their association (generic or x86); prompts run as
-decode steps (no batched prefill in this mode).
+decode steps (no batched prefill in this mode); batched steps run the FA attention per slot.
 
 - every quant type and both head dims (tiny presets): 40 steps bit-identical, and
   different from the non-flash attention of the same association;
@@ -100,15 +100,16 @@ def test_fa_order_trajectory(gpu, synth_dir, preset, n_prompt, n_gen, assoc):
             f.write(json.dumps(rep) + "\n")
 
 
-def test_fa_batch_api_sequential(gpu, tiny_models):
-    """A flash-attention context with n_seq_max >= 2 runs its sequences one after another
-    (no batched kernels in this mode): each equals its own single-sequence decode."""
-    path = tiny_models["tiny-mixed"]
+def test_fa_batched_equals_single(gpu, tiny_models):
+    """A flash-attention context with n_seq_max >= 2 advances its sequences through batched
+    steps (matvecs batched, the FA attention per slot): each equals its own single-sequence
+    decode (and that one equals the oracle: test_fa_tiny_decode_vs_oracle)."""
+    path = tiny_models["tiny-mixed-d128"]
     m = llmi.Model(path, numerics=llmi.NUMERICS_FA)
-    c = llmi.Context(m, n_ctx=128, n_seq=2)
-    got = c.generate_greedy_batch([0, 1], [5, 9], [0, 0], 12)
+    c = llmi.Context(m, n_ctx=128, n_seq=3)
+    got = c.generate_greedy_batch([0, 1, 2], [5, 9, 11], [0, 0, 0], 12)
     c1 = llmi.Context(m, n_ctx=128)
-    for k, first in enumerate((5, 9)):
+    for k, first in enumerate((5, 9, 11)):
         c1.kv_clear()
         assert c1.generate_greedy(first, 0, 12) == got[k]
     c.close(), c1.close(), m.close()
