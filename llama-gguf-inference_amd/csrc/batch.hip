@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 float tm[9];
-                if constexpr (X86) unit_store_x86<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
+                if constexpr (X86) unit_store_x86<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, F, r, ul, g.lr, g.R, lu.valid);
                 else unit_terms<T>(cur, smem + (size_t)t * img + (size_t)lu.u * kRec, tm);
                 const MVArgs B = token_view(A, t, tseq[t]);
                 sub_finish<ACT, EPI, MVArgs, X86>(B, F, g, s, b, sg, tm, lu, r, ul, acc[t], vg[t], tpos[t], best[t]);

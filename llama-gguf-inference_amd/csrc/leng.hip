@@ -459,7 +459,7 @@ __device__ __forceinline__ void le_sub(const MVArgs& M, LeCtl* ctl, const uint8_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pieces are in registers ...
     lds_st(&ctl->cons[cw], bend);                      // ... and free for the loader
     float tm[9];
-    if constexpr (X86) unit_store_x86<T>(w, img + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
+    if constexpr (X86) unit_store_x86<T>(w, img + (size_t)lu.u * kRec, F, r, ul, g.lr, g.R, lu.valid);
     else unit_terms<T>(w, img + (size_t)lu.u * kRec, tm);
     unsigned long long best = 0;
     sub_finish<ACT, EPI, MVArgs, X86, WT, EPI == EPI_ADD || EPI == EPI_QKV>(M, F, g, s, sb, sg, tm, lu, r, ul, acc, vg,

@@ -707,11 +707,22 @@ __device__ __forceinline__ void unit_terms_q6m(const UnitW<T_Q6_K>& w, const uin
 // dword, so the integer code is the generic one with l read as the lane; the fold runs
 // the fma chains (d and the lane sums kept apart until the chain's fma).
 // Fold buffer per wave (floats): K-quants S[R][12][Lr] | D[R][2][Lr] (d, -dmin) | G[R][12];
-// Q8_0 S[R][8][8 Lr] | D[R][8 Lr] | G[R][8].
+// Q8_0 S[R][8][CS] | D[R][8 Lr] | G[R][8] with the chain stride CS = x86q_cs(Lr) = 8 Lr + 4
+// (Lr >= 8): fold lane f reads chain f at f CS, so the 16 lanes of a ds_read_b128 group
+// start on 16 different 16-B bank slots (an 8 Lr stride put them all on one: 16-way, and
+// the unit's 64 single-dword stores were 8-way); the largest geometry (Lr = 8, R = 8)
+// takes 4352 + 512 + 64 floats.
 // ----------------------------------------------------------------------------------
 constexpr int kFoldF = 9 * 64, kFoldFloats = kFoldF + 9 * 16;
 constexpr int kX86KD = 12 * 64, kX86KG = kX86KD + 2 * 64, kX86KFloats = kX86KG + 12 * 16;
-constexpr int kX86QD = 8 * 8 * 64, kX86QG = kX86QD + 8 * 64, kX86QFloats = kX86QG + 8 * 16;
+__host__ __device__ constexpr int x86q_cs(int lr) { return lr >= 8 ? 8 * lr + 4 : 8 * lr; }
+__host__ __device__ constexpr int x86q_d(int R, int lr) { return R * 8 * x86q_cs(lr); }
+__host__ __device__ constexpr int x86q_g(int R, int lr) { return x86q_d(R, lr) + R * 8 * lr; }
+constexpr int kX86QFloats = 4928;
+static_assert(x86q_g(8, 8) + 8 * 8 <= kX86QFloats && x86q_g(16, 4) + 8 * 16 <= kX86QFloats &&
+                  x86q_g(4, 16) + 8 * 4 <= kX86QFloats && x86q_g(2, 32) + 8 * 2 <= kX86QFloats &&
+                  x86q_g(1, 64) + 8 <= kX86QFloats,
+              "x86 Q8_0 fold buffer");
 template <int ACT, int X86>
 __host__ __device__ constexpr int fold_floats() { return X86 ? (ACT ? kX86QFloats : kX86KFloats) : kFoldFloats; }
 template <int ACT>
@@ -726,26 +737,33 @@ __device__ __forceinline__ float x86_hsum8(const float* a) {
 // the unit's x86 terms straight into the fold buffer (lane: row r, unit ul of the sub-item)
 template <int T>
 __device__ __forceinline__ void unit_store_x86(const UnitW<T>& w, const uint8_t* rec, float* F, int r, int ul, int lr,
-                                               bool valid) {
+                                               int R, bool valid) {
     if constexpr (T == T_Q8_0) {
-        // per 32-block b: lanes k < 4 are dwords of part 2b, k >= 4 of part 2b + 1
-        float* S = F + (size_t)r * 8 * 8 * lr + 8 * ul;
-        float* D = F + kX86QD + (size_t)r * 8 * lr + 8 * ul;
+        // per 32-block b: lanes k < 4 are dwords of part 2b, k >= 4 of part 2b + 1; the
+        // unit's 8 terms of chain k are 8 consecutive floats: blocks 0-3 and 4-7 go out
+        // as one 16-B store each (16 stores of 64 terms instead of 64 single dwords)
+        const int cs = x86q_cs(lr);
+        float* S = F + (size_t)r * 8 * cs + 8 * ul;
+        float* D = F + x86q_d(R, lr) + (size_t)r * 8 * lr + 8 * ul;
         float db[8];
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const i32x4 a0 = *(const i32x4*)(rec + 32 * b), a1 = *(const i32x4*)(rec + 32 * b + 16);
-            const float dw = h2f(w.s[b >> 1] >> (16 * (b & 1))), da = *(const float*)(rec + kRecBs + 4 * b);
-            db[b] = dw * da;
-            float s[8];
+        for (int h = 0; h < 2; ++h) {
+            float s[4][8];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                s[m] = (float)dot4(w.q[2 * b][m], a0[m], 0);
-                s[4 + m] = (float)dot4(w.q[2 * b + 1][m], a1[m], 0);
+            for (int bb = 0; bb < 4; ++bb) {
+                const int b = 4 * h + bb;
+                const i32x4 a0 = *(const i32x4*)(rec + 32 * b), a1 = *(const i32x4*)(rec + 32 * b + 16);
+                const float dw = h2f(w.s[b >> 1] >> (16 * (b & 1))), da = *(const float*)(rec + kRecBs + 4 * b);
+                db[b] = dw * da;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    s[bb][m] = (float)dot4(w.q[2 * b][m], a0[m], 0);
+                    s[bb][4 + m] = (float)dot4(w.q[2 * b + 1][m], a1[m], 0);
+                }
             }
             if (valid) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) S[(size_t)k * 8 * lr + b] = s[k];
+                for (int k = 0; k < 8; ++k) *(float4*)(S + (size_t)k * cs + 4 * h) = make_float4(s[0][k], s[1][k], s[2][k], s[3][k]);
             }
         }
         if (valid) {
@@ -850,7 +868,7 @@ __device__ __forceinline__ float chain_batched(int len, float a, OP&& term) {
     term.load(0, c);
     int b = 0;
     for (; b + TB <= len; b += TB) {
-        term.load(b + TB, nx);
+        if (b + TB < len) term.load(b + TB, nx);  // (uniform: len is the wave's)
 #pragma unroll
         for (int k = 0; k < TB; ++k) a = term.apply(a, c, k);
 #pragma unroll
@@ -907,10 +925,10 @@ __device__ __forceinline__ void fold_sub_x86(float* F, int R, int lr, int n, boo
         const int r = f / NC, c = f - r * NC;
         float a;
         if constexpr (ACT) {
-            const float* s = F + (size_t)(r * 8 + c) * 8 * lr;
-            const float* d = F + kX86QD + (size_t)r * 8 * lr;
+            const float* s = F + (size_t)(r * 8 + c) * x86q_cs(lr);
+            const float* d = F + x86q_d(R, lr) + (size_t)r * 8 * lr;
             a = chain_batched(8 * n, acc, ChainFma{d, s});
-            if (last) F[kX86QG + f] = a;
+            if (last) F[x86q_g(R, lr) + f] = a;
         } else {
             const float* s = F + (size_t)(r * 12 + c) * lr;
             const float* d = F + kX86KD + (size_t)(r * 2 + (c >= 8 ? 1 : 0)) * lr;
@@ -923,9 +941,9 @@ __device__ __forceinline__ void fold_sub_x86(float* F, int R, int lr, int n, boo
 }
 // final value of row r of the task (after a wave_lds_sync)
 template <int ACT>
-__device__ __forceinline__ float row_final_x86(const float* F, int r, int type) {
+__device__ __forceinline__ float row_final_x86(const float* F, int r, int type, int R, int lr) {
     if constexpr (ACT) {
-        return x86_hsum8(F + kX86QG + 8 * r);
+        return x86_hsum8(F + x86q_g(R, lr) + 8 * r);
     } else {
         const float* g = F + kX86KG + 12 * r;
         const float h = x86_hsum8(g);
@@ -977,7 +995,9 @@ __host__ __device__ inline TaskGeo task_geo(const MVArgs& A) {
 }
 
 // Fold buffer per wave: F[row][chain][Lr] terms + G[row][chain] chain results (kFoldF,
-// kFoldFloats: above, with the x86 buffers).
+// kFoldFloats: above, with the x86 buffers).  Q8_0: row r's 8 Lr terms at r * (8 Lr + 4),
+// so the fold lanes' 16-B reads start on different bank slots (R (8 Lr + 4) <= kFoldF).
+__host__ __device__ constexpr int q80_rs(int lr) { return 8 * lr + 4; }
 
 // Fold lane f (< R * chains) adds its chain's n terms of the sub-item (K-quants: chain f
 // = (row f / 9, chain f % 9), Lr terms apart; Q8_0: chain = row f, 8 terms per unit) in
@@ -988,7 +1008,7 @@ template <int ACT>
 __device__ __forceinline__ void fold_sub(float* F, int R, int lr, int n, bool last, float& acc) {
     constexpr int NC = row_chains<ACT>();
     const int lane = threadIdx.x & 63, nf = R * NC;
-    const int len = ACT ? 8 * n : n, stride = ACT ? 8 * lr : lr;
+    const int len = ACT ? 8 * n : n, stride = ACT ? q80_rs(lr) : lr;
     for (int f = lane; f < nf; f += 64) {
         float a = chain_batched(len, acc, ChainAdd{F + f * stride});
         if (last) {
@@ -1015,7 +1035,7 @@ __device__ __forceinline__ float row_final(const float* F, int r) {
 template <int T>
 __device__ __forceinline__ void store_terms(float* F, int r, int ul, int lr, const float (&tm)[9]) {
     if constexpr (T == T_Q8_0) {
-        float* q = F + (r * lr + ul) * 8;
+        float* q = F + r * q80_rs(lr) + 8 * ul;
         *(float4*)q = make_float4(tm[0], tm[1], tm[2], tm[3]);
         *(float4*)(q + 4) = make_float4(tm[4], tm[5], tm[6], tm[7]);
     } else {
@@ -1233,7 +1253,7 @@ __device__ __forceinline__ void sub_finish(const MA& A, float* F, const TaskGeo&
     const bool last = b.j == g.nj - 1;
     if constexpr (X86) fold_sub_x86<ACT>(F, g.R, g.lr, n, last, acc);
     else fold_sub<ACT>(F, g.R, g.lr, n, last, acc);
-    auto final_of = [&](int rr) { return X86 ? row_final_x86<ACT>(F, rr, sg.type) : row_final<ACT>(F, rr); };
+    auto final_of = [&](int rr) { return X86 ? row_final_x86<ACT>(F, rr, sg.type, g.R, g.lr) : row_final<ACT>(F, rr); };
     if (last) {
         wave_lds_sync();
         const int lane = threadIdx.x & 63;
@@ -1276,12 +1296,12 @@ __device__ __forceinline__ void task_any(const MA& A, const Lds& L, float* F, co
         float tm[9];
         if constexpr (X86) {
             if constexpr (ACT == 1) {
-                unit_store_x86<T_Q8_0>(load_unit<T_Q8_0>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid);
+                unit_store_x86<T_Q8_0>(load_unit<T_Q8_0>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, g.R, lu.valid);
             } else {
                 switch (sg.type) {
-                    case T_Q4_K: unit_store_x86<T_Q4_K>(load_unit<T_Q4_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid); break;
-                    case T_Q5_K: unit_store_x86<T_Q5_K>(load_unit<T_Q5_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid); break;
-                    default: unit_store_x86<T_Q6_K>(load_unit<T_Q6_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, lu.valid); break;
+                    case T_Q4_K: unit_store_x86<T_Q4_K>(load_unit<T_Q4_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, g.R, lu.valid); break;
+                    case T_Q5_K: unit_store_x86<T_Q5_K>(load_unit<T_Q5_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, g.R, lu.valid); break;
+                    default: unit_store_x86<T_Q6_K>(load_unit<T_Q6_K>(sg, lu.row, lu.u, g.U), rec, F, r, ul, g.lr, g.R, lu.valid); break;
                 }
             }
         } else if constexpr (ACT == 1) {

@@ -127,7 +127,7 @@ __device__ __forceinline__ unsigned long long mv_body(const MVArgs& A, const Lds
             nxt = load_unit<T>(sgn, has_next ? lun.row : 0u, has_next ? lun.u : 0u, g.U);
             float tm[9];
             if constexpr (X86)
-                unit_store_x86<T>(cur, L.act + (size_t)lu.u * kRec, F, r, ul, g.lr, lu.valid);
+                unit_store_x86<T>(cur, L.act + (size_t)lu.u * kRec, F, r, ul, g.lr, g.R, lu.valid);
             else if constexpr (T == T_Q6_K && kQ6Masked)
                 unit_terms_q6m(cur, q6m + (size_t)lu.u * kQ6MaskRec, *(const float*)(L.act + (size_t)lu.u * kRec + kRecD), tm);
             else
