@@ -1376,7 +1376,6 @@ int32_t llmi_pf_gemm(int32_t type, const void* w, int64_t rows, int64_t cols, co
                      int32_t n_tok, float* y, double* usec) {
     if (!pf_gemm_ok(type, (int)rows, (int)cols) || n_tok <= 0) { set_err("llmi_pf_gemm: unsupported type/shape"); return -1; }
     const int x86 = (t_hook_numerics & NUMERICS_X86) != 0;
-    if (x86 && type == T_Q8_0) { set_err("llmi_pf_gemm: x86 numerics take K-quants only"); return -1; }
     const int tpad = (n_tok + 63) / 64 * 64;
     void* aq = nullptr;
     int16_t* abs = nullptr;

@@ -975,12 +975,10 @@ bool prefill_supported(const Model& m) {
     if (m.fa) return false;  // flash-attention numerics: prompts as decode steps (attnfa.hip is decode-only)
     if (hp.head_dim != 128 && hp.head_dim != 64) return false;
     if (hp.n_rot % 2 || hp.n_rot > hp.head_dim) return false;
-    const bool x86 = m.numerics == NUMERICS_X86;
     for (const Layer& L : m.layers) {
         const DevMat* ms[] = {&L.wq, &L.wk, &L.wv, &L.wo, &L.wg, &L.wu, &L.wd};
         for (const DevMat* d : ms) {
             if (!pf_gemm_ok(d->type, (int)d->rows, (int)d->cols)) return false;
-            if (x86 && d->type == T_Q8_0) return false;  // x86 Q8_0 prompts: decode steps
         }
         if (act_kind(L.wg.type) != act_kind(L.wu.type)) return false;
     }

@@ -327,11 +327,13 @@ def test_x86_batch_api_sequential(gpu, tiny_models):
 
 
 # ---- prefill (batched MFMA GEMM + k_pf_a86) ---------------------------------------------------
-@pytest.mark.parametrize("qtype", [Q4_K, Q5_K, Q6_K], ids=["q4_K", "q5_K", "q6_K"])
-@pytest.mark.parametrize("rows,cols,n_tok", [(64, 256, 5), (128, 4096, 40), (1024, 4096, 130), (64, 14336, 64)])
+@pytest.mark.parametrize("qtype", [Q4_K, Q5_K, Q6_K, Q8_0], ids=["q4_K", "q5_K", "q6_K", "q8_0"])
+@pytest.mark.parametrize("rows,cols,n_tok", [(64, 256, 5), (128, 4096, 40), (1024, 4096, 130), (64, 14336, 64),
+                                             (256, 5632, 33)])
 def test_x86_pf_gemm_equals_matvecs(gpu, qtype, rows, cols, n_tok):
     """The x86 prefill GEMM (f16-MFMA integer sums, x86 fma lane chains, Q4_K's four min
-    lanes from masked sumi MFMAs) equals n_tok x86 matvecs and the oracle bit for bit."""
+    lanes from masked sumi MFMAs; Q8_0's eight lanes per block from masked-weight MFMAs)
+    equals n_tok x86 matvecs and the oracle bit for bit."""
     import torch
 
     rng = np.random.default_rng(rows + cols + n_tok + qtype)
@@ -387,6 +389,40 @@ def test_x86_mistral_2048_prefill_vs_oracle(gpu, synth_dir, preset):
     om.close()
     _assert_same(got, want)
 
+
+
+def test_x86_tinyllama_prefill_vs_oracle(gpu, synth_dir):
+    """C1's model in x86 numerics (Q8_0 everywhere; 2 layers, full V 32000): a 300-token
+    prompt through the batched prefill (the Q8_0 x86 GEMM + k_pf_a86),
+    then 3 decode steps; logits bit-identical to the oracle's x86 mode at every step."""
+    from test_gpu_long import _assert_same
+
+    path = str(synth_dir / "tinyllama-q8_0-L2-full.gguf")
+    if not os.path.exists(path):
+        llmi.write_synthetic_gguf(path, "tinyllama-q8_0", seed=3, n_layer=2)
+    rng = np.random.default_rng(12)
+    prompt = [1] + [int(t) for t in rng.integers(3, 32000, 299)]
+    m = llmi.Model(path, numerics=llmi.NUMERICS_X86)
+    assert m.prefill_supported
+    c = llmi.Context(m, n_ctx=512)
+    assert c.decode(prompt) == 0
+    got = [c.logits(-1)]
+    pos = len(prompt)
+    for _ in range(3):
+        t = c.greedy(-1)
+        assert c.decode([t], pos=[pos]) == 0
+        got.append(c.logits(-1))
+        pos += 1
+    om = po.OracleModel(path, n_ctx=512, x86=X86)
+    om.prefill(prompt[:-1])
+    want = [om.decode(prompt[-1], len(prompt) - 1)]
+    pos = len(prompt)
+    for _ in range(3):
+        want.append(om.decode(int(np.argmax(want[-1])), pos))
+        pos += 1
+    om.close()
+    c.close(), m.close()
+    _assert_same(got, want)
 
 
 # ---- batched steps in x86 numerics (k_mvn's x86 form; VERDICT r5 item 6) -----------------------
