@@ -588,8 +588,10 @@ def main(argv=None):
                                     "note": "k sequences per replica in batched steps (one weight stream per step), "
                                             f"{args.prompt}-token prompts, {args.batch_steps} timed steps; "
                                             "aggregate tokens/s of this rank; not the metric's value",
-                                    "matvec": ("k_mvn's x86 form (VALU; every sequence in its own x86 decode's fp32 order), "
-                                               "attention per slot" if eng.numerics == eng.llmi.NUMERICS_X86 else
+                                    "matvec": ("k_bmd's x86 fold (f16 MFMA integer sums, x86 fma lane chains) from "
+                                               f"{os.environ.get('LLMI_BMM_MIN', '3')} sequences on K-quant "
+                                               "segments, else k_mvn's x86 form (VALU); attention per slot"
+                                               if eng.numerics == eng.llmi.NUMERICS_X86 else
                                                "k_bmd (f16 MFMA, weights staged by LDS-DMA, batch.hip; k_bmm "
                                                "with LLMI_BMM_DMA=0) from "
                                                f"{os.environ.get('LLMI_BMM_MIN', '3')} sequences on K-quant "

@@ -62,7 +62,8 @@ struct llama_model_params {
 /* OR-ed into either: decode attention in ggml's CPU flash-attention numerics (online
  * softmax, f16 V accumulation, glibc expf; what a llama-server without --flash-attn runs
  * when -fa auto resolves to on), oracle flag OR_X86_FA.  Such a model runs prompts as
- * decode steps and batched sequences one after another; up to 8192 positions. */
+ * decode steps (batched steps advance its sequences together, the flash attention of
+ * every slot in one launch); up to 8192 positions. */
 #define LLMI_NUMERICS_FA 2
 
 /* upstream llama_context_params (subset) */

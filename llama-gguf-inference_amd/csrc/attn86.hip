@@ -179,7 +179,7 @@ __device__ __forceinline__ float a86_quad_reduce(float (&acc)[8]) {
 #define A86_STAMP(I)
 #endif
 template <int D, int DS, int U>
-__global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, int gq, int kvb, int stop) {
+__device__ __forceinline__ void a86_h_body(const AttnArgs& a, int n_head, int gq, int kvb, int stop) {
     constexpr int NT = kA86Threads, NW = NT / 64, VP = DS * kA86MaxKV / 8 / NT, NE = D / 32;
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     const int vst = kvb + 8;                                  // V row stride (f16): rows off one bank quad
@@ -199,6 +199,20 @@ __global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, i
         const int i = tid + k * NT;
         if (i < DS * prow) vr[k] = *(const u32x4*)(vb + (size_t)(i / prow) * a.n_ctx + (i % prow) * 8);
     }
+    // the first pass's K rows, issued before q is waited on (their latencies overlap) where
+    // the registers allow (head_dim 128 at 1024 positions per pass would spill)
+    constexpr bool kHoist = U * NE <= 16;
+    const uint16_t* K = a.kc + (size_t)g * a.n_ctx * D + 8 * qg;
+    // a pass: U positions per quad, wave w takes positions pass * 128 U + 128 u + 16 w + lane / 4
+    const int pw = wave * 16 + (lane >> 2);
+    u32x4 kr[U][NE];
+    if constexpr (kHoist)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = min(NW * 16 * u + pw, n_kv - 1);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) kr[u][e] = *(const u32x4*)(K + (size_t)t * D + 32 * e);
+    }
     // this lane's q values: q[8 qg + 32 e + j], f16-rounded
     float qv[NE][8];
 #pragma unroll
@@ -209,19 +223,17 @@ __global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, i
 #pragma unroll
         for (int j = 0; j < 8; ++j) qv[e][j] = h2f(f2h(qf[j]));
     }
-    const uint16_t* K = a.kc + (size_t)g * a.n_ctx * D + 8 * qg;
-    // a pass: U positions per quad, wave w takes positions pass * 128 U + 128 u + 16 w + lane / 4
-    const int pw = wave * 16 + (lane >> 2);
     A86_STAMP(1)
     if (stop == 1) return;
     float m = -INFINITY;
     for (int t0 = 0; t0 < n_kv; t0 += NW * 16 * U) {
-        u32x4 kr[U][NE];
+        if (!kHoist || t0 > 0) {  // (uniform) the later passes
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int t = min(t0 + NW * 16 * u + pw, n_kv - 1);
+            for (int u = 0; u < U; ++u) {
+                const int t = min(t0 + NW * 16 * u + pw, n_kv - 1);
 #pragma unroll
-            for (int e = 0; e < NE; ++e) kr[u][e] = *(const u32x4*)(K + (size_t)t * D + 32 * e);
+                for (int e = 0; e < NE; ++e) kr[u][e] = *(const u32x4*)(K + (size_t)t * D + 32 * e);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -254,23 +266,31 @@ __global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, i
     float mx = redm[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redm[w]);
+    // one exp per thread (position t, kept in wl[t] for p), the 8-position chunk sums of
+    // the AVX2 code, ((e0 + e4) + (e2 + e6)) + ((e1 + e5) + (e3 + e7)), across each 8-lane
+    // group by DPP: lane 4 + i takes e_i by row_shr:4 (t_i = e_i + e_{i+4} in lanes 4..7; the
+    // xor-4 helper's half-mirror would pair e_i with e_{7-i}), then quad xor 2 and xor 1;
+    // the chunk sums (lane 4 of each group) into the double total
     double sum = 0.0;
-    for (int c8 = tid; 8 * c8 < n_kv; c8 += NT) {
-        float e[8];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) e[l] = 8 * c8 + l < n_kv ? x86_v_expf(wl[8 * c8 + l] - mx) : 0.f;
-        sum += (double)x86_hsum8(e);
+    const int n8 = (n_kv + 7) & ~7;
+    for (int t = tid; t < n8; t += NT) {
+        const float e = t < n_kv ? x86_v_expf(wl[t] - mx) : 0.f;
+        wl[t] = e;
+        const float t4 = e + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(e), 0x114, 0xF, 0xF, false));
+        const float t2 = t4 + xor_partner<2>(t4);
+        const float c = t2 + xor_partner<1>(t2);
+        if ((lane & 7) == 4) sum += (double)c;
     }
     sum = wave_sum_d(sum);
     if (lane == 0) reds[wave] = sum;
-    __syncthreads();  // also: every score read before any p replaces it
+    __syncthreads();
     A86_STAMP(3)
     if (stop == 3) return;
     double tot = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) tot += reds[w];
     const float inv = (float)(1.0 / tot);
-    for (int t = tid; t < np; t += NT) wl[t] = t < n_kv ? h2f(f2h(x86_v_expf(wl[t] - mx) * inv)) : 0.f;
+    for (int t = tid; t < np; t += NT) wl[t] = t < n_kv ? h2f(f2h(wl[t] * inv)) : 0.f;  // wl[t] = e (own thread)
     __syncthreads();
     A86_STAMP(4)
     if (stop == 4) return;
@@ -287,6 +307,16 @@ __global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, i
         if (c == 0) a.out[(size_t)h * D + d0 + dl] = r;
     }
     A86_STAMP(5)
+}
+template <int D, int DS, int U>
+__global__ __launch_bounds__(kA86Threads) void k_a86_h(AttnArgs a, int n_head, int gq, int kvb, int stop) {
+    a86_h_body<D, DS, U>(a, n_head, gq, kvb, stop);
+}
+// batched decode (batch.hip launch_battention): batch slot = blockIdx.y, its own sequence's
+// caches, q, output and position (kvb: the batch's common KV bound)
+template <int D, int DS, int U>
+__global__ __launch_bounds__(kA86Threads) void k_ba86_h(BAttnArgs b, int n_head, int gq, int kvb) {
+    a86_h_body<D, DS, U>(b.a[blockIdx.y], n_head, gq, kvb, 0);
 }
 
 template <int D, int G>
@@ -310,6 +340,34 @@ static hipError_t a86_launch(const AttnArgs& a, int n_head, int hk, int kv_bound
     launch_k(k_a86_softmax, dim3(n_head), dim3(256), 0, s, false, false, a);
     launch_k(k_a86_pv<D, G>, dim3(hk, D / 16), dim3(512), 0, s, false, true, a);
     return hipGetLastError();
+}
+
+template <int D>
+static hipError_t ba86_launch(const BAttnArgs& b, int nt, int n_head, int G, int kv_bound, hipStream_t s) {
+    constexpr int DS = 16;
+    const size_t lds = (size_t)kv_bound * 4 + (size_t)DS * (kv_bound + 8) * 2;
+    const dim3 grid(n_head * (D / DS), nt);
+    if (kv_bound <= 128) launch_k(k_ba86_h<D, DS, 1>, grid, dim3(kA86Threads), lds, s, true, true, b, n_head, G, kv_bound);
+    else if (kv_bound <= 256) launch_k(k_ba86_h<D, DS, 2>, grid, dim3(kA86Threads), lds, s, true, true, b, n_head, G, kv_bound);
+    else if (kv_bound <= 512) launch_k(k_ba86_h<D, DS, 4>, grid, dim3(kA86Threads), lds, s, true, true, b, n_head, G, kv_bound);
+    else launch_k(k_ba86_h<D, DS, 8>, grid, dim3(kA86Threads), lds, s, true, true, b, n_head, G, kv_bound);
+    return hipGetLastError();
+}
+// the batched step's x86 attention: one launch for every slot up to kA86MaxKV positions, past
+// it the three-launch form per slot
+hipError_t launch_battention_x86(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
+                                 hipStream_t s) {
+    if (nt < 1 || nt > kMaxBatch || n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    if (head_dim != 128 && head_dim != 64) return hipErrorInvalidValue;
+    if (kv_bound > kA86MaxKV) {
+        for (int t = 0; t < nt; ++t) {
+            const hipError_t e = launch_attention_x86(b.a[t], n_head, n_head_kv, head_dim, kv_bound, s, 0);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    const int G = n_head / n_head_kv;
+    return head_dim == 128 ? ba86_launch<128>(b, nt, n_head, G, kv_bound, s) : ba86_launch<64>(b, nt, n_head, G, kv_bound, s);
 }
 
 hipError_t launch_attention_x86(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s,

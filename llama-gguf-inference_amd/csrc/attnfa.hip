@@ -34,7 +34,7 @@ namespace llmi {
 namespace {
 
 template <int D, int X86>
-__global__ __launch_bounds__(256) void k_attn_fa(AttnArgs a, int G) {
+__device__ __forceinline__ void attn_fa_body(const AttnArgs& a, int G) {
     extern __shared__ __attribute__((aligned(16))) float fa_lds[];
     float* sc = fa_lds;               // [kFaMaxKV] scores, then vs
     float* msv = fa_lds + kFaMaxKV;   // [kFaMaxKV] ms
@@ -132,8 +132,28 @@ __global__ __launch_bounds__(256) void k_attn_fa(AttnArgs a, int G) {
     const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
     a.out[(size_t)h * D + tid] = h2f(y) * S_inv;
 }
+template <int D, int X86>
+__global__ __launch_bounds__(256) void k_attn_fa(AttnArgs a, int G) { attn_fa_body<D, X86>(a, G); }
+// batched decode: batch slot = blockIdx.y (its own sequence's caches, q, output, position)
+template <int D, int X86>
+__global__ __launch_bounds__(256) void k_battn_fa(BAttnArgs b, int G) { attn_fa_body<D, X86>(b.a[blockIdx.y], G); }
 
 }  // namespace
+
+hipError_t launch_battention_fa(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
+                                hipStream_t s) {
+    const AttnArgs& a = b.a[0];
+    if (nt < 1 || nt > kMaxBatch || n_head_kv <= 0 || n_head % n_head_kv || kv_bound > kFaMaxKV || kv_bound > a.n_ctx ||
+        a.n_ctx % 8)
+        return hipErrorNotSupported;
+    const int G = n_head / n_head_kv, x86 = a.num ? 1 : 0;
+    const size_t lds = (size_t)2 * kFaMaxKV * 4;
+#define LLMI_BFA(D_, X_) \
+    if (head_dim == D_ && x86 == X_) { launch_k(k_battn_fa<D_, X_>, dim3(n_head, nt), dim3(256), lds, s, true, true, b, G); return hipGetLastError(); }
+    LLMI_BFA(128, 0) LLMI_BFA(128, 1) LLMI_BFA(64, 0) LLMI_BFA(64, 1)
+#undef LLMI_BFA
+    return hipErrorNotSupported;
+}
 
 hipError_t launch_attention_fa(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s) {
     if (n_head_kv <= 0 || n_head % n_head_kv || kv_bound > kFaMaxKV || kv_bound > a.n_ctx || a.n_ctx % 8)

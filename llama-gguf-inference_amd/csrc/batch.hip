@@ -275,6 +275,13 @@ __global__ __launch_bounds__(512) void k_battn_pv16(BAttnArgs b, int kvb) {
 // token's results equal its single-sequence decode (k_matvec) and the oracle bit for bit.
 // The padded token rows of the MFMA are zero fragments (bm_load zeroes them; discarded).
 constexpr int kBmW = 8, kBmT = kBmW * 64;
+// chains per (row, token): generic 8 residues + sumf (Q6_K: no mins); x86 (X86 = 1, model
+// numerics LLMI_NUMERICS_X86) the 8 AVX2 lanes + Q4_K's 4 min lanes / Q5_K's summs.  A
+// round buffer holds bm_ns() term slots per (stage, matrix): generic 9, x86 one per chain.
+template <int T, int X86>
+__host__ __device__ constexpr int bm_nc() { return X86 ? (T == T_Q4_K ? 12 : T == T_Q5_K ? 9 : 8) : (T == T_Q6_K ? 8 : 9); }
+template <int T, int X86>
+__host__ __device__ constexpr int bm_ns() { return X86 ? bm_nc<T, X86>() : 9; }
 
 template <int T, int NW>
 struct BmStage {
@@ -314,9 +321,13 @@ __device__ __forceinline__ void bm_load(BmStage<T, NW>& st, const RowPtr (&rp)[N
     if constexpr (T != T_Q6_K) st.bs = n < ntl ? *(const h8*)(abf + pf_abf_off(n, s, grp, S)) : h8{};
 }
 
-// the stage's terms tm[wi][chain][i] (token 4 grp + i, row lane & 15)
-template <int T, int NW>
-__device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[NW][9][4]) {
+// the stage's terms tm[wi][chain][i] (token 4 grp + i, row lane & 15).  X86: the chains'
+// integer sums as floats (the x86 weight planes and activation fragments make residue l's
+// MFMA sum exactly x86 lane l's, as in k_pf_gemm), Q4_K's min lanes from masked sumi MFMAs;
+// the fold multiplies by d_w d_a / -d_a dmin_w itself (dw[wi], dmw[wi] returned)
+template <int T, int NW, int X86 = 0>
+__device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[NW][12][4], float (&dwo)[NW],
+                                         float (&dmwo)[NW]) {
     const int lane = threadIdx.x & 63, grp = lane >> 4;
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) {
@@ -352,16 +363,18 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
                 s6o[2 * k + 1] = s6[2 * k + 1] * h2{(_Float16)1056.f, (_Float16)1056.f};
             }
         }
+        dwo[wi] = dw;
+        dmwo[wi] = dmw;
         float d[4], dm[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            d[i] = dw * st.da[i];
+            d[i] = X86 ? 1.0f : dw * st.da[i];
             dm[i] = dmw * st.da[i];
         }
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
             h8 bf[2];
-            pf_build_b<T>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf);
+            pf_build_b<T, X86>(w, l, slo, shi, slo_o, shi_o, s6, s6o, bf);
             f4 acc = mfma16(st.a[l], bf[0], f4{0.f, 0.f, 0.f, 0.f});
             if constexpr (T == T_Q6_K) {
                 const f4 acc_h = mfma16(st.a[l], bf[1], f4{0.f, 0.f, 0.f, 0.f});
@@ -369,14 +382,27 @@ __device__ __forceinline__ void bm_terms(const BmStage<T, NW>& st, float (&tm)[N
                 for (int i = 0; i < 4; ++i) acc[i] = acc_h[i] * 16.f + acc[i];  // exact (< 2^24)
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) tm[wi][l][i] = d[i] * acc[i];
+            for (int i = 0; i < 4; ++i) tm[wi][l][i] = X86 ? acc[i] : d[i] * acc[i];
         }
-        // sumi = mins . bsum pairs on the MFMA (every product and partial sum an integer
-        // < 2^24: exact, prefill.hip.inc k_pf_quant); the term -(dmin * d_a) * sumi
-        f4 sm{0.f, 0.f, 0.f, 0.f};
-        if constexpr (T != T_Q6_K) sm = mfma16(st.bs, bm, f4{0.f, 0.f, 0.f, 0.f});
+        if constexpr (X86 && T == T_Q4_K) {  // prod[k] = lane group k's slice of the mins . bsum pairs
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tm[wi][8][i] = T != T_Q6_K ? -(dm[i] * sm[i]) : 0.f;
+            for (int k = 0; k < 4; ++k) {
+                const f4 sm = mfma16(st.bs, grp == k ? bm : h8{}, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                for (int i = 0; i < 4; ++i) tm[wi][8 + k][i] = sm[i];
+            }
+        } else if constexpr (X86 && T == T_Q5_K) {
+            const f4 sm = mfma16(st.bs, bm, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tm[wi][8][i] = sm[i];
+        } else if constexpr (!X86) {
+            // sumi = mins . bsum pairs on the MFMA (every product and partial sum an integer
+            // < 2^24: exact, prefill.hip.inc k_pf_quant); the term -(dmin * d_a) * sumi
+            f4 sm{0.f, 0.f, 0.f, 0.f};
+            if constexpr (T != T_Q6_K) sm = mfma16(st.bs, bm, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tm[wi][8][i] = T != T_Q6_K ? -(dm[i] * sm[i]) : 0.f;
+        }
     }
 }
 
@@ -406,8 +432,9 @@ __device__ __forceinline__ void bm_tile(const MVArgs& A, int tile, int& si, int&
 
 // wave 0 of a k_bmm / k_bmd workgroup: the tile's row values from its chain results G and the
 // epilogue per token
-template <int T, int EPI, int NW, int NC>
+template <int T, int EPI, int NW, int NC, int X86 = 0>
 __device__ __forceinline__ void bm_epilogue(const MVArgs& A, const float4* G, int nt, int tile, int si, int row0) {
+    constexpr int NS = bm_ns<T, X86>();
     const int t = threadIdx.x >> 3, n0 = 2 * (threadIdx.x & 7);
     unsigned long long best = 0;
     int seq = 0, pos = 0;
@@ -421,9 +448,18 @@ __device__ __forceinline__ void bm_epilogue(const MVArgs& A, const float4* G, in
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int L = n0 + h + 16 * (t >> 2), i = t & 3;
-                float x = NC == 9 ? Gf[((wi * 9 + 8) * 32 + L) * 4 + i] : 0.f;  // sumf, then + sums[0..7]
+                auto g = [&](int c) { return Gf[((wi * NS + c) * 32 + L) * 4 + i]; };
+                float x;
+                if constexpr (X86) {  // hsum_float_8 of the lanes [+ min lanes (Q4_K) / summs (Q5_K)]
+                    const float t0 = g(0) + g(4), t1 = g(1) + g(5), t2 = g(2) + g(6), t3 = g(3) + g(7);
+                    x = (t0 + t2) + (t1 + t3);
+                    if constexpr (T == T_Q4_K) x = x + ((g(8) + g(10)) + (g(9) + g(11)));
+                    if constexpr (T == T_Q5_K) x = x + g(8);
+                } else {
+                    x = NC == 9 ? g(8) : 0.f;  // sumf, then + sums[0..7]
 #pragma unroll
-                for (int l = 0; l < 8; ++l) x += Gf[((wi * 9 + l) * 32 + L) * 4 + i];
+                    for (int l = 0; l < 8; ++l) x += g(l);
+                }
                 v[wi][h] = x;
             }
         const MVArgs B = token_view(A, t, seq);
@@ -434,10 +470,10 @@ __device__ __forceinline__ void bm_epilogue(const MVArgs& A, const float4* G, in
         ref.vb = 1;
         ref.type = T;
         if constexpr (EPI == EPI_SWIGLU) {
-            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
-            epilogue<EPI, false, MVArgs, true>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
+            epilogue<EPI, false, MVArgs, true, X86>(B, ref, row0 + n0, PairSum{v[0][0], v[NW - 1][0]}, pos, best);
+            epilogue<EPI, false, MVArgs, true, X86>(B, ref, row0 + n0 + 1, PairSum{v[0][1], v[NW - 1][1]}, pos, best);
         } else {
-            epilogue<EPI, false, MVArgs, true>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
+            epilogue<EPI, false, MVArgs, true, X86>(B, ref, ref.ra, PairSum{v[0][0], v[0][1]}, pos, best);
         }
     }
     if constexpr (EPI == EPI_LOGITS) {
@@ -500,7 +536,7 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
         bm_load<T, NW>(nxt, rpn, aq, abf, ad, sn < S ? sn : S - 1, S, nt, A.prio_alt);
         float4* Tm = TmB + (it & 1) * kBuf;
         if (s < S) {
-            float tm[NW][9][4];
+            float tm[NW][12][4], dw_[NW], dmw_[NW];
 #if defined(LLMI_EXPERIMENTS)
             if (A.prio_alt & 4) {  // experiment: no terms (zeros)
 #pragma unroll
@@ -511,7 +547,7 @@ __global__ __launch_bounds__(kBmT) void k_bmm(MVArgs A, const uint8_t* aq, const
                         for (int i = 0; i < 4; ++i) tm[wi][c][i] = cur.da[i] + (float)cur.w[wi].q0[i & 3];
             } else
 #endif
-            bm_terms<T, NW>(cur, tm);
+            bm_terms<T, NW>(cur, tm, dw_, dmw_);
             if (lane < 32) {
 #pragma unroll
                 for (int wi = 0; wi < NW; ++wi)
@@ -626,16 +662,30 @@ __device__ __forceinline__ void bmd_w(BmStage<T, NW>& st, const uint8_t* wb, int
     }
 }
 
-// the persistent tile loop of one k_bmd workgroup: tiles tile0, tile0 + stride, ... < ntiles
-template <int T, int EPI>
+// LDS of a k_bmd workgroup: the round's term slots, the tile's chain results G, (X86) the
+// round's weight scales and activation d, the round's weight buffer
+template <int T, int NW, int X86>
+__host__ __device__ constexpr size_t bmd_lds() {
+    return ((size_t)kBmW * NW * bm_ns<T, X86>() + (size_t)NW * bm_ns<T, X86>()) * 32 * 16 +
+           (X86 ? (size_t)kBmW * NW * 16 * 8 + (size_t)kBmW * 8 * 4 : 0) + bmd_wbytes<T, NW>();
+}
+
+// the persistent tile loop of one k_bmd workgroup: tiles tile0, tile0 + stride, ... < ntiles.
+// X86: the fold runs the x86 fma chains, a = fma(d, term, a) with d = d_w d_a (lanes) or
+// -d_a dmin_w (Q4_K's min lanes, Q5_K's summs), d formed from the round's scales (Dw: per
+// stage, matrix and row) and activation d (Da: per stage and token) exactly as the
+// single-token fold's unit terms form it
+template <int T, int EPI, int X86 = 0>
 __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
                                          int ntiles, int tile0, int stride, uint8_t* smem) {
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
-    constexpr int NC = T == T_Q6_K ? 8 : 9;
-    constexpr int kBuf = kBmW * NW * 9 * 32;        // float4 of a round's terms
+    constexpr int NC = bm_nc<T, X86>(), NS = bm_ns<T, X86>();
+    constexpr int kBuf = kBmW * NW * NS * 32;        // float4 of a round's terms
     float4* Tm = (float4*)smem;
     float4* G = Tm + kBuf;
-    uint8_t* Wb = (uint8_t*)(G + NW * 9 * 32);
+    float2* Dw = (float2*)(G + NW * NS * 32);        // X86: [stage][matrix][row] (d_w, dmin_w)
+    float* Da = (float*)(Dw + (X86 ? kBmW * NW * 16 : 0));  // X86: [stage][token] d_a
+    uint8_t* Wb = (uint8_t*)(Da + (X86 ? kBmW * 8 : 0));
     const int wave = uniform((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const int S = A.cols >> 8, R = (S + kBmW - 1) / kBmW;
     int tile = tile0;
@@ -644,6 +694,7 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
     RowPtr rp[NW];
     bm_tile<T, EPI, NW>(A, tile, si, row0, rp);
     constexpr int NI = NW * NC * 32;
+    static_assert(NI <= 2 * kBmT, "two fold items per thread");
     float4 fs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
     BmStage<T, NW> cur;
     bm_load<T, NW>(cur, rp, aq, abf, ad, wave < S ? wave : S - 1, S, nt, 0, false);
@@ -670,15 +721,22 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
         BmStage<T, NW> nxt;
         bm_load<T, NW>(nxt, rpn, aq, abf, ad, sn < S ? sn : S - 1, S, nt, 0, false);
         if (s < S) {
-            float tm[NW][9][4];
-            bm_terms<T, NW>(cur, tm);
+            float tm[NW][12][4], dw[NW], dmw[NW];
+            bm_terms<T, NW, X86>(cur, tm, dw, dmw);
             if (lane < 32) {
 #pragma unroll
                 for (int wi = 0; wi < NW; ++wi)
 #pragma unroll
                     for (int c = 0; c < NC; ++c)
-                        Tm[((wave * NW + wi) * 9 + c) * 32 + lane] =
+                        Tm[((wave * NW + wi) * NS + c) * 32 + lane] =
                             make_float4(tm[wi][c][0], tm[wi][c][1], tm[wi][c][2], tm[wi][c][3]);
+            }
+            if constexpr (X86) {
+                if (lane < 16)
+#pragma unroll
+                    for (int wi = 0; wi < NW; ++wi) Dw[(wave * NW + wi) * 16 + lane] = make_float2(dw[wi], dmw[wi]);
+                if ((lane & 15) == 0 && lane < 32)
+                    *(float4*)(Da + wave * 8 + 4 * (lane >> 4)) = make_float4(cur.da[0], cur.da[1], cur.da[2], cur.da[3]);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next round's DMA has landed ...
@@ -692,14 +750,27 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
                 const int wi = f / (NC * 32), c = (f / 32) % NC, L = f & 31;
                 float4 a = fs[k];
                 for (int w = 0; w < nv; ++w) {
-                    const float4 v = Tm[((w * NW + wi) * 9 + c) * 32 + L];
-                    a.x += v.x;
-                    a.y += v.y;
-                    a.z += v.z;
-                    a.w += v.w;
+                    const float4 v = Tm[((w * NW + wi) * NS + c) * 32 + L];
+                    if constexpr (X86) {
+                        const float2 sc = Dw[(w * NW + wi) * 16 + (L & 15)];
+                        const float4 da = *(const float4*)(Da + w * 8 + 4 * (L >> 4));
+                        const bool lanes = c < 8;  // the 8 lane chains: d_w d_a; else -d_a dmin_w
+                        const float m = lanes ? sc.x : sc.y;
+                        const float4 dd = lanes ? make_float4(m * da.x, m * da.y, m * da.z, m * da.w)
+                                                : make_float4(-da.x * m, -da.y * m, -da.z * m, -da.w * m);
+                        a.x = __builtin_fmaf(dd.x, v.x, a.x);
+                        a.y = __builtin_fmaf(dd.y, v.y, a.y);
+                        a.z = __builtin_fmaf(dd.z, v.z, a.z);
+                        a.w = __builtin_fmaf(dd.w, v.w, a.w);
+                    } else {
+                        a.x += v.x;
+                        a.y += v.y;
+                        a.z += v.z;
+                        a.w += v.w;
+                    }
                 }
                 if (last) {
-                    G[(wi * 9 + c) * 32 + L] = a;
+                    G[(wi * NS + c) * 32 + L] = a;
                     a = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
                 fs[k] = a;
@@ -707,7 +778,7 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
         }
         if (last) {
             __syncthreads();
-            if (threadIdx.x < 64) bm_epilogue<T, EPI, NW, NC>(A, G, nt, tile, si, row0);
+            if (threadIdx.x < 64) bm_epilogue<T, EPI, NW, NC, X86>(A, G, nt, tile, si, row0);
         }
         if (!has_next) break;
         cur = nxt;
@@ -719,21 +790,21 @@ __device__ __forceinline__ void bmd_body(const MVArgs& A, const uint8_t* aq, con
         for (int wi = 0; wi < NW; ++wi) rp[wi] = rpn[wi];
     }
 }
-template <int T, int EPI>
+template <int T, int EPI, int X86 = 0>
 __global__ __launch_bounds__(kBmT) void k_bmd(MVArgs A, const uint8_t* aq, const uint8_t* abf, const float* ad, int nt,
                                               int ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    bmd_body<T, EPI>(A, aq, abf, ad, nt, ntiles, blockIdx.x, gridDim.x, smem);
+    bmd_body<T, EPI, X86>(A, aq, abf, ad, nt, ntiles, blockIdx.x, gridDim.x, smem);
 }
 // A QKV whose attn_v rows have another type (Llama-3 Q4_K_M: Q6_K in half the layers): both
 // type groups in ONE launch, workgroups [0, w1) on the A1 tiles (type T), the rest on A2's
 // (type T2) -- one launch instead of two, no second resident grid competing for the CUs
-template <int T, int T2>
+template <int T, int T2, int X86 = 0>
 __global__ __launch_bounds__(kBmT) void k_bmd2(MVArgs A1, MVArgs A2, const uint8_t* aq, const uint8_t* abf, const float* ad,
                                                int nt, int ntiles1, int ntiles2, int w1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if ((int)blockIdx.x < w1) bmd_body<T, EPI_QKV>(A1, aq, abf, ad, nt, ntiles1, blockIdx.x, w1, smem);
-    else bmd_body<T2, EPI_QKV>(A2, aq, abf, ad, nt, ntiles2, blockIdx.x - w1, gridDim.x - w1, smem);
+    if ((int)blockIdx.x < w1) bmd_body<T, EPI_QKV, X86>(A1, aq, abf, ad, nt, ntiles1, blockIdx.x, w1, smem);
+    else bmd_body<T2, EPI_QKV, X86>(A2, aq, abf, ad, nt, ntiles2, blockIdx.x - w1, gridDim.x - w1, smem);
 }
 
 // ---- launchers -----------------------------------------------------------------------------
@@ -866,8 +937,18 @@ int bmm_min_tokens() {
     return e ? atoi(e) : 3;
 }
 
+// LLMI_BMM_DMA (A/B): 1 k_bmd (weights through LDS by DMA, default), 0 k_bmm; read per
+// launch (step capture), so tests can run both
+static int bmm_dma() {
+    const char* e = getenv("LLMI_BMM_DMA");
+    return e ? atoi(e) : 1;
+}
+
 bool bmm_ok(const MVArgs& a, int epi) {
     if (!g_bmm_env || a.nseg < 1 || a.cols <= 0 || a.cols % 256) return false;
+    if (a.num && !bmm_dma()) return false;  // the x86 fold is k_bmd's only
+    for (int i = 0; i < a.nseg; ++i)
+        if ((a.seg[i].x86 != 0) != (a.num != 0)) return false;  // the planes' byte order
     const int t = a.seg[0].type;
     if (!(t == T_Q4_K || t == T_Q5_K || t == T_Q6_K)) return false;
     if (epi == EPI_SWIGLU && (a.nseg != 2 || a.seg[0].rows != a.seg[1].rows)) return false;
@@ -899,20 +980,13 @@ static int bmm_cap(const void* k, size_t lds) {
     return cap;
 }
 
-// LLMI_BMM_DMA (A/B): 1 k_bmd (weights through LDS by DMA, default), 0 k_bmm; read per
-// launch (step capture), so tests can run both
-static int bmm_dma() {
-    const char* e = getenv("LLMI_BMM_DMA");
-    return e ? atoi(e) : 1;
-}
 
-template <int T, int EPI>
+template <int T, int EPI, int X86>
 static hipError_t bmm_launch(const MVArgs& a, const void* aq, const void* abf, const float* ad, int nt, hipStream_t s) {
     constexpr int NW = EPI == EPI_SWIGLU ? 2 : 1;
-    const bool dma = bmm_dma() != 0;
-    auto k = dma ? k_bmd<T, EPI> : k_bmm<T, EPI>;
-    const size_t lds = dma ? (size_t)(kBmW + 1) * NW * 9 * 32 * 16 + bmd_wbytes<T, NW>()
-                           : (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
+    const bool dma = X86 || bmm_dma() != 0;
+    auto k = dma ? k_bmd<T, EPI, X86> : k_bmm<T, EPI>;
+    const size_t lds = dma ? bmd_lds<T, NW, X86>() : (size_t)(2 * kBmW + 1) * NW * 9 * 32 * 16;
     // shape / occupancy rejections are hipErrorNotSupported: the caller then runs the two
     // type groups as separate launches (engine.cpp) instead of failing the step
     if (lds > 160 * 1024) return hipErrorNotSupported;
@@ -933,11 +1007,11 @@ static hipError_t bmm_launch(const MVArgs& a, const void* aq, const void* abf, c
     return hipGetLastError();
 }
 
-template <int T, int T2>
+template <int T, int T2, int X86>
 static hipError_t bmm2_launch(const MVArgs& a1, const MVArgs& a2, const void* aq, const void* abf, const float* ad, int nt,
                               hipStream_t s) {
-    auto k = k_bmd2<T, T2>;
-    const size_t lds = (size_t)(kBmW + 1) * 9 * 32 * 16 + std::max(bmd_wbytes<T, 1>(), bmd_wbytes<T2, 1>());
+    auto k = k_bmd2<T, T2, X86>;
+    const size_t lds = std::max(bmd_lds<T, 1, X86>(), bmd_lds<T2, 1, X86>());
     // shape / occupancy rejections are hipErrorNotSupported: the caller then runs the two
     // type groups as separate launches (engine.cpp) instead of failing the step
     if (lds > 160 * 1024) return hipErrorNotSupported;
@@ -966,30 +1040,45 @@ hipError_t launch_bmm_qkv2(const MVArgs& a1, const MVArgs& a2, int nt, const voi
         a1.cols != a2.cols)
         return hipErrorNotSupported;
     const int t1 = a1.seg[0].type, t2 = a2.seg[0].type;
-    if (t1 == T_Q4_K && t2 == T_Q6_K) return bmm2_launch<T_Q4_K, T_Q6_K>(a1, a2, aq, abf, ad, nt, s);
-    if (t1 == T_Q4_K && t2 == T_Q5_K) return bmm2_launch<T_Q4_K, T_Q5_K>(a1, a2, aq, abf, ad, nt, s);
-    if (t1 == T_Q5_K && t2 == T_Q6_K) return bmm2_launch<T_Q5_K, T_Q6_K>(a1, a2, aq, abf, ad, nt, s);
+    if (a1.num != a2.num) return hipErrorNotSupported;
+    if (a1.num) {
+        if (t1 == T_Q4_K && t2 == T_Q6_K) return bmm2_launch<T_Q4_K, T_Q6_K, 1>(a1, a2, aq, abf, ad, nt, s);
+        if (t1 == T_Q4_K && t2 == T_Q5_K) return bmm2_launch<T_Q4_K, T_Q5_K, 1>(a1, a2, aq, abf, ad, nt, s);
+        if (t1 == T_Q5_K && t2 == T_Q6_K) return bmm2_launch<T_Q5_K, T_Q6_K, 1>(a1, a2, aq, abf, ad, nt, s);
+        return hipErrorNotSupported;
+    }
+    if (t1 == T_Q4_K && t2 == T_Q6_K) return bmm2_launch<T_Q4_K, T_Q6_K, 0>(a1, a2, aq, abf, ad, nt, s);
+    if (t1 == T_Q4_K && t2 == T_Q5_K) return bmm2_launch<T_Q4_K, T_Q5_K, 0>(a1, a2, aq, abf, ad, nt, s);
+    if (t1 == T_Q5_K && t2 == T_Q6_K) return bmm2_launch<T_Q5_K, T_Q6_K, 0>(a1, a2, aq, abf, ad, nt, s);
     return hipErrorNotSupported;
 }
 
-template <int T>
+template <int T, int X86>
 static hipError_t bmm_epi(const MVArgs& a, int epi, const void* aq, const void* abf, const float* ad, int nt, hipStream_t s) {
     switch (epi) {
-        case EPI_STORE: return bmm_launch<T, EPI_STORE>(a, aq, abf, ad, nt, s);
-        case EPI_ADD: return bmm_launch<T, EPI_ADD>(a, aq, abf, ad, nt, s);
-        case EPI_QKV: return bmm_launch<T, EPI_QKV>(a, aq, abf, ad, nt, s);
-        case EPI_SWIGLU: return bmm_launch<T, EPI_SWIGLU>(a, aq, abf, ad, nt, s);
-        case EPI_LOGITS: return bmm_launch<T, EPI_LOGITS>(a, aq, abf, ad, nt, s);
+        case EPI_STORE: return bmm_launch<T, EPI_STORE, X86>(a, aq, abf, ad, nt, s);
+        case EPI_ADD: return bmm_launch<T, EPI_ADD, X86>(a, aq, abf, ad, nt, s);
+        case EPI_QKV: return bmm_launch<T, EPI_QKV, X86>(a, aq, abf, ad, nt, s);
+        case EPI_SWIGLU: return bmm_launch<T, EPI_SWIGLU, X86>(a, aq, abf, ad, nt, s);
+        case EPI_LOGITS: return bmm_launch<T, EPI_LOGITS, X86>(a, aq, abf, ad, nt, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t launch_bmm(const MVArgs& a, int epi, int nt, const void* aq, const void* abf, const float* ad, hipStream_t s) {
     if (nt < 1 || nt > kMaxBatch || !bmm_ok(a, epi)) return hipErrorInvalidValue;
+    if (a.num) {
+        switch (a.seg[0].type) {
+            case T_Q4_K: return bmm_epi<T_Q4_K, 1>(a, epi, aq, abf, ad, nt, s);
+            case T_Q5_K: return bmm_epi<T_Q5_K, 1>(a, epi, aq, abf, ad, nt, s);
+            case T_Q6_K: return bmm_epi<T_Q6_K, 1>(a, epi, aq, abf, ad, nt, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (a.seg[0].type) {
-        case T_Q4_K: return bmm_epi<T_Q4_K>(a, epi, aq, abf, ad, nt, s);
-        case T_Q5_K: return bmm_epi<T_Q5_K>(a, epi, aq, abf, ad, nt, s);
-        case T_Q6_K: return bmm_epi<T_Q6_K>(a, epi, aq, abf, ad, nt, s);
+        case T_Q4_K: return bmm_epi<T_Q4_K, 0>(a, epi, aq, abf, ad, nt, s);
+        case T_Q5_K: return bmm_epi<T_Q5_K, 0>(a, epi, aq, abf, ad, nt, s);
+        case T_Q6_K: return bmm_epi<T_Q6_K, 0>(a, epi, aq, abf, ad, nt, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1050,6 +1139,9 @@ static int battn_path(int g, int n_head, int head_dim, int kv_bound, int nt) {
 hipError_t launch_battention(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
                              hipStream_t s) {
     if (nt < 1 || nt > kMaxBatch || n_head_kv <= 0 || n_head % n_head_kv) return hipErrorInvalidValue;
+    // the model's numerics (every slot's): flash attention, x86 association, else generic
+    if (b.a[0].fa) return launch_battention_fa(b, nt, n_head, n_head_kv, head_dim, kv_bound, s);
+    if (b.a[0].num) return launch_battention_x86(b, nt, n_head, n_head_kv, head_dim, kv_bound, s);
     const int g = n_head / n_head_kv;
     const int path = battn_path(g, n_head, head_dim, kv_bound, nt);
     if (path == 6) {

@@ -822,14 +822,16 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     base.tpos = c.btpos; base.tseq = c.btseq; base.kv_stride = c.kv_seq_elems; base.st = c.st0;
     base.num = m.numerics;
     const bool x86 = m.numerics == NUMERICS_X86;
-    // one matvec of the step: k_bmm (matrix cores) after quantizing the nt inputs, where
-    // its segments qualify, else k_mvn (x86 numerics: always k_mvn's x86 form); `quantized`
-    // skips the quantization for a launch that reads the same input as the previous one
+    // one matvec of the step: k_bmd / k_bmm (matrix cores; x86 numerics: k_bmd's x86 fold)
+    // after quantizing the nt inputs, where its segments qualify, else k_mvn (x86: its x86
+    // form); `quantized` skips the quantization for a launch that reads the same input as
+    // the previous one
     bool qkv_quant = false;
     auto bmv = [&](const MVArgs& a, int epi, bool& quantized) -> hipError_t {
-        if (x86 || nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
+        if (nt < bmm_min_tokens() || !bmm_ok(a, epi)) return launch_mvn(a, epi, nt, c.max_blocks, c.stream);
         if (!quantized) {
-            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream);
+            const hipError_t e = launch_pf_quant(a.x, a.x_stride, a.nw, a.eps, a.cols, 0, nt, c.baq, c.babs, c.bad, c.babf,
+                                                 c.stream, x86 ? 1 : 0);
             if (e != hipSuccess) return e;
             quantized = true;
         }
@@ -856,8 +858,8 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
             i = j;
         }
         bool done = false;
-        if (!x86 && ng == 2 && nt >= bmm_min_tokens() && bmm_ok(grp[0], EPI_QKV) && bmm_ok(grp[1], EPI_QKV)) {
-            BC(launch_pf_quant(c.bx, E, grp[0].nw, hp.eps, E, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream));
+        if (ng == 2 && nt >= bmm_min_tokens() && bmm_ok(grp[0], EPI_QKV) && bmm_ok(grp[1], EPI_QKV)) {
+            BC(launch_pf_quant(c.bx, E, grp[0].nw, hp.eps, E, 0, nt, c.baq, c.babs, c.bad, c.babf, c.stream, x86 ? 1 : 0));
             qkv_quant = true;
             const hipError_t e2 = launch_bmm_qkv2(grp[0], grp[1], nt, c.baq, c.babf, c.bad, c.stream);
             if (e2 != hipErrorNotSupported) {
@@ -879,11 +881,8 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
             at.num = m.numerics;
             at.fa = m.fa;
         }
-        if (x86 || m.fa) {  // the x86 / flash-attention kernels, one launch set per slot
-            for (int s = 0; s < nt; ++s) BC(launch_attention(ba.a[s], hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
-        } else {
-            BC(launch_battention(ba, nt, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
-        }
+        // every slot in one launch (generic, x86 and flash-attention kernels alike)
+        BC(launch_battention(ba, nt, hp.n_head, hp.n_head_kv, D, kv_bound, c.stream));
         MVArgs o = base;
         o.seg[0] = seg_of(m, L.wo, 0); o.nseg = 1; o.cols = QD; o.x = c.batt; o.x_stride = QD; o.y = c.bx; o.y_stride = E;
         o.npairs = (E + 1) / 2;

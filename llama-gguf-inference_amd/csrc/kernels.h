@@ -261,6 +261,11 @@ void set_attn_mode(int mode);
 // flash-attention numerics decode attention (attnfa.hip): up to kFaMaxKV positions
 constexpr int kFaMaxKV = 8192;
 hipError_t launch_attention_fa(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t s);
+// the batched step's flash-attention / x86 attention: every batch slot in one launch
+hipError_t launch_battention_fa(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
+                                hipStream_t s);
+hipError_t launch_battention_x86(const BAttnArgs& b, int nt, int n_head, int n_head_kv, int head_dim, int kv_bound,
+                                 hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, int n_head, int n_head_kv, int head_dim, int kv_bound, hipStream_t stream,
                             int mode = -1);
 hipError_t launch_embed(const EmbArgs& a, hipStream_t stream);

@@ -707,18 +707,24 @@ __device__ __forceinline__ void unit_terms_q6m(const UnitW<T_Q6_K>& w, const uin
 // dword, so the integer code is the generic one with l read as the lane; the fold runs
 // the fma chains (d and the lane sums kept apart until the chain's fma).
 // Fold buffer per wave (floats): K-quants S[R][12][Lr] | D[R][2][Lr] (d, -dmin) | G[R][12];
-// Q8_0 S[R][8][CS] | D[R][8 Lr] | G[R][8] with the chain stride CS = x86q_cs(Lr) = 8 Lr + 4
-// (Lr >= 8): fold lane f reads chain f at f CS, so the 16 lanes of a ds_read_b128 group
-// start on 16 different 16-B bank slots (an 8 Lr stride put them all on one: 16-way, and
-// the unit's 64 single-dword stores were 8-way); the largest geometry (Lr = 8, R = 8)
-// takes 4352 + 512 + 64 floats.
+// Q8_0 S[R][8][CS] | D[R][CS] | G[R][8] with the chain (and d-row) stride CS = x86q_cs(Lr)
+// = 8 Lr + 4 (Lr >= 8): fold lane f reads chain f at f CS, so the 16 lanes of a
+// ds_read_b128 group start on 16 different 16-B bank slots (an 8 Lr stride put them all on
+// one: 16-way, and the unit's 64 single-dword stores were 8-way).  The buffer is sized per
+// geometry (fold_stride): the largest (Lr = 8, R = 8) takes 4352 + 544 + 64 floats, and
+// wide rows far less (TinyLlama's ffn_down, Lr = 24: 3544), which keeps two 4-wave
+// workgroups per CU where a fixed 4960 would not.
 // ----------------------------------------------------------------------------------
-constexpr int kFoldF = 9 * 64, kFoldFloats = kFoldF + 9 * 16;
+// generic K-quants: S[R][9][CS] chains at stride CS = kq_cs(Lr) (Lr, or Lr + 4 when Lr / 4 is
+// even, so the stride in 16-B slots is odd and a fold read group's 16 lanes meet 16 slots:
+// Lr = 16 (Llama-3-8B's 4096 columns) had them on 4 slots, 4-way); R 9 CS <= 864.
+__host__ __device__ constexpr int kq_cs(int lr) { return (lr / 4) % 2 == 0 ? lr + 4 : lr; }
+constexpr int kFoldF = 864, kFoldFloats = kFoldF + 9 * 16;
 constexpr int kX86KD = 12 * 64, kX86KG = kX86KD + 2 * 64, kX86KFloats = kX86KG + 12 * 16;
 __host__ __device__ constexpr int x86q_cs(int lr) { return lr >= 8 ? 8 * lr + 4 : 8 * lr; }
 __host__ __device__ constexpr int x86q_d(int R, int lr) { return R * 8 * x86q_cs(lr); }
-__host__ __device__ constexpr int x86q_g(int R, int lr) { return x86q_d(R, lr) + R * 8 * lr; }
-constexpr int kX86QFloats = 4928;
+__host__ __device__ constexpr int x86q_g(int R, int lr) { return x86q_d(R, lr) + R * x86q_cs(lr); }
+constexpr int kX86QFloats = 4960;
 static_assert(x86q_g(8, 8) + 8 * 8 <= kX86QFloats && x86q_g(16, 4) + 8 * 16 <= kX86QFloats &&
                   x86q_g(4, 16) + 8 * 4 <= kX86QFloats && x86q_g(2, 32) + 8 * 2 <= kX86QFloats &&
                   x86q_g(1, 64) + 8 <= kX86QFloats,
@@ -727,6 +733,26 @@ template <int ACT, int X86>
 __host__ __device__ constexpr int fold_floats() { return X86 ? (ACT ? kX86QFloats : kX86KFloats) : kFoldFloats; }
 template <int ACT>
 __host__ __device__ constexpr int x86_chains() { return ACT ? 8 : 12; }
+// floats of one wave's fold buffer at task geometry (R, Lr) -- a multiple of 4 (16-B aligned)
+__host__ __device__ constexpr int fold_stride(int act, int x86, int R, int lr) {
+    return x86 && act ? (x86q_g(R, lr) + 8 * R + 3) & ~3 : x86 ? kX86KFloats : kFoldFloats;
+}
+// the largest fold_stride a launch over `cols` columns can take (mv_geometry's Lr for both
+// epilogue caps, R before any halving)
+__host__ __device__ inline int fold_stride_cols(int act, int x86, int cols) {
+    if (!(x86 && act)) return fold_stride(act, x86, 1, 4);
+    const int U = cols >> 8;
+    int f = 0;
+    for (int lmax = 32; lmax <= 64; lmax += 32) {
+        int lr = ((U < lmax ? U : lmax) + 3) & ~3;
+        lr = lr < 4 ? 4 : lr > lmax ? lmax : lr;
+        int R = 1;
+        while (2 * R * lr <= 64) R *= 2;
+        const int v = fold_stride(act, x86, R, lr);
+        f = v > f ? v : f;
+    }
+    return f;
+}
 
 // upstream hsum_float_8 (AVX: lo128 + hi128, movehl + add, movehdup + add_ss)
 __device__ __forceinline__ float x86_hsum8(const float* a) {
@@ -744,7 +770,7 @@ __device__ __forceinline__ void unit_store_x86(const UnitW<T>& w, const uint8_t*
         // as one 16-B store each (16 stores of 64 terms instead of 64 single dwords)
         const int cs = x86q_cs(lr);
         float* S = F + (size_t)r * 8 * cs + 8 * ul;
-        float* D = F + x86q_d(R, lr) + (size_t)r * 8 * lr + 8 * ul;
+        float* D = F + x86q_d(R, lr) + (size_t)r * cs + 8 * ul;
         float db[8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -926,7 +952,7 @@ __device__ __forceinline__ void fold_sub_x86(float* F, int R, int lr, int n, boo
         float a;
         if constexpr (ACT) {
             const float* s = F + (size_t)(r * 8 + c) * x86q_cs(lr);
-            const float* d = F + x86q_d(R, lr) + (size_t)r * 8 * lr;
+            const float* d = F + x86q_d(R, lr) + (size_t)r * x86q_cs(lr);
             a = chain_batched(8 * n, acc, ChainFma{d, s});
             if (last) F[x86q_g(R, lr) + f] = a;
         } else {
@@ -1008,7 +1034,7 @@ template <int ACT>
 __device__ __forceinline__ void fold_sub(float* F, int R, int lr, int n, bool last, float& acc) {
     constexpr int NC = row_chains<ACT>();
     const int lane = threadIdx.x & 63, nf = R * NC;
-    const int len = ACT ? 8 * n : n, stride = ACT ? q80_rs(lr) : lr;
+    const int len = ACT ? 8 * n : n, stride = ACT ? q80_rs(lr) : kq_cs(lr);
     for (int f = lane; f < nf; f += 64) {
         float a = chain_batched(len, acc, ChainAdd{F + f * stride});
         if (last) {
@@ -1039,9 +1065,10 @@ __device__ __forceinline__ void store_terms(float* F, int r, int ul, int lr, con
         *(float4*)q = make_float4(tm[0], tm[1], tm[2], tm[3]);
         *(float4*)(q + 4) = make_float4(tm[4], tm[5], tm[6], tm[7]);
     } else {
-        float* q = F + r * 9 * lr + ul;
+        const int cs = kq_cs(lr);
+        float* q = F + r * 9 * cs + ul;
 #pragma unroll
-        for (int c = 0; c < 9; ++c) q[c * lr] = tm[c];
+        for (int c = 0; c < 9; ++c) q[c * cs] = tm[c];
     }
 }
 

@@ -24,7 +24,7 @@ namespace llmi {
 constexpr bool kQ6Masked = LLMI_Q6_MASKED != 0;
 // LDS of a k_matvec launch of NW waves whose pipelined types are T / T2
 __host__ inline size_t mv_lds_total(int act, int cols, int nw, int t, int t2, int x86 = 0) {
-    const int ff = x86 ? (act ? fold_floats<1, 1>() : fold_floats<0, 1>()) : kFoldFloats;
+    const int ff = fold_stride_cols(act, x86, cols);
     const size_t base = fold_off(act, cols, nw) + (size_t)nw * ff * 4;
     return base + ((kQ6Masked && !x86 && (t == T_Q6_K || t2 == T_Q6_K)) ? (size_t)(cols >> 8) * kQ6MaskRec : 0);
 }
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(NT) void k_matvec(MVArgs A) {
     const Lds L = carve(smem, ACT, A.cols);
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
-    float* F = (float*)(smem + fold_off(ACT, A.cols, NW)) + wave * fold_floats<ACT, X86>();
+    float* F = (float*)(smem + fold_off(ACT, A.cols, NW)) + wave * fold_stride(ACT, X86, A.rpt, A.lr);
     unsigned long long best;
     if constexpr (T2 == T) {
         // single type: optionally two task ranges, the larger one for the first dispatch
