@@ -2,7 +2,7 @@
 # (profiles/r06/configs), then smoke + the whole GPU suite + the default bench reading the
 # 8B's fresh traffic file (profiles/r06/final)
 set -o pipefail
-O=gpurun_out/r6_final
+O=gpurun_out/${OUT:-r6_final}
 mkdir -p $O
 bash tools/evidence.sh config $O llama3-8b-q4km || exit 1
 cp $O/prof_llama3-8b-q4km/traffic_llama3-8b-q4km.json profiles/r06/ || exit 1

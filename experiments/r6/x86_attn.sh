@@ -11,3 +11,13 @@ for num in x86 generic; do
 done
 timeout -k 10 300 python -u bench.py --preset tinyllama-q8_0 --numerics x86 --no-cpu-baseline --no-c2-full --steps 256 --warmup 16 --batch-seqs '' > $O/bench_tinyllama_x86.json 2> $O/bench_tinyllama_x86.log || { tail $O/bench_tinyllama_x86.log; exit 1; }
 python -c "import json;d=json.load(open('$O/bench_tinyllama_x86.json'));print('tinyllama x86', d['value'], {k:v['us'] for k,v in d['kernels'].items()})"
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bx86 -o run -- python3 -u bench.py --numerics x86 --no-cpu-baseline --no-c2-full --no-other-numerics --steps 16 --warmup 4 --batch-seqs 8 --batch-steps 32 > $O/prof_bx86.log 2>&1 || { tail -20 $O/prof_bx86.log; exit 1; }
+python3 - $O <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/prof_bx86/**/*kernel_stats.csv", recursive=True)[0]
+rows = list(csv.DictReader(open(f)))
+rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+for r in rows[:14]:
+    print(f'{float(r["TotalDurationNs"])/1e6:9.3f} ms {int(r["Calls"]):7d} x {float(r["AverageNs"])/1e3:8.2f} us  {r["Name"][:110]}')
+PY

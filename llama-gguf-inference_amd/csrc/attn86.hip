@@ -180,7 +180,10 @@ __device__ __forceinline__ float a86_quad_reduce(float (&acc)[8]) {
 #endif
 template <int D, int DS, int U>
 __device__ __forceinline__ void a86_h_body(const AttnArgs& a, int n_head, int gq, int kvb, int stop) {
-    constexpr int NT = kA86Threads, NW = NT / 64, VP = DS * kA86MaxKV / 8 / NT, NE = D / 32;
+    // V staging registers sized for this pass class's largest KV bound (U: 128 U positions
+    // per pass up to 512, else up to kA86MaxKV)
+    constexpr int KVMAX = U >= 8 ? kA86MaxKV : 128 * U;
+    constexpr int NT = kA86Threads, NW = NT / 64, VP = (DS * KVMAX / 8 + NT - 1) / NT, NE = D / 32;
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     const int vst = kvb + 8;                                  // V row stride (f16): rows off one bank quad
     float* wl = (float*)sm;                                   // [kvb]: scores, then p
@@ -342,9 +345,11 @@ static hipError_t a86_launch(const AttnArgs& a, int n_head, int hk, int kv_bound
     return hipGetLastError();
 }
 
+// 32-dim slices (half the workgroups of the single-sequence launch: nt heads' worth of
+// workgroups already fill the chip, and each slice recomputes its head's scores)
 template <int D>
 static hipError_t ba86_launch(const BAttnArgs& b, int nt, int n_head, int G, int kv_bound, hipStream_t s) {
-    constexpr int DS = 16;
+    constexpr int DS = 32;
     const size_t lds = (size_t)kv_bound * 4 + (size_t)DS * (kv_bound + 8) * 2;
     const dim3 grid(n_head * (D / DS), nt);
     if (kv_bound <= 128) launch_k(k_ba86_h<D, DS, 1>, grid, dim3(kA86Threads), lds, s, true, true, b, n_head, G, kv_bound);
