@@ -408,6 +408,9 @@ def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tup
     fast = po.set_fast_dots(True)
     ctx_toks = (prompt + list(generated))[: window[0]]
     om = po.OracleModel(path, n_ctx=window[0] + n_tokens + 8, threads=threads)
+    # the weights out of the file's page cache (on the node that wrote the file) into
+    # memory whose rows are first-touched by the threads that read them (NUMA placement)
+    local_bytes = om.localize()
     res = {}
     try:
         t = time.perf_counter()
@@ -443,6 +446,8 @@ def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tup
             "threads_8": {"value": round(res["t8"], 3), "unit": "tokens/s",
                           "achieved_GBps": round(res["t8"] * bpt / 1e9, 2)},
             "dots": "avx2 (x86 kernel association)" if fast else "generic scalar (no AVX2 in this build)",
+            "placement": f"decode matrices ({local_bytes / 1e9:.2f} GB) copied into rows first-touched by their "
+                         f"reading thread of {threads} (oracle or_model_localize)",
             "host_dram_roofline": {"stream_read_GBps": round(host_gbps, 1),
                                    "decode_tok_s_at_roofline": round(host_gbps * 1e9 / bpt, 2)},
             "sample": f"{n_tokens} greedy decode steps at ctx {window[0]}..{window[0] + n_tokens - 1}, the GPU's timed "

@@ -888,6 +888,8 @@ struct or_model {
     uint16_t *kc, *vc;       /* [layer][pos][n_head_kv*head_dim] f16 */
     float *x, *xb, *q, *k, *v, *att, *hb, *hb2, *tmp, *sc;
     float *tap_embd, *tap_final;
+    /* or_model_localize: the decode matrices' anonymous copies */
+    uint8_t** local; int n_local;
 };
 
 static const or_tensor* find_t(const or_model* m, const char* name) {
@@ -1005,8 +1007,77 @@ fail:
     return NULL;
 }
 
+static size_t tensor_bytes(const or_tensor* T) {
+    int64_t n = T->ne[0] * T->ne[1] * T->ne[2] * T->ne[3];
+    return (size_t)(n / or_block_size(T->type)) * or_type_size(T->type);
+}
+
+/* CPU-baseline placement (bench.py cpu_baseline leg; numerics untouched): copy every
+ * matrix the decode step streams out of the file mapping into anonymous memory, each row
+ * written by the OpenMP thread of nth that or_decode's static row loops will give it
+ * (q/k/v and gate/up as the concatenations matvec_multi splits), so under Linux's
+ * first-touch policy a row's pages sit on the NUMA node of the thread that reads them.
+ * The mapping's page cache sits on the node that wrote the file.  Returns bytes copied. */
+static uint8_t* loc_rows(const or_tensor* const* T, int n, int nth, uint8_t** out) {
+    int64_t rows0[4] = {0, 0, 0, 0};
+    size_t rb[3];
+    for (int i = 0; i < n; ++i) {
+        rows0[i + 1] = rows0[i] + T[i]->ne[1];
+        rb[i] = (size_t)(T[i]->ne[0] / or_block_size(T[i]->type)) * or_type_size(T[i]->type);
+        out[i] = aligned_alloc(4096, ((size_t)T[i]->ne[1] * rb[i] + 4095) / 4096 * 4096);
+        if (!out[i]) return NULL;
+    }
+#pragma omp parallel for schedule(static) num_threads(nth > 0 ? nth : 1)
+    for (int64_t g = 0; g < rows0[n]; ++g) {
+        int i = 0;
+        while (g >= rows0[i + 1]) ++i;
+        const int64_t r = g - rows0[i];
+        memcpy(out[i] + (size_t)r * rb[i], (const uint8_t*)T[i]->data + (size_t)r * rb[i], rb[i]);
+    }
+    return out[0];
+}
+int64_t or_model_localize(or_model* m, int nth) {
+    if (m->local) return 0;
+    const int nm = m->n_layer * 7 + 1;
+    m->local = calloc((size_t)nm, sizeof(uint8_t*));
+    if (!m->local) return -1;
+    int k = 0;
+    int64_t bytes = 0;
+    for (int l = 0; l < m->n_layer; ++l) {
+        const or_tensor* const qkv[3] = {m->L[l].wq, m->L[l].wk, m->L[l].wv};
+        const or_tensor* const gu[2] = {m->L[l].wg, m->L[l].wu};
+        const or_tensor* const wo[1] = {m->L[l].wo};
+        const or_tensor* const wd[1] = {m->L[l].wd};
+        const or_tensor* const* sets[4] = {qkv, wo, gu, wd};
+        const int ns[4] = {3, 1, 2, 1};
+        for (int j = 0; j < 4; ++j) {
+            uint8_t* out[3] = {NULL, NULL, NULL};
+            if (!loc_rows(sets[j], ns[j], nth, out)) return -1;
+            for (int i = 0; i < ns[j]; ++i) {
+                m->local[k++] = out[i];
+                ((or_tensor*)sets[j][i])->data = out[i];
+                bytes += (int64_t)tensor_bytes(sets[j][i]);
+            }
+        }
+    }
+    {
+        const or_tensor* const o[1] = {m->output};
+        uint8_t* out[3] = {NULL, NULL, NULL};
+        if (!loc_rows(o, 1, nth, out)) return -1;
+        m->local[k++] = out[0];
+        ((or_tensor*)m->output)->data = out[0];
+        bytes += (int64_t)tensor_bytes(m->output);
+    }
+    m->n_local = k;
+    return bytes;
+}
+
 void or_model_free(or_model* m) {
     if (!m) return;
+    if (m->local) {
+        for (int i = 0; i < m->n_local; ++i) free(m->local[i]);
+        free(m->local);
+    }
     if (m->map) munmap(m->map, m->map_len);
     if (m->fd >= 0) close(m->fd);
     free(m->tensors); free(m->L); free(m->kc); free(m->vc);
@@ -1026,10 +1097,6 @@ void or_kv_clear(or_model* m) {
     memset(m->vc, 0, (size_t)m->n_layer * m->n_ctx * kvd * 2);
 }
 
-static size_t tensor_bytes(const or_tensor* T) {
-    int64_t n = T->ne[0] * T->ne[1] * T->ne[2] * T->ne[3];
-    return (size_t)(n / or_block_size(T->type)) * or_type_size(T->type);
-}
 
 double or_bytes_per_token(const or_model* m, int ctx) {
     double b = 0;

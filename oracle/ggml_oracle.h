@@ -78,6 +78,10 @@ typedef struct or_model or_model;
 /* Opens a GGUF v3 file with its own reader (independent of the product's loader). */
 or_model* or_model_load(const char* path, int n_ctx);
 void or_model_free(or_model* m);
+/* copy the decode matrices into anonymous memory, each row first-touched by the OpenMP
+ * thread (of nth) that reads it in or_decode (NUMA placement for the CPU baseline);
+ * returns the bytes copied, < 0 on allocation failure */
+int64_t or_model_localize(or_model* m, int nth);
 const char* or_last_error(void);
 /* out[0..9] = n_embd, n_layer, n_head, n_head_kv, n_ff, n_vocab, n_rot, n_ctx, head_dim, file_type */
 void or_model_info(const or_model* m, int64_t* out);

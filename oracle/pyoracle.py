@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
         "or_rms_norm_mul": (None, [P, P, P, C.c_int, C.c_float]),
         "or_model_load": (P, [C.c_char_p, C.c_int]),
         "or_model_free": (None, [P]),
+        "or_model_localize": (C.c_int64, [P, C.c_int]),
         "or_last_error": (C.c_char_p, []),
         "or_model_info": (None, [P, P]),
         "or_decode": (C.c_int, [P, C.c_int32, C.c_int32, P, C.c_int]),
@@ -218,6 +219,14 @@ class OracleModel:
         (self.n_embd, self.n_layer, self.n_head, self.n_head_kv, self.n_ff, self.n_vocab,
          self.n_rot, self.n_ctx, self.head_dim, self.file_type) = (int(v) for v in info)
         self.threads = threads or nthreads()
+
+    def localize(self) -> int:
+        """Copy the decode matrices into anonymous memory, each row first-touched by the
+        OpenMP thread (of self.threads) that reads it (NUMA placement; numerics unchanged)."""
+        n = int(lib().or_model_localize(self._h, self.threads))
+        if n < 0:
+            raise RuntimeError("or_model_localize: out of memory")
+        return n
 
     def decode(self, token: int, pos: int, logits: bool = True) -> np.ndarray | None:
         """One decode step; logits=False skips the output head (prompt tokens)."""

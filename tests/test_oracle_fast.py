@@ -50,3 +50,18 @@ def test_fast_dots_match_generic(simd, qt):
     # off again: bit-identical to the generic order
     assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y1), 4) == 0
     assert np.array_equal(y0, y1)
+
+
+def test_localized_weights_decode_identically(tmp_path):
+    """or_model_localize (the CPU baseline's NUMA placement: decode matrices copied into
+    rows first-touched by their reading thread) moves bytes only: logits bit-identical."""
+    import llmi
+
+    p = str(tmp_path / "t.gguf")
+    llmi.write_synthetic_gguf(p, "tiny-mixed", seed=5)
+    a = po.OracleModel(p, n_ctx=64, threads=3)
+    b = po.OracleModel(p, n_ctx=64, threads=3)
+    assert b.localize() > 0 and b.localize() == 0  # once
+    for pos, t in enumerate([1, 7, 42, 300, 5]):
+        assert np.array_equal(a.decode(t, pos), b.decode(t, pos))
+    a.close(), b.close()

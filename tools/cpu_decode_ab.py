@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """CPU-baseline A/B (bench.py's cpu_baseline leg in isolation): the oracle port's AVX2 decode
 of a synthetic preset at the C2 window under the current OpenMP environment; prints tok/s,
-GB/s and the host's streaming-read rate at the same thread count.  Env: PRESET, TH, N."""
+GB/s and the host's streaming-read rate at the same thread count.  Env: PRESET, TH, N,
+LOCAL (1: or_model_localize, the decode matrices in rows first-touched by their thread)."""
 import os
 import sys
 import time
@@ -26,6 +27,9 @@ if not os.path.exists(path):
 po.prefer_simd()
 po.set_fast_dots(True)
 om = po.OracleModel(path, n_ctx=512, threads=th)
+local = os.environ.get("LOCAL", "0") == "1"
+if local:
+    om.localize()
 rng = np.random.default_rng(1)
 toks = [1] + [int(t) for t in rng.integers(3, 100000, 159)]
 om.prefill(toks[:-1], 0)
@@ -39,5 +43,5 @@ for rep in range(2):
     best = max(best, n / (time.perf_counter() - t0))
 bpt = om.bytes_per_token(len(toks) + n)
 env = {k: v for k, v in os.environ.items() if k.startswith(("OMP_", "GOMP_"))}
-print(f"{preset} threads {th} {env}: {best:.2f} tok/s, {best * bpt / 1e9:.1f} GB/s; "
+print(f"{preset} threads {th} local {int(local)} {env}: {best:.2f} tok/s, {best * bpt / 1e9:.1f} GB/s; "
       f"stream {po.host_stream_gbps(1 << 30, 3, th):.1f} GB/s", flush=True)
