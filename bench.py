@@ -445,7 +445,8 @@ def cpu_baseline(path: str, prompt: list[int], generated: list[int], window: tup
             "stream_frac": round(gbps / host_gbps, 4) if host_gbps > 0 else None,
             "threads_8": {"value": round(res["t8"], 3), "unit": "tokens/s",
                           "achieved_GBps": round(res["t8"] * bpt / 1e9, 2)},
-            "dots": "avx2 (x86 kernel association)" if fast else "generic scalar (no AVX2 in this build)",
+            "dots": {2: "avx512bw (the AVX2 kernels at twice the width, 16-lane fp32 block accumulators)",
+                     1: "avx2 (x86 kernel association)"}.get(fast, "generic scalar (no AVX2 in this build)"),
             "placement": f"decode matrices ({local_bytes / 1e9:.2f} GB) copied into rows first-touched by their "
                          f"reading thread of {threads} (oracle or_model_localize)",
             "host_dram_roofline": {"stream_read_GBps": round(host_gbps, 1),

@@ -465,6 +465,7 @@ static float vd_generic_unpacked(int wtype, int n, const RowConst* rcs, const ui
 static int g_fast = 0;
 #if defined(__AVX2__) && defined(__FMA__)
 #include <immintrin.h>
+static inline float fh2f(uint16_t h) { return _cvtsh_ss(h); }  /* exact, = llmi_h2f */
 static inline float hsum8(__m256 v) {
     __m128 a = _mm_add_ps(_mm256_castps256_ps128(v), _mm256_extractf128_ps(v, 1));
     a = _mm_add_ps(a, _mm_movehl_ps(a, a));
@@ -507,13 +508,13 @@ static float fd_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
             const __m256i ph = _mm256_madd_epi16(_mm256_maddubs_epi16(hi, yh), _mm256_set1_epi16(sc[2 * j + 1]));
             sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
         }
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * llmi_h2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * fh2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
         /* upstream's min terms: 4 lanes prod[k] = madd(mins, hadd(bsums)), FMA-accumulated */
         const __m256i q8sums = _mm256_loadu_si256((const __m256i*)y[i].bsums);
         const __m128i q8s = _mm_hadd_epi16(_mm256_castsi256_si128(q8sums), _mm256_extracti128_si256(q8sums, 1));
         const __m128i mins = _mm_cvtepu8_epi16(_mm_loadl_epi64((const __m128i*)mn));
         const __m128i prod = _mm_madd_epi16(mins, q8s);
-        accm4 = _mm_fmadd_ps(_mm_set1_ps(-y[i].d * llmi_h2f(x[i].dmin)), _mm_cvtepi32_ps(prod), accm4);
+        accm4 = _mm_fmadd_ps(_mm_set1_ps(-y[i].d * fh2f(x[i].dmin)), _mm_cvtepi32_ps(prod), accm4);
     }
     accm4 = _mm_add_ps(accm4, _mm_movehl_ps(accm4, accm4));
     accm4 = _mm_add_ss(accm4, _mm_movehdup_ps(accm4));
@@ -541,9 +542,9 @@ static float fd_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
             const __m256i ph = _mm256_madd_epi16(_mm256_maddubs_epi16(hi, yh), _mm256_set1_epi16(sc[2 * j + 1]));
             sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
         }
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * llmi_h2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * fh2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
         /* upstream: one scalar summs += dmin * sum(prod), FMA-contracted (gnu11 build) */
-        summs = fmaf(-y[i].d * llmi_h2f(x[i].dmin), (float)kq_mins_dot(y[i].bsums, mn), summs);
+        summs = fmaf(-y[i].d * fh2f(x[i].dmin), (float)kq_mins_dot(y[i].bsums, mn), summs);
     }
     return hsum8(acc) + summs;
 }
@@ -570,7 +571,7 @@ static float fd_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
                 sumi = _mm256_add_epi32(sumi, _mm256_madd_epi16(p, s));
             }
         }
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * llmi_h2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(y[i].d * fh2f(x[i].d)), _mm256_cvtepi32_ps(sumi), acc);
     }
     return hsum8(acc);
 }
@@ -580,11 +581,137 @@ static float fd_q8_0(int n, const block_q8_0* x, const block_q8_0* y) {
     for (int ib = 0; ib < n / QK8_0; ++ib) {
         const __m256i a = _mm256_loadu_si256((const __m256i*)x[ib].qs), b = _mm256_loadu_si256((const __m256i*)y[ib].qs);
         const __m256i p = _mm256_madd_epi16(_mm256_maddubs_epi16(_mm256_sign_epi8(a, a), _mm256_sign_epi8(b, a)), ones);
-        acc = _mm256_fmadd_ps(_mm256_set1_ps(llmi_h2f(x[ib].d) * llmi_h2f(y[ib].d)), _mm256_cvtepi32_ps(p), acc);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(fh2f(x[ib].d) * fh2f(y[ib].d)), _mm256_cvtepi32_ps(p), acc);
     }
     return hsum8(acc);
 }
-int or_set_fast_dots(int on) { g_fast = on ? 1 : 0; return 1; }
+/* AVX-512BW forms (g_fast == 2; Zen 4/5 and recent Xeon hosts, where a GGML_CPU_ALL_VARIANTS
+ * image also loads its AVX-512 variant): the AVX2 kernels above at twice the width, two
+ * 32-byte groups per instruction, 16 fp32 lanes per block accumulator -- the same integer
+ * sums, a 16-lane fp32 association (timing only, like every fast dot; test_oracle_fast.py).
+ * Compiled by target attribute in the x86-64-v3 build and chosen at run time. */
+#define OR_AVX512 __attribute__((target("avx512f,avx512bw,avx512vl,avx512dq")))
+OR_AVX512 static inline __m512i ld2x256(const void* a, const void* b) {
+    return _mm512_inserti64x4(_mm512_castsi256_si512(_mm256_loadu_si256((const __m256i*)a)),
+                              _mm256_loadu_si256((const __m256i*)b), 1);
+}
+OR_AVX512 static inline __m512i set2x16(int a, int b) {  /* int16 a in the low 256 bits, b in the high */
+    return _mm512_inserti64x4(_mm512_castsi256_si512(_mm256_set1_epi16((short)a)), _mm256_set1_epi16((short)b), 1);
+}
+OR_AVX512 static float fd512_q4_K(int n, const block_q4_K* x, const block_q8_K* y) {
+    const __m512i m4 = _mm512_set1_epi8(0x0F);
+    __m512 acc = _mm512_setzero_ps();
+    __m128 accm4 = _mm_setzero_ps();
+    for (int i = 0; i < n / QK_K; ++i) {
+        uint8_t sc[8], mn[8];
+        scales_mins_k4(x[i].scales, sc, mn);
+        __m512i sumi = _mm512_setzero_si512();
+        for (int jj = 0; jj < 2; ++jj) {  /* 32-byte groups j = 2 jj, 2 jj + 1 */
+            const __m512i qb = _mm512_loadu_si512((const void*)(x[i].qs + 64 * jj));
+            const __m512i lo = _mm512_and_si512(qb, m4), hi = _mm512_and_si512(_mm512_srli_epi16(qb, 4), m4);
+            const int8_t* q8 = y[i].qs + 128 * jj;
+            const __m512i yl = ld2x256(q8, q8 + 64), yh = ld2x256(q8 + 32, q8 + 96);
+            const __m512i pl = _mm512_madd_epi16(_mm512_maddubs_epi16(lo, yl), set2x16(sc[4 * jj], sc[4 * jj + 2]));
+            const __m512i ph = _mm512_madd_epi16(_mm512_maddubs_epi16(hi, yh), set2x16(sc[4 * jj + 1], sc[4 * jj + 3]));
+            sumi = _mm512_add_epi32(sumi, _mm512_add_epi32(pl, ph));
+        }
+        acc = _mm512_fmadd_ps(_mm512_set1_ps(y[i].d * fh2f(x[i].d)), _mm512_cvtepi32_ps(sumi), acc);
+        const __m256i q8sums = _mm256_loadu_si256((const __m256i*)y[i].bsums);
+        const __m128i q8s = _mm_hadd_epi16(_mm256_castsi256_si128(q8sums), _mm256_extracti128_si256(q8sums, 1));
+        const __m128i mins = _mm_cvtepu8_epi16(_mm_loadl_epi64((const __m128i*)mn));
+        accm4 = _mm_fmadd_ps(_mm_set1_ps(-y[i].d * fh2f(x[i].dmin)), _mm_cvtepi32_ps(_mm_madd_epi16(mins, q8s)), accm4);
+    }
+    accm4 = _mm_add_ps(accm4, _mm_movehl_ps(accm4, accm4));
+    accm4 = _mm_add_ss(accm4, _mm_movehdup_ps(accm4));
+    return _mm512_reduce_add_ps(acc) + _mm_cvtss_f32(accm4);
+}
+OR_AVX512 static float fd512_q5_K(int n, const block_q5_K* x, const block_q8_K* y) {
+    const __m512i m4 = _mm512_set1_epi8(0x0F), b16 = _mm512_set1_epi8(0x10);
+    __m512 acc = _mm512_setzero_ps();
+    float summs = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        uint8_t sc[8], mn[8];
+        scales_mins_k4(x[i].scales, sc, mn);
+        const __m512i hb = _mm512_broadcast_i64x4(_mm256_loadu_si256((const __m256i*)x[i].qh));
+        __m512i sumi = _mm512_setzero_si512();
+        for (int jj = 0; jj < 2; ++jj) {
+            const __m512i qb = _mm512_loadu_si512((const void*)(x[i].qs + 64 * jj));
+            const __m512i ml = _mm512_inserti64x4(_mm512_set1_epi8((char)(1 << (4 * jj))), _mm256_set1_epi8((char)(1 << (4 * jj + 2))), 1);
+            const __m512i mh = _mm512_inserti64x4(_mm512_set1_epi8((char)(1 << (4 * jj + 1))), _mm256_set1_epi8((char)(1 << (4 * jj + 3))), 1);
+            const __m512i lo = _mm512_or_si512(_mm512_and_si512(qb, m4),
+                                               _mm512_maskz_mov_epi8(_mm512_test_epi8_mask(hb, ml), b16));
+            const __m512i hi = _mm512_or_si512(_mm512_and_si512(_mm512_srli_epi16(qb, 4), m4),
+                                               _mm512_maskz_mov_epi8(_mm512_test_epi8_mask(hb, mh), b16));
+            const int8_t* q8 = y[i].qs + 128 * jj;
+            const __m512i yl = ld2x256(q8, q8 + 64), yh = ld2x256(q8 + 32, q8 + 96);
+            const __m512i pl = _mm512_madd_epi16(_mm512_maddubs_epi16(lo, yl), set2x16(sc[4 * jj], sc[4 * jj + 2]));
+            const __m512i ph = _mm512_madd_epi16(_mm512_maddubs_epi16(hi, yh), set2x16(sc[4 * jj + 1], sc[4 * jj + 3]));
+            sumi = _mm512_add_epi32(sumi, _mm512_add_epi32(pl, ph));
+        }
+        acc = _mm512_fmadd_ps(_mm512_set1_ps(y[i].d * fh2f(x[i].d)), _mm512_cvtepi32_ps(sumi), acc);
+        summs = fmaf(-y[i].d * fh2f(x[i].dmin), (float)kq_mins_dot(y[i].bsums, mn), summs);
+    }
+    return _mm512_reduce_add_ps(acc) + summs;
+}
+OR_AVX512 static float fd512_q6_K(int n, const block_q6_K* x, const block_q8_K* y) {
+    const __m512i m4 = _mm512_set1_epi8(0x0F), m2 = _mm512_set1_epi8(0x30), k32 = _mm512_set1_epi8(32);
+    /* int16 index vectors: scale s of 16 elements -> 8 int16 lanes each */
+    const __m512i i01 = _mm512_set_epi16(3, 3, 3, 3, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0);
+    const __m512i i23 = _mm512_add_epi16(i01, _mm512_set1_epi16(4));
+    __m512 acc = _mm512_setzero_ps();
+    for (int i = 0; i < n / QK_K; ++i) {
+        __m512i sumi = _mm512_setzero_si512();
+        for (int h = 0; h < 2; ++h) {
+            const __m256i l0 = _mm256_loadu_si256((const __m256i*)(x[i].ql + 64 * h));
+            const __m256i l1 = _mm256_loadu_si256((const __m256i*)(x[i].ql + 64 * h + 32));
+            const __m256i qh = _mm256_loadu_si256((const __m256i*)(x[i].qh + 32 * h));
+            /* (q0 | q1), (q2 | q3): elements 128h + 0..63 and 64..127 */
+            const __m512i L01 = _mm512_inserti64x4(_mm512_castsi256_si512(l0), l1, 1);
+            const __m512i H = _mm512_broadcast_i64x4(qh);
+            const __m512i Hlo = _mm512_inserti64x4(_mm512_castsi256_si512(_mm256_slli_epi16(qh, 4)), _mm256_slli_epi16(qh, 2), 1);
+            const __m512i Hhi = _mm512_inserti64x4(_mm512_castsi256_si512(qh), _mm256_srli_epi16(qh, 2), 1);
+            (void)H;
+            const __m512i q01 = _mm512_or_si512(_mm512_and_si512(L01, m4), _mm512_and_si512(Hlo, m2));
+            const __m512i q23 = _mm512_or_si512(_mm512_and_si512(_mm512_srli_epi16(L01, 4), m4), _mm512_and_si512(Hhi, m2));
+            const __m512i y01 = _mm512_loadu_si512((const void*)(y[i].qs + 128 * h));
+            const __m512i y23 = _mm512_loadu_si512((const void*)(y[i].qs + 128 * h + 64));
+            const __m512i p01 = _mm512_sub_epi16(_mm512_maddubs_epi16(q01, y01), _mm512_maddubs_epi16(k32, y01));
+            const __m512i p23 = _mm512_sub_epi16(_mm512_maddubs_epi16(q23, y23), _mm512_maddubs_epi16(k32, y23));
+            const __m512i s8 = _mm512_broadcast_i32x4(_mm_cvtepi8_epi16(_mm_loadl_epi64((const __m128i*)(x[i].scales + 8 * h))));
+            sumi = _mm512_add_epi32(sumi, _mm512_madd_epi16(p01, _mm512_permutexvar_epi16(i01, s8)));
+            sumi = _mm512_add_epi32(sumi, _mm512_madd_epi16(p23, _mm512_permutexvar_epi16(i23, s8)));
+        }
+        acc = _mm512_fmadd_ps(_mm512_set1_ps(y[i].d * fh2f(x[i].d)), _mm512_cvtepi32_ps(sumi), acc);
+    }
+    return _mm512_reduce_add_ps(acc);
+}
+OR_AVX512 static float fd512_q8_0(int n, const block_q8_0* x, const block_q8_0* y) {
+    __m512 acc = _mm512_setzero_ps();
+    const __m512i ones = _mm512_set1_epi16(1);
+    int ib = 0;
+    for (; ib + 1 < n / QK8_0; ib += 2) {
+        const __m512i a = ld2x256(x[ib].qs, x[ib + 1].qs), b = ld2x256(y[ib].qs, y[ib + 1].qs);
+        const __m512i ua = _mm512_abs_epi8(a);
+        const __m512i sb = _mm512_mask_sub_epi8(b, _mm512_movepi8_mask(a), _mm512_setzero_si512(), b);  /* sign(b, a) */
+        const __m512i p = _mm512_madd_epi16(_mm512_maddubs_epi16(ua, sb), ones);
+        const __m512 d = _mm512_insertf32x8(_mm512_set1_ps(fh2f(x[ib].d) * fh2f(y[ib].d)),
+                                            _mm256_set1_ps(fh2f(x[ib + 1].d) * fh2f(y[ib + 1].d)), 1);
+        acc = _mm512_fmadd_ps(d, _mm512_cvtepi32_ps(p), acc);
+    }
+    float r = _mm512_reduce_add_ps(acc);
+    if (ib < n / QK8_0) r += fd_q8_0(QK8_0, x + ib, y + ib);
+    return r;
+}
+/* 1 = AVX2 dots, 2 = AVX-512BW dots (falls back to 1 on hosts without it) */
+int or_set_fast_dots(int on) {
+    if (on >= 2 && __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512f") &&
+        __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512dq")) {
+        g_fast = 2;
+        return 2;
+    }
+    g_fast = on ? 1 : 0;
+    return on ? 1 : 0;
+}
 #else
 int or_set_fast_dots(int on) { g_fast = 0; (void)on; return 0; }  /* no AVX2 in this build */
 #endif
@@ -760,6 +887,15 @@ float or_vec_dot(int wtype, int n, const void* w, const void* a) {
         }
     }
 #if defined(__AVX2__) && defined(__FMA__)
+    if (g_fast == 2) {
+        switch (wtype) {
+            case OR_Q4_K: return fd512_q4_K(n, w, a);
+            case OR_Q5_K: return fd512_q5_K(n, w, a);
+            case OR_Q6_K: return fd512_q6_K(n, w, a);
+            case OR_Q8_0: return fd512_q8_0(n, w, a);
+            default: break;
+        }
+    }
     if (g_fast) {
         switch (wtype) {
             case OR_Q4_K: return fd_q4_K(n, w, a);

@@ -38,10 +38,12 @@ def build() -> str:
     return LIB
 
 
-def set_fast_dots(on: bool) -> bool:
-    """CPU-baseline timing only: AVX2 dots in the x86 kernels' association (not the
-    generic order the parity checks use).  False if the loaded build has no AVX2."""
-    return bool(lib().or_set_fast_dots(1 if on else 0))
+def set_fast_dots(on) -> int:
+    """CPU-baseline timing only: vectorised dots (not the generic order the parity checks
+    use).  on: True / 2 = the AVX-512BW forms where the host has them, else AVX2; 1 = AVX2.
+    Returns the mode in effect (2 AVX-512BW, 1 AVX2, 0 off / no AVX2 in this build)."""
+    mode = 0 if not on else (1 if on == 1 and on is not True else 2)
+    return int(lib().or_set_fast_dots(mode))
 
 
 # x86 association flags (ggml_oracle.c "x86 association mode"): parity MEASUREMENT only

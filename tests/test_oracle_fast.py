@@ -27,20 +27,24 @@ def simd():
     L.or_set_fast_dots(0)
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["avx2", "avx512bw"])
 @pytest.mark.parametrize("qt", [Q4_K, Q5_K, Q6_K, Q8_0])
-def test_fast_dots_match_generic(simd, qt):
-    if not simd.or_set_fast_dots(1):
-        pytest.skip("oracle build without AVX2")
+def test_fast_dots_match_generic(simd, qt, mode):
+    got = simd.or_set_fast_dots(mode)
     simd.or_set_fast_dots(0)
+    if not got:
+        pytest.skip("oracle build without AVX2")
+    if got != mode:
+        pytest.skip("host without AVX-512BW")
     rng = np.random.default_rng(qt)
-    rows, cols = 64, 4096
+    rows, cols = 64, 4096 + (32 if qt == Q8_0 else 0)  # Q8_0: an odd block count (the 2-block loop's tail)
     w = random_blocks(qt, rows, cols, rng)
     x = rng.standard_normal(cols).astype(np.float32)
     y0 = np.empty(rows, np.float32)
     y1 = np.empty(rows, np.float32)
     P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
     assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y0), 4) == 0
-    assert simd.or_set_fast_dots(1)
+    assert simd.or_set_fast_dots(mode) == mode
     try:
         assert simd.or_matvec(qt, P(w), rows, cols, P(x), P(y1), 4) == 0
     finally:

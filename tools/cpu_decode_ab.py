@@ -2,7 +2,8 @@
 """CPU-baseline A/B (bench.py's cpu_baseline leg in isolation): the oracle port's AVX2 decode
 of a synthetic preset at the C2 window under the current OpenMP environment; prints tok/s,
 GB/s and the host's streaming-read rate at the same thread count.  Env: PRESET, TH, N,
-LOCAL (1: or_model_localize, the decode matrices in rows first-touched by their thread)."""
+LOCAL (1: or_model_localize, the decode matrices in rows first-touched by their thread),
+FAST (1 AVX2 dots, 2 AVX-512BW where the host has them)."""
 import os
 import sys
 import time
@@ -25,7 +26,7 @@ if not os.path.exists(path):
     llmi.write_synthetic_gguf(path + ".tmp", preset, seed=3)
     os.replace(path + ".tmp", path)
 po.prefer_simd()
-po.set_fast_dots(True)
+fast = po.set_fast_dots(int(os.environ.get("FAST", "2")))
 om = po.OracleModel(path, n_ctx=512, threads=th)
 local = os.environ.get("LOCAL", "0") == "1"
 if local:
@@ -43,5 +44,5 @@ for rep in range(2):
     best = max(best, n / (time.perf_counter() - t0))
 bpt = om.bytes_per_token(len(toks) + n)
 env = {k: v for k, v in os.environ.items() if k.startswith(("OMP_", "GOMP_"))}
-print(f"{preset} threads {th} local {int(local)} {env}: {best:.2f} tok/s, {best * bpt / 1e9:.1f} GB/s; "
+print(f"{preset} threads {th} local {int(local)} dots {fast} {env}: {best:.2f} tok/s, {best * bpt / 1e9:.1f} GB/s; "
       f"stream {po.host_stream_gbps(1 << 30, 3, th):.1f} GB/s", flush=True)
