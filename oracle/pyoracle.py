@@ -40,9 +40,10 @@ def build() -> str:
 
 def set_fast_dots(on) -> int:
     """CPU-baseline timing only: vectorised dots (not the generic order the parity checks
-    use).  on: True / 2 = the AVX-512BW forms where the host has them, else AVX2; 1 = AVX2.
-    Returns the mode in effect (2 AVX-512BW, 1 AVX2, 0 off / no AVX2 in this build)."""
-    mode = 0 if not on else (1 if on == 1 and on is not True else 2)
+    use).  on: True / 1 = AVX2 (the baseline's default: faster than the AVX-512BW forms on
+    the GPU boxes' Zen 5 host, profiles/r06/cpu_baseline/avx512_ab.txt); 2 = AVX-512BW where
+    the host has them.  Returns the mode in effect (2, 1, or 0 = off / no AVX2 build)."""
+    mode = 0 if not on else (2 if on == 2 else 1)
     return int(lib().or_set_fast_dots(mode))
 
 

@@ -26,7 +26,7 @@ if not os.path.exists(path):
     llmi.write_synthetic_gguf(path + ".tmp", preset, seed=3)
     os.replace(path + ".tmp", path)
 po.prefer_simd()
-fast = po.set_fast_dots(int(os.environ.get("FAST", "2")))
+fast = po.set_fast_dots(int(os.environ.get("FAST", "1")))
 om = po.OracleModel(path, n_ctx=512, threads=th)
 local = os.environ.get("LOCAL", "0") == "1"
 if local:
