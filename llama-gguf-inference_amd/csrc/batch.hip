@@ -25,6 +25,10 @@ namespace llmi {
 namespace {
 
 constexpr int kBT = 512, kBW = kBT / 64;  // threads / waves per workgroup
+// waves of a k_mvn workgroup that run row tasks: all 8, except for x86 Q8_0 rows, whose
+// fold buffers (up to 19.8 KB per wave, mv_device.h fold_stride) fit the LDS for 4 waves
+// beside the tokens' images; the other 4 waves take part in the prologue only
+__host__ __device__ constexpr int mvn_work_waves(int act, int x86) { return act && x86 ? 4 : kBW; }
 
 __host__ __device__ inline size_t img_bytes(int act, int cols) { return a16(lds_red_off(act, cols)); }
 
@@ -124,8 +128,7 @@ __device__ __forceinline__ MVArgs token_view(const MVArgs& A, int t, int seq) {
 // X86 = 1: the x86 association (model numerics LLMI_NUMERICS_X86; mv_device.h "x86
 // numerics"): x86 q8 images, the lane's per-4-byte-lane integer sums stored as fp32 fma
 // chain terms (unit_store_x86), x86 fold and epilogues -- every token equal to its own
-// single-sequence x86 decode.  K-quants only (the Q8_0 x86 fold buffers of 8 waves do not
-// fit the LDS).
+// single-sequence x86 decode (Q8_0: 4 working waves, mvn_work_waves).
 template <int ACT, bool NORM, int EPI, int T, int NT, int X86 = 0>
 __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -133,11 +136,12 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
     double* red = (double*)(smem + NT * img);
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
-    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * fold_floats<ACT, X86>();
+    constexpr int NWK = mvn_work_waves(ACT, X86);
     const TaskGeo g = task_geo(A);
+    float* F = (float*)(smem + a16(NT * img + (size_t)kMaxBatch * kBW * 8)) + wave * fold_stride(ACT, X86, g.R, g.lr);
     const int S = EPI == EPI_SWIGLU ? 2 * g.nj : g.nj;
     const int r = lane / g.lr, ul = lane - r * g.lr;
-    const int G = gridDim.x * kBW;
+    const int G = gridDim.x * NWK;
     unsigned long long best[NT];  // per token: the lane's LOGITS key
 #pragma unroll
     for (int t = 0; t < NT; ++t) best[t] = 0;
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(kBT) void k_mvn(MVArgs A) {
         tpos[t] = A.tpos ? A.tpos[t] : 0;
         tseq[t] = A.tseq ? A.tseq[t] : 0;
     }
-    int task = blockIdx.x * kBW + wave;
+    int task = wave < NWK ? blockIdx.x * NWK + wave : A.ntasks;  // (the others: prologue only)
     if (task < A.ntasks) {
         int s = 0;
         Sub b = sub_of<EPI>(A, g, task, 0);
@@ -810,11 +814,13 @@ __global__ __launch_bounds__(kBmT) void k_bmd2(MVArgs A1, MVArgs A2, const uint8
 // ---- launchers -----------------------------------------------------------------------------
 size_t mvn_lds_bytes(int act, int cols, int nt, int x86) {
     const size_t fold = x86 ? (act ? (size_t)kX86QFloats : (size_t)kX86KFloats) : (size_t)kFoldFloats;
-    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) + (size_t)kBW * fold * 4;
+    (void)fold;
+    return a16((size_t)nt * img_bytes(act, cols) + (size_t)kMaxBatch * kBW * 8) +
+           (size_t)mvn_work_waves(act, x86) * fold_stride_cols(act, x86, cols) * 4;
 }
 
 template <typename K>
-static int mvn_grid(K kernel, int ntasks, size_t lds, int max_blocks) {
+static int mvn_grid(K kernel, int ntasks, size_t lds, int max_blocks, int nwk) {
     static std::mutex mu;
     static std::map<std::tuple<const void*, size_t, int>, int> cache;
     int dev = 0;
@@ -835,7 +841,7 @@ static int mvn_grid(K kernel, int ntasks, size_t lds, int max_blocks) {
             cache.emplace(key, cap);
         }
     }
-    int blocks = (ntasks + kBW - 1) / kBW;
+    int blocks = (ntasks + nwk - 1) / nwk;
     blocks = std::min(blocks, std::min(cap, max_blocks));
     return std::max(blocks, 1);
 }
@@ -845,7 +851,7 @@ static hipError_t mvn_launch(const MVArgs& a, int max_blocks, hipStream_t s) {
     auto k = k_mvn<ACT, NORM, EPI, T, NT, X86>;
     const size_t lds = mvn_lds_bytes(ACT, a.cols, NT, X86);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const int blocks = mvn_grid(k, a.ntasks, lds, max_blocks);
+    const int blocks = mvn_grid(k, a.ntasks, lds, max_blocks, mvn_work_waves(ACT, X86));
     hipLaunchKernelGGL(k, dim3(blocks), dim3(kBT), lds, s, a);
     return hipGetLastError();
 }
@@ -875,11 +881,12 @@ static hipError_t mvn_epi(const MVArgs& a, int epi, int nt, int mb, hipStream_t 
 }
 
 static hipError_t mvn_type(const MVArgs& a, int epi, int nt, int max_blocks, hipStream_t s) {
-    if (a.num) {  // x86 association: K-quants (mvn_ok_x86)
+    if (a.num) {  // x86 association
         switch (a.seg[0].type) {
             case T_Q4_K: return mvn_epi<0, T_Q4_K, 1>(a, epi, nt, max_blocks, s);
             case T_Q5_K: return mvn_epi<0, T_Q5_K, 1>(a, epi, nt, max_blocks, s);
             case T_Q6_K: return mvn_epi<0, T_Q6_K, 1>(a, epi, nt, max_blocks, s);
+            case T_Q8_0: return mvn_epi<1, T_Q8_0, 1>(a, epi, nt, max_blocks, s);
             default: return hipErrorNotSupported;
         }
     }
@@ -906,7 +913,6 @@ hipError_t launch_mvn(const MVArgs& a0, int epi, int nt, int max_blocks, hipStre
     // images (70B ffn_down: 28672 columns, 32 KB per token) run as several launches of
     // fewer tokens each (each streams the weights again; results per token unchanged).
     const int act = t == T_Q8_0 ? 1 : 0, x86 = a.num ? 1 : 0;
-    if (x86 && act) return hipErrorNotSupported;
     for (int i = 0; i < a.nseg; ++i)
         if ((a.seg[i].x86 != 0) != (x86 != 0)) return hipErrorInvalidValue;  // the planes' byte order
     int group = mvn_pad(nt);

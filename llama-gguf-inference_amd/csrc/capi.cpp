@@ -477,7 +477,7 @@ int32_t llmi_generate_greedy_batch(struct llama_context* ctx, int32_t n, const i
         context_select_seq(c, seqs[0]);
         return llmi_generate_greedy(ctx, first[0], pos0[0], n_gen, out);
     }
-    if (!bstep_supported(*c.m)) {  // no batched step (x86 numerics with Q8_0 weights): one sequence after another
+    if (!bstep_supported(*c.m)) {  // (every numerics has a batched step since round 6; kept for a model that has none)
         for (int k = 0; k < n; ++k) {
             context_select_seq(c, seqs[k]);
             const int32_t r = llmi_generate_greedy(ctx, first[k], pos0[k], n_gen, out + (size_t)k * n_gen);

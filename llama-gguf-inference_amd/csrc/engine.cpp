@@ -905,23 +905,20 @@ static bool bstep_enqueue(Context& c, int nt, const int* seqs, int kv_bound, std
     return true;
 }
 
-// the batched step in this model's numerics: generic (matrix cores from 3 tokens) and
-// flash-attention models; x86 models through k_mvn's x86 form, K-quant weights only (the
-// Q8_0 x86 fold buffers of a workgroup's 8 waves do not fit the LDS)
+// the batched step in this model's numerics: every numerics and weight type (generic and
+// x86 K-quant rows on the matrix cores from 3 tokens, the rest through k_mvn; x86 Q8_0
+// rows with 4 working waves per workgroup, batch.hip mvn_work_waves).  A layer whose
+// ffn_gate and ffn_up differ in type has no batched step in any numerics (bstep_run's
+// error; llama_decode then steps such sequences one at a time)
 bool bstep_supported(const Model& m) {
-    if (m.numerics == NUMERICS_GENERIC) return true;
-    for (const Layer& L : m.layers) {
-        const DevMat* ms[] = {&L.wq, &L.wk, &L.wv, &L.wo, &L.wg, &L.wu, &L.wd};
-        for (const DevMat* d : ms)
-            if (d->type == T_Q8_0) return false;
-    }
-    return m.output.type != T_Q8_0;
+    (void)m;
+    return true;
 }
 
 bool bstep_run(Context& c, int nt, const int* seqs, int max_pos, std::string& err) {
     const HParams& hp = c.m->hp;
     if (nt < 1 || nt > kMaxBatch || c.n_seq < 2) { err = "batched step: 1..8 slots of a context with n_seq_max >= 2"; return false; }
-    if (!bstep_supported(*c.m)) { err = "batched step: x86 numerics with Q8_0 weights decode one sequence per step"; return false; }
+    if (!bstep_supported(*c.m)) { err = "batched step: not supported for this model"; return false; }
     for (const Layer& L : c.m->layers)
         if (L.wg.type != L.wu.type) { err = "batched step: ffn_gate / ffn_up of different types"; return false; }
     if (!balloc(c, err)) return false;

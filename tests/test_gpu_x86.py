@@ -313,9 +313,10 @@ def test_x86_per_op_taps_8b_widths(gpu, synth_dir):
 
 
 def test_x86_batch_api_sequential(gpu, tiny_models):
-    """x86 numerics have no batched step: llmi_generate_greedy_batch runs the sequences
-    one after another, each equal to its own single-sequence generation."""
-    path = tiny_models["tiny-mixed"]
+    """x86 numerics on a model with Q8_0 and K-quant tensors (tiny-mixed-d128: Q8_0
+    attn_output / ffn_down): llmi_generate_greedy_batch (batched steps: k_mvn's x86 forms
+    incl. Q8_0's 4-wave one) equals each sequence's own single-sequence generation."""
+    path = tiny_models["tiny-mixed-d128"]
     m = llmi.Model(path, numerics=llmi.NUMERICS_X86)
     c = llmi.Context(m, n_ctx=128, n_seq=3)
     got = c.generate_greedy_batch([0, 1, 2], [5, 9, 11], [0, 0, 0], 12)
@@ -426,17 +427,18 @@ def test_x86_tinyllama_prefill_vs_oracle(gpu, synth_dir):
 
 
 # ---- batched steps in x86 numerics (k_mvn's x86 form) -----------------------
+@pytest.mark.parametrize("preset", ["llama3-8b-q4km", "tinyllama-q8_0"])
 @pytest.mark.parametrize("numerics", [llmi.NUMERICS_X86, llmi.NUMERICS_X86 | llmi.NUMERICS_FA,
                                       llmi.NUMERICS_FA])
-def test_x86_and_fa_batched_steps_vs_oracle(gpu, synth_dir, numerics):
+def test_x86_and_fa_batched_steps_vs_oracle(gpu, synth_dir, numerics, preset):
     """A K-quant model in x86 (and/or flash-attention) numerics advances 5 sequences per
     llama_decode call through the batched step (k_mvn x86 form / matrix cores, attention per
     slot), each sequence's logits bit-identical to the oracle's decode in the same mode;
     llmi_generate_greedy_batch (which fails rather than falling back) over 8 sequences
     equals each sequence's single decode."""
-    path = str(synth_dir / "llama3-8b-q4km-L2-v32000.gguf")
+    path = str(synth_dir / f"{preset}-L2-v32000.gguf")
     if not os.path.exists(path):
-        llmi.write_synthetic_gguf(path, "llama3-8b-q4km", seed=3, n_layer=2, n_vocab=32000)
+        llmi.write_synthetic_gguf(path, preset, seed=3, n_layer=2, n_vocab=32000)
     flags = (X86 if numerics & llmi.NUMERICS_X86 else 0) | (po.X86_FA if numerics & llmi.NUMERICS_FA else 0)
     rng = np.random.default_rng(41)
     prompts = [[1] + [int(t) for t in rng.integers(3, 30000, int(n))] for n in rng.integers(2, 40, 5)]
