@@ -3,7 +3,7 @@ r5 item 4): decode attention as upstream's CPU flash_attn_ext one
 (online max / sum, f16 V accumulator rescaled on a new maximum, glibc expf), in both dot
 associations, bit-identical to the oracle's OR_X86_FA mode (oracle/ggml_oracle.c
 attn_head_fa).  The matvecs keep their association (generic or x86); prompts run as
-decode steps (no batched prefill in this mode); batched steps run the FA attention per slot.
+decode steps (no batched prefill in this mode); batched steps run every slot's FA attention in one launch.
 
 - every quant type and both head dims (tiny presets): 40 steps bit-identical, and
   different from the non-flash attention of the same association;
@@ -102,7 +102,7 @@ def test_fa_order_trajectory(gpu, synth_dir, preset, n_prompt, n_gen, assoc):
 
 def test_fa_batched_equals_single(gpu, tiny_models):
     """A flash-attention context with n_seq_max >= 2 advances its sequences through batched
-    steps (matvecs batched, the FA attention per slot): each equals its own single-sequence
+    steps (matvecs batched, every slot's FA attention in one launch): each equals its own single-sequence
     decode (and that one equals the oracle: test_fa_tiny_decode_vs_oracle)."""
     path = tiny_models["tiny-mixed-d128"]
     m = llmi.Model(path, numerics=llmi.NUMERICS_FA)
