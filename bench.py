@@ -63,8 +63,8 @@ def parse(argv=None):
                     help="committed rocprof evidence: traffic_<preset>.json (FETCH_SIZE pass, rocprof us)")
     ap.add_argument("--experiment", action="store_true", help="allow LLMI_EXP_* knobs (line marked as an experiment)")
     ap.add_argument("--numerics", choices=("generic", "x86"), default="generic",
-                    help="fp32 association of every kernel (DESIGN.md §5): ggml's generic order, or upstream's "
-                         "x86 AVX2 build (the reference's NGL=0 path)")
+                    help="fp32 association of every kernel (DESIGN.md §5): ggml's generic order, or the oracle's "
+                         "model of upstream's x86 AVX2 association (match with the reference's CPU image unpinned)")
     ap.add_argument("--no-other-numerics", action="store_true",
                     help="skip the leg that times the same window in the other numerics mode")
     return ap.parse_args(argv)
